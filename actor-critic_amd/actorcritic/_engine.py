@@ -1,0 +1,251 @@
+"""Device-resident state of the Nature-CNN actor-critic on one GPU.
+
+One flat fp32 parameter vector in the C-ABI layout (include/acmi.h: each layer's
+homogeneous [W; b] block is one contiguous slice), activation buffers keyed by batch
+size, and the update workspaces.  Every arithmetic call goes through libacmi.so.
+"""
+
+import ctypes
+
+import numpy as np
+import torch
+
+from actorcritic import _lib
+
+OBS_SHAPE = (84, 84, 4)
+OBS_BYTES = 84 * 84 * 4
+
+
+def _roundup4(x):
+    return (x + 3) // 4 * 4
+
+
+def _orthogonal(shape, gain, rng):
+    """tf.orthogonal_initializer semantics (envs/atari/model.py:132-135)."""
+    rows = int(np.prod(shape[:-1]))
+    cols = shape[-1]
+    a = rng.standard_normal((max(rows, cols), min(rows, cols)))
+    q, r = np.linalg.qr(a)
+    q = q * np.sign(np.diag(r))
+    if rows < cols:
+        q = q.T
+    return (gain * q[:rows, :cols]).reshape(shape)
+
+
+class Layout(object):
+    def __init__(self, A, C3):
+        lib = _lib.load()
+        self.A, self.C3 = A, C3
+        self.nparams = int(lib.acmi_param_count(A, C3))
+        if self.nparams <= 0:
+            raise ValueError('unsupported model: num_actions={} conv3_filters={}'.format(A, C3))
+        off = (ctypes.c_int64 * 12)()
+        _lib.call('acmi_param_offsets', A, C3, off)
+        self.offsets = list(off)
+        din = (ctypes.c_int64 * 6)()
+        dout = (ctypes.c_int64 * 6)()
+        so = (ctypes.c_int64 * 11)()
+        tot = ctypes.c_int64()
+        _lib.call('acmi_kfac_layout', A, C3, din, dout, so, ctypes.byref(tot))
+        self.din, self.dout, self.stat_off, self.stat_total = list(din), list(dout), list(so), tot.value
+        self.inv_total = int(lib.acmi_kfac_inverse_floats(A, C3))
+        self.shapes = [(8, 8, 4, 32), (32,), (4, 4, 32, 64), (64,), (3, 3, 64, C3), (C3,), (49 * C3, 512), (512,),
+                       (512, A), (A,), (512, 1), (1,)]
+        self.names = ['conv1', 'conv2', 'conv3', 'fc4', 'fc_policy', 'fc_baseline']
+
+    def init_params(self, seed=0):
+        """Orthogonal init with gains sqrt(2) / 0.01 / 1.0 and zero biases."""
+        rng = np.random.default_rng(seed)
+        gains = [np.sqrt(2.0)] * 4 + [0.01, 1.0]
+        parts = []
+        for l in range(6):
+            parts.append(_orthogonal(self.shapes[2 * l], gains[l], rng).ravel())
+            parts.append(np.zeros(int(np.prod(self.shapes[2 * l + 1]))))
+        return np.concatenate(parts).astype(np.float32)
+
+    def split(self, flat):
+        ends = self.offsets[1:] + [self.nparams]
+        return [flat[o:e].reshape(s) for o, e, s in zip(self.offsets, ends, self.shapes)]
+
+
+class Activations(object):
+    """a1..a4, logits, value for a batch of B images (row-major, env-major)."""
+
+    def __init__(self, B, layout, device):
+        z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=device)
+        self.B = B
+        self.a1 = z(B, 20, 20, 32)
+        self.a2 = z(B, 9, 9, 64)
+        self.a3 = z(B, 7, 7, layout.C3)
+        self.a4 = z(B, 512)
+        self.logits = z(B, layout.A)
+        self.value = z(B)
+        self.struct = self.view(0, 1)
+
+    def view(self, row, stride):
+        """Acts struct whose batch row b is image row + b*stride (rollout step view)."""
+        el = lambda t, per: t.data_ptr() + 4 * row * per
+        A = self.logits.shape[1]
+        return _lib.Acts(el(self.a1, 400 * 32), el(self.a2, 81 * 64), el(self.a3, self.a3[0].numel()),
+                         el(self.a4, 512), el(self.logits, A), el(self.value, 1), A)
+
+
+class UpdateState(object):
+    """Workspaces of one update over M = N*T rows.
+
+    ``red`` is the one buffer a data-parallel update all-reduces:
+    [grads (nparams) | loss scalars (4) | factor stats (A factors, then G factors)].
+    """
+
+    def __init__(self, eng, M):
+        L = eng.layout
+        dev = eng.device
+        z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)
+        n, S = L.nparams, L.stat_total
+        self.M = M
+        self.red = z(n + 4 + S)
+        self.grads = self.red[:n]
+        self.loss = self.red[n:n + 4]
+        # acmi_backward writes the A part and acmi_kfac_output_stats the G part of one
+        # stats vector laid out like the factors (acmi_kfac_layout)
+        self.stats = self.red[n + 4:]
+        self.astat = self.stats
+        self.gstat = self.stats
+        self.n_grad_red = n + 4
+        self.targets = z(M)
+        self.adv = z(M)
+        self.dhead = z(M, eng.ldh)
+        self.d1 = z(M, 20, 20, 32)
+        self.d2 = z(M, 9, 9, 64)
+        self.d3 = z(M, 7, 7, L.C3)
+        self.d4 = z(M, 512)
+        self.bwd_ws = z(int(eng.lib.acmi_backward_ws_floats(M, L.A, L.C3)))
+        self.loss_ws = z(int(eng.lib.acmi_a2c_loss_ws_floats(M)))
+        self.bwd = _lib.Bwd(self.d1.data_ptr(), self.d2.data_ptr(), self.d3.data_ptr(), self.d4.data_ptr(),
+                            self.dhead.data_ptr(), eng.ldh)
+        self.actions = None
+        self.fwd = None
+
+
+class NetEngine(object):
+    """Parameters + kernels of one AtariModel on one device."""
+
+    def __init__(self, num_actions, conv3_filters, device=None, seed=0, params=None):
+        _lib.require_gpu()
+        self.lib = _lib.load()
+        self.device = torch.device(device) if device is not None else torch.device('cuda',
+                                                                                    torch.cuda.current_device())
+        self.layout = Layout(num_actions, conv3_filters)
+        self.A, self.C3 = num_actions, conv3_filters
+        init = self.layout.init_params(seed) if params is None else np.asarray(params, np.float32)
+        self.params = torch.from_numpy(init).to(self.device)
+        from actorcritic import parallel
+        self.rank = parallel.rank()
+        self.world_size = parallel.world_size()
+        if self.world_size > 1:  # identical initial parameters on every rank
+            parallel.broadcast_(self.params)
+        self.version = 0  # bumped by every parameter update (activation-cache key)
+        self.ldh = max(8, _roundup4(num_actions + 1))
+        self._acts = {}
+        self._updates = {}
+        self._rollout_cache = None
+        self._bad_rows = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.sample_counter = 0
+
+    # -- update plumbing -------------------------------------------------------
+    def update_state(self, M):
+        if M not in self._updates:
+            self._updates[M] = UpdateState(self, M)
+        return self._updates[M]
+
+    def bump_version(self):
+        self.version += 1
+
+    def register_rollout(self, obs, fwd_out):
+        """Marks `obs` ([N,T,84,84,4] device buffer) as already forwarded with the current
+        parameters: the update re-uses the rollout activations instead of recomputing the
+        tower on identical (params, obs) (DESIGN.md §Rollout/update fusion)."""
+        self._rollout_cache = (obs.data_ptr(), tuple(obs.shape), self.version, fwd_out)
+
+    def lookup_rollout(self, x):
+        c = self._rollout_cache
+        if c is None or not isinstance(x, torch.Tensor) or not x.is_cuda:
+            return None
+        if x.data_ptr() == c[0] and tuple(x.shape) == c[1] and c[2] == self.version:
+            return c[3]
+        return None
+
+    def backward(self, fwd, st, with_stats):
+        net = self.net()
+        _lib.call('acmi_backward', ctypes.byref(net), ctypes.c_void_p(fwd.obs.data_ptr()), OBS_BYTES, fwd.M,
+                  ctypes.byref(fwd.acts.struct), ctypes.byref(st.bwd), _lib.ptr(st.grads),
+                  _lib.ptr(st.astat) if with_stats else None, _lib.ptr(st.bwd_ws), self.stream())
+
+    def output_stats(self, fwd, st, seed, counter):
+        net = self.net()
+        _lib.call('acmi_kfac_output_stats', ctypes.byref(net), fwd.M, ctypes.byref(fwd.acts.struct),
+                  ctypes.byref(st.bwd), seed, self.rank, counter, _lib.ptr(st.gstat), _lib.ptr(st.bwd_ws),
+                  self.stream())
+
+    def allreduce(self, st, with_stats):
+        """Sums [grads | losses (| factor stats)] over ranks (RCCL); the 1/world scale is
+        folded into the loss gradient and the factor EMA."""
+        if self.world_size > 1:
+            from actorcritic import parallel
+            k = st.red.numel() if with_stats else st.n_grad_red
+            parallel.allreduce_sum_(st.red[:k])
+
+    # -- plumbing ------------------------------------------------------------
+    def net(self):
+        return _lib.Net(self.A, self.C3, self.params.data_ptr())
+
+    def activations(self, B, key='default'):
+        k = (key, B)
+        if k not in self._acts:
+            self._acts[k] = Activations(B, self.layout, self.device)
+        return self._acts[k]
+
+    def stream(self):
+        return _lib.stream_handle(self.device)
+
+    # -- ops -----------------------------------------------------------------
+    def forward(self, obs_ptr, B, acts_struct, want_value=True, img_stride=OBS_BYTES, act_stride=1):
+        net = self.net()
+        _lib.call('acmi_forward_strided', ctypes.byref(net), ctypes.c_void_p(obs_ptr), img_stride, B,
+                  ctypes.byref(acts_struct), 1 if want_value else 0, act_stride, self.stream())
+
+    def forward_obs(self, obs, key='default'):
+        """obs: uint8 device tensor [B, 84, 84, 4] (contiguous)."""
+        obs = _as_obs(obs, self.device)
+        B = obs.shape[0]
+        acts = self.activations(B, key)
+        self.forward(obs.data_ptr(), B, acts.struct)
+        return acts, obs
+
+    def sample(self, logits, B, out, mode=False, seed=0, stream_id=0, uniforms=None, ld=None):
+        _lib.call('acmi_sample_actions', ctypes.c_void_p(logits.data_ptr()), ld or self.A, B, self.A, seed,
+                  stream_id, self.sample_counter, _lib.ptr(uniforms), 1 if mode else 0,
+                  ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(self._bad_rows.data_ptr()), self.stream())
+        self.sample_counter += 1
+
+    def check_bad_rows(self):
+        """Raises like the reference's out-of-range label error if any logits were NaN."""
+        bad = int(self._bad_rows.item())
+        if bad:
+            self._bad_rows.zero_()
+            raise FloatingPointError('{} policy rows had non-finite logits (reference: InvalidArgumentError '
+                                     '"Received a label value ... outside the valid range", README.md:53)'
+                                     .format(bad))
+
+
+def _as_obs(obs, device):
+    if isinstance(obs, torch.Tensor):
+        t = obs
+    else:
+        t = torch.from_numpy(np.asarray(obs, dtype=np.uint8))
+    if t.dtype != torch.uint8:
+        raise TypeError('observations must be uint8 (model.py:172-186 placeholder dtype)')
+    t = t.reshape(-1, *OBS_SHAPE)
+    if t.device != device:
+        t = t.to(device, non_blocking=True)
+    return t.contiguous()

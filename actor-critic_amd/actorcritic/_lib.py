@@ -1,0 +1,142 @@
+"""ctypes binding of libacmi.so (the C-ABI in include/acmi.h).
+
+The library is the product path: there is no CPU or PyTorch fallback.  If the
+shared object is missing or fails to load, every entry point raises.
+"""
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), 'libacmi.so')
+
+c_int = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_u32 = ctypes.c_uint32
+c_float = ctypes.c_float
+c_vp = ctypes.c_void_p
+
+
+class AcmiError(RuntimeError):
+    """A libacmi entry point returned a non-zero status."""
+
+
+class Net(ctypes.Structure):
+    _fields_ = [('num_actions', c_int), ('conv3_filters', c_int), ('params', c_vp)]
+
+
+class Acts(ctypes.Structure):
+    _fields_ = [('a1', c_vp), ('a2', c_vp), ('a3', c_vp), ('a4', c_vp),
+                ('logits', c_vp), ('value', c_vp), ('ld_logits', c_int)]
+
+
+class Bwd(ctypes.Structure):
+    _fields_ = [('d1', c_vp), ('d2', c_vp), ('d3', c_vp), ('d4', c_vp),
+                ('dhead', c_vp), ('ldh', c_int)]
+
+
+class EnvState(ctypes.Structure):
+    _fields_ = [('episode', c_vp), ('step', c_vp), ('length', c_vp), ('total', c_vp), ('done', c_vp)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    'acmi_last_error': (ctypes.c_char_p, []),
+    'acmi_abi_version': (c_int, []),
+    'acmi_param_count': (c_i64, [c_int, c_int]),
+    'acmi_param_offsets': (c_int, [c_int, c_int, ctypes.POINTER(c_i64)]),
+    'acmi_kfac_layout': (c_int, [c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
+                                 ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
+    'acmi_forward': (c_int, [ctypes.POINTER(Net), c_vp, c_i64, c_int, ctypes.POINTER(Acts), c_int, c_vp]),
+    'acmi_forward_strided': (c_int, [ctypes.POINTER(Net), c_vp, c_i64, c_int, ctypes.POINTER(Acts), c_int,
+                                     c_i64, c_vp]),
+    'acmi_sample_actions': (c_int, [c_vp, c_int, c_int, c_int, c_u32, c_u32, c_u32, c_vp, c_int, c_vp,
+                                    c_vp, c_vp]),
+    'acmi_categorical': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    'acmi_returns': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'acmi_a2c_loss_ws_floats': (c_i64, [c_int]),
+    'acmi_a2c_loss': (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_float, c_float,
+                              c_vp, c_int, c_vp, c_vp, c_vp]),
+    'acmi_backward_ws_floats': (c_i64, [c_int, c_int, c_int]),
+    'acmi_backward': (c_int, [ctypes.POINTER(Net), c_vp, c_i64, c_int, ctypes.POINTER(Acts),
+                              ctypes.POINTER(Bwd), c_vp, c_vp, c_vp, c_vp]),
+    'acmi_kfac_output_stats': (c_int, [ctypes.POINTER(Net), c_int, ctypes.POINTER(Acts), ctypes.POINTER(Bwd),
+                                       c_u32, c_u32, c_u32, c_vp, c_vp, c_vp]),
+    'acmi_kfac_ema': (c_int, [c_vp, c_vp, c_vp, c_i64, c_float, c_float, c_float, c_vp]),
+    'acmi_kfac_inverse_floats': (c_i64, [c_int, c_int]),
+    'acmi_kfac_inverse_ws_doubles': (c_i64, [c_int, c_int]),
+    'acmi_kfac_inverse': (c_int, [c_int, c_int, c_vp, c_float, c_int, c_vp, c_vp, c_vp]),
+    'acmi_kfac_eig_ws_doubles': (c_i64, [c_int, c_int]),
+    'acmi_kfac_eigvals': (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    'acmi_kfac_step_ws_floats': (c_i64, [c_int, c_int]),
+    'acmi_kfac_step': (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_float, c_float, c_float, c_vp, c_vp,
+                               c_vp, c_vp]),
+    'acmi_opt_ws_floats': (c_i64, [c_i64]),
+    'acmi_momentum_apply': (c_int, [c_vp, c_vp, c_vp, c_i64, c_float, c_float, c_float, c_vp, c_vp, c_vp]),
+    'acmi_rmsprop_apply': (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_float, c_float, c_float, c_float, c_float,
+                                   c_vp, c_vp, c_vp]),
+    'acmi_env_reset': (c_int, [ctypes.POINTER(EnvState), c_int, c_int, c_u32, c_vp, c_i64, c_vp]),
+    'acmi_env_step': (c_int, [ctypes.POINTER(EnvState), c_int, c_int, c_u32, c_vp, c_vp, c_i64, c_vp, c_i64,
+                              c_vp, c_vp, c_vp, c_i64, c_vp]),
+    'acmi_gemm_f32': (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
+    'acmi_prof_enable': (c_int, [c_int, c_int]),
+    'acmi_prof_collect': (c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int)]),
+}
+
+PROF_CONV1_WGRAD = 1
+PROF_CONV2_WGRAD = 2
+PROF_CONV1_FWD = 3
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def load():
+    """Loads libacmi.so once; raises ImportError if it is missing (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError('libacmi.so not found at {} - build it with `python __graft_entry__.py build` '
+                              '(hipcc --offload-arch=gfx950); there is no CPU fallback'.format(LIB_PATH))
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.acmi_abi_version() != 1:
+            raise ImportError('libacmi ABI mismatch')
+        _lib = lib
+    return _lib
+
+
+def check(status, what=''):
+    if status != 0:
+        msg = load().acmi_last_error().decode(errors='replace')
+        raise AcmiError('{} failed ({}): {}'.format(what, status, msg))
+
+
+def call(name, *args):
+    """Calls a status-returning entry point and raises AcmiError on failure."""
+    check(getattr(load(), name)(*args), name)
+
+
+def ptr(t):
+    """Device (or host) pointer of a contiguous tensor, or None."""
+    if t is None:
+        return None
+    assert t.is_contiguous(), 'libacmi needs contiguous buffers'
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    """hipStream_t of torch's current stream (graph-capture friendly)."""
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError('actorcritic (MI355X) needs a ROCm GPU: torch.cuda.is_available() is False; '
+                           'there is no CPU fallback for the hot path')

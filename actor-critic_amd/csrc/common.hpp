@@ -1,0 +1,87 @@
+// Shared device/host helpers for libacmi (MI355X / gfx950 only).
+//
+// Everything here is stream-ordered and allocation-free: entry points take
+// caller-owned device buffers and a hipStream_t, never synchronise, and report
+// errors through an int status + acmi_last_error() (see include/acmi.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/acmi.h"
+
+namespace acmi {
+
+// ---------------------------------------------------------------------------
+// error reporting (host)
+// ---------------------------------------------------------------------------
+void set_error(const char* fmt, ...);
+
+#define ACMI_REQUIRE(cond, code, ...)        \
+  do {                                       \
+    if (!(cond)) {                           \
+      ::acmi::set_error(__VA_ARGS__);        \
+      return (code);                         \
+    }                                        \
+  } while (0)
+
+#define ACMI_LAUNCH_CHECK(what)                                              \
+  do {                                                                       \
+    hipError_t e_ = hipGetLastError();                                       \
+    if (e_ != hipSuccess) {                                                  \
+      ::acmi::set_error("%s: HIP launch failed: %s", what,                   \
+                        hipGetErrorString(e_));                              \
+      return ACMI_ERR_HIP;                                                   \
+    }                                                                        \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// counter-based hashing (bit-identical restatement in oracle/oracle.py:mix32)
+// lowbias32 finaliser (C. Wellons); all arithmetic mod 2^32.
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+
+// key of a 4-field counter; the fields are folded one at a time
+__host__ __device__ __forceinline__ uint32_t key4(uint32_t a, uint32_t b,
+                                                 uint32_t c, uint32_t d) {
+  uint32_t h = mix32(a ^ 0x9e3779b9U);
+  h = mix32(h ^ b);
+  h = mix32(h ^ c);
+  h = mix32(h ^ d);
+  return h;
+}
+
+// uniform in [0, 1) with 24 random bits, exactly representable in f32
+__host__ __device__ __forceinline__ float u01(uint32_t h) {
+  return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
+// ---------------------------------------------------------------------------
+// wave helpers (wave64)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace acmi

@@ -1,0 +1,672 @@
+// K-FAC on gfx950: running factors (EMA with zero-debias), pi-adjusted
+// damped inverses in fp64 (batched block Gauss-Jordan), fp64 one-sided
+// Jacobi eigenvalues, natural-gradient preconditioning with the trust-region
+// coefficient computed on the device, and the momentum update.
+//
+// Reference: kfac_utils.py:38-53 (schedule + apply), a2c_acktr.py:233-247
+// (hyper-parameters), third-party tensorflow/kfac (un-vendored, unpinned:
+// conventions restated in DESIGN.md §K-FAC and oracle/oracle.py).
+#include <math.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "gemm.hpp"
+
+namespace acmi {
+
+struct Layout;
+bool get_layout(int A, int C3, Layout* L);
+
+// mirror of net.hip's Layout (kept in sync through acmi_kfac_layout)
+struct KLayout {
+  long long din[6], dout[6], stat_off[11], stat_total;
+  long long poff[12];  // param offsets
+  long long nparams;
+  long long inv_off[12];  // Ainv_l at [2l], Ginv_l at [2l+1]
+  long long inv_total;
+};
+
+static bool klayout(int A, int C3, KLayout* K) {
+  int64_t din[6], dout[6], so[11], tot, off[12];
+  if (acmi_kfac_layout(A, C3, din, dout, so, &tot) != ACMI_OK) return false;
+  if (acmi_param_offsets(A, C3, off) != ACMI_OK) return false;
+  for (int l = 0; l < 6; ++l) {
+    K->din[l] = din[l];
+    K->dout[l] = dout[l];
+  }
+  for (int f = 0; f < 11; ++f) K->stat_off[f] = so[f];
+  K->stat_total = tot;
+  for (int i = 0; i < 12; ++i) K->poff[i] = off[i];
+  K->nparams = acmi_param_count(A, C3);
+  long long o = 0;
+  for (int l = 0; l < 6; ++l) {
+    K->inv_off[2 * l] = o;
+    o += K->din[l] * K->din[l];
+    K->inv_off[2 * l + 1] = o;
+    o += K->dout[l] * K->dout[l];
+  }
+  K->inv_total = o;
+  return true;
+}
+
+static const int CONV_LOCATIONS[6] = {400, 81, 49, 1, 1, 1};
+
+// ---------------------------------------------------------------------------
+// EMA
+// ---------------------------------------------------------------------------
+__global__ void ema_kernel(float* biased, float* fac, const float* st, long long n, float decay,
+                           float debias, float sscale) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const float b = decay * biased[i] + (1.f - decay) * (st[i] * sscale);
+    biased[i] = b;
+    fac[i] = b * debias;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// damped inverse: traces -> damped fp64 copies -> block Gauss-Jordan
+// ---------------------------------------------------------------------------
+constexpr int GJB = 32;  // pivot block
+constexpr int MAXM = 12;
+
+struct MatSet {
+  int count;
+  int n[MAXM];        // logical size
+  int np[MAXM];       // padded to GJB
+  long long m_off[MAXM];    // np x np doubles in ws
+  long long row_off[MAXM];  // GJB x np doubles (Rrow')
+  long long col_off[MAXM];  // np x GJB doubles (Ccol)
+  int id[MAXM];       // original matrix index (for active subsets)
+};
+
+// traces of the 11 factors (normalised by dimension) -> tr[f]
+struct TraceSet {
+  const float* fac;
+  long long off[11];
+  int dim[11];
+};
+__global__ void traces_kernel(TraceSet t, double* tr) {
+  const int f = blockIdx.x;
+  const int n = t.dim[f];
+  const float* m = t.fac + t.off[f];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += (double)m[(long long)i * n + i];
+  __shared__ double red[4];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) tr[f] = (red[0] + red[1] + red[2] + red[3]) / (double)n;
+}
+
+// damped matrix m = 2l + (isG): source factor, damping from pi
+struct DampSet {
+  const float* fac;
+  long long src_off[12];
+  int n[12];
+  int np[12];
+  long long m_off[12];
+  int afac[12];   // trace index of the layer's A factor
+  int gfac[12];   // trace index of the layer's G factor
+  float lam[12];  // normalised damping lambda_l
+};
+__global__ void damp_kernel(DampSet d, const double* tr, double* ws) {
+  const int m = blockIdx.y;
+  const int n = d.n[m], np = d.np[m];
+  const long long tot = (long long)np * np;
+  const double ta = tr[d.afac[m]], tg = tr[d.gfac[m]];
+  double pi = (ta > 0.0 && tg > 0.0) ? sqrt(ta / tg) : 1.0;
+  const double sl = sqrt((double)d.lam[m]);
+  const double add = (m & 1) ? sl / pi : sl * pi;
+  const float* src = d.fac + d.src_off[m];
+  double* dst = ws + d.m_off[m];
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(e / np), c = (int)(e - (long long)r * np);
+    double v;
+    if (r < n && c < n) {
+      // symmetrise the f32 factor exactly
+      v = 0.5 * ((double)src[(long long)r * n + c] + (double)src[(long long)c * n + r]);
+      if (r == c) v += add;
+    } else {
+      v = (r == c) ? 1.0 : 0.0;  // identity padding: block-diag(M, I)
+    }
+    dst[e] = v;
+  }
+}
+
+// in-LDS Gauss-Jordan (sweep) inverse of the GJB x GJB pivot block
+__device__ void pivot_inverse(double (*P)[GJB + 1]) {
+  const int tid = threadIdx.x;  // 256 threads, 4 elements each
+  for (int t = 0; t < GJB; ++t) {
+    const double piv = P[t][t];
+    const double ipiv = 1.0 / piv;
+    double nv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q;
+      const int r = e / GJB, c = e - r * GJB;
+      const double v = P[r][c];
+      if (r == t && c == t) nv[q] = ipiv;
+      else if (r == t) nv[q] = v * ipiv;
+      else if (c == t) nv[q] = -v * ipiv;
+      else nv[q] = v - P[r][t] * P[t][c] * ipiv;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q;
+      P[e / GJB][e % GJB] = nv[q];
+    }
+    __syncthreads();
+  }
+}
+
+constexpr int PANEL_COLS = 256;
+// grid: (column chunks of PANEL_COLS, active matrices)
+__global__ __launch_bounds__(256) void gj_panel_kernel(MatSet s, double* ws, int step) {
+  const int mi = blockIdx.y;
+  const int np = s.np[mi];
+  const int c0 = blockIdx.x * PANEL_COLS;
+  if (c0 >= np) return;
+  const int kb = step * GJB;
+  double* M = ws + s.m_off[mi];
+  double* R = ws + s.row_off[mi];
+  double* C = ws + s.col_off[mi];
+  __shared__ double P[GJB][GJB + 1];
+  for (int e = threadIdx.x; e < GJB * GJB; e += 256)
+    P[e / GJB][e % GJB] = M[(long long)(kb + e / GJB) * np + kb + e % GJB];
+  __syncthreads();
+  pivot_inverse(P);
+  // Rrow'[t][j] = (Pinv M[kb.., j]) for j outside the pivot block, Pinv inside
+  const int j = c0 + threadIdx.x;
+  if (j < np) {
+    if (j >= kb && j < kb + GJB) {
+      for (int t = 0; t < GJB; ++t) R[(long long)t * np + j] = P[t][j - kb];
+    } else {
+      double col[GJB];
+#pragma unroll
+      for (int q = 0; q < GJB; ++q) col[q] = M[(long long)(kb + q) * np + j];
+      for (int t = 0; t < GJB; ++t) {
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < GJB; ++q) acc += P[t][q] * col[q];
+        R[(long long)t * np + j] = acc;
+      }
+    }
+    // Ccol[i][t] = M[i][kb + t] for rows i in this chunk (old values)
+    const int i = j;
+#pragma unroll
+    for (int t = 0; t < GJB; ++t) C[(long long)i * GJB + t] = M[(long long)i * np + kb + t];
+  }
+}
+
+// grid: (np/64, np/64, active matrices); 64x64 tile, 4x4 per thread
+__global__ __launch_bounds__(256) void gj_update_kernel(MatSet s, double* ws, int step) {
+  const int mi = blockIdx.z;
+  const int np = s.np[mi];
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  if (i0 >= np || j0 >= np) return;
+  const int kb = step * GJB;
+  double* M = ws + s.m_off[mi];
+  const double* R = ws + s.row_off[mi];
+  const double* C = ws + s.col_off[mi];
+  __shared__ double Cs[64][GJB + 1];
+  __shared__ double Rs[GJB][64 + 1];
+  for (int e = threadIdx.x; e < 64 * GJB; e += 256) {
+    const int r = e / GJB, t = e % GJB;
+    Cs[r][t] = (i0 + r < np) ? C[(long long)(i0 + r) * GJB + t] : 0.0;
+    const int tt = e / 64, c = e % 64;
+    Rs[tt][c] = (j0 + c < np) ? R[(long long)tt * np + j0 + c] : 0.0;
+  }
+  __syncthreads();
+  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int i = i0 + ty + 16 * a;
+    if (i >= np) continue;
+    const bool ipiv = i >= kb && i < kb + GJB;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int j = j0 + tx + 16 * b;
+      if (j >= np) continue;
+      const bool jpiv = j >= kb && j < kb + GJB;
+      double v;
+      if (ipiv) {
+        v = R[(long long)(i - kb) * np + j];  // pivot rows: Pinv M_kj (Pinv itself in-block)
+      } else {
+        double acc = 0.0;
+#pragma unroll 8
+        for (int t = 0; t < GJB; ++t) acc += Cs[ty + 16 * a][t] * Rs[t][tx + 16 * b];
+        v = (jpiv ? 0.0 : M[(long long)i * np + j]) - acc;
+      }
+      M[(long long)i * np + j] = v;
+    }
+  }
+}
+
+struct OutSet {
+  const double* ws;
+  long long m_off[12];
+  int n[12];
+  int np[12];
+  long long dst_off[12];
+};
+__global__ void gj_store_kernel(OutSet o, float* inv) {
+  const int m = blockIdx.y;
+  const int n = o.n[m], np = o.np[m];
+  const double* M = o.ws + o.m_off[m];
+  float* dst = inv + o.dst_off[m];
+  const long long tot = (long long)n * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(e / n), c = (int)(e - (long long)r * n);
+    dst[e] = (float)(0.5 * (M[(long long)r * np + c] + M[(long long)c * np + r]));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// eigenvalues: fp64 one-sided (Hestenes) Jacobi, round-robin pairs, one wave
+// per column pair, one launch per round; singular values == eigenvalues of
+// the SPD factors.
+// ---------------------------------------------------------------------------
+struct EigSet {
+  int count;
+  int n[11];
+  int ne[11];  // n rounded up to even
+  long long u_off[11];
+};
+
+__global__ void eig_load_kernel(const float* fac, EigSet s, TraceSet t, double* ws) {
+  const int m = blockIdx.y;
+  const int n = s.n[m];
+  const float* src = fac + t.off[m];
+  double* U = ws + s.u_off[m];
+  const long long tot = (long long)n * n;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(e / n), c = (int)(e - (long long)r * n);
+    // column-major U (column c contiguous) of the symmetrised factor
+    U[(long long)c * n + r] = 0.5 * ((double)src[(long long)r * n + c] + (double)src[(long long)c * n + r]);
+  }
+}
+
+// grid.x = pair index (waves of 64 in blocks of 256), grid.y = matrix
+__global__ __launch_bounds__(256) void eig_round_kernel(EigSet s, double* ws, int round,
+                                                        int* rotated, double tol) {
+  const int m = blockIdx.y;
+  const int n = s.n[m], ne = s.ne[m];
+  const int npairs = ne / 2;
+  const int pair = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (pair >= npairs || ne < 2) return;
+  const int lane = threadIdx.x & 63;
+  const int rr = round % (ne - 1);
+  int p, q;
+  if (pair == 0) {
+    p = rr;
+    q = ne - 1;
+  } else {
+    p = (rr + pair) % (ne - 1);
+    q = (rr - pair + (ne - 1)) % (ne - 1);
+  }
+  if (p >= n || q >= n) return;
+  double* U = ws + s.u_off[m];
+  double* up = U + (long long)p * n;
+  double* uq = U + (long long)q * n;
+  double a = 0.0, b = 0.0, g = 0.0;
+  for (int i = lane; i < n; i += 64) {
+    const double x = up[i], y = uq[i];
+    a += x * x;
+    b += y * y;
+    g += x * y;
+  }
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  g = wave_sum_d(g);
+  if (fabs(g) <= tol * sqrt(a * b) || g == 0.0) return;
+  const double zeta = (b - a) / (2.0 * g);
+  const double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+  const double c = 1.0 / sqrt(1.0 + t * t);
+  const double sn = c * t;
+  for (int i = lane; i < n; i += 64) {
+    const double x = up[i], y = uq[i];
+    up[i] = c * x - sn * y;
+    uq[i] = sn * x + c * y;
+  }
+  if (lane == 0) atomicOr(rotated, 1);
+}
+
+// eigenvalue = column norm; sorted ascending by rank
+__global__ void eig_store_kernel(EigSet s, const double* ws, long long* out_off, double* out,
+                                 double* tmp) {
+  const int m = blockIdx.x;
+  const int n = s.n[m];
+  const double* U = ws + s.u_off[m];
+  double* nr = tmp + out_off[m];
+  for (int c = threadIdx.x; c < n; c += blockDim.x) {
+    double acc = 0.0;
+    for (int i = 0; i < n; ++i) acc += U[(long long)c * n + i] * U[(long long)c * n + i];
+    nr[c] = sqrt(acc);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < n; c += blockDim.x) {
+    const double v = nr[c];
+    int rank = 0;
+    for (int d = 0; d < n; ++d) {
+      const double w = nr[d];
+      rank += (w < v) || (w == v && d < c);
+    }
+    out[out_off[m] + rank] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// natural-gradient step
+// ---------------------------------------------------------------------------
+constexpr int KRED = 512;
+__global__ void kdot_partial_kernel(const float* x, const float* y, long long n, float* part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    s += x[i] * y[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void kcoeff_kernel(const float* part, int nb, float lr, float c, float* coeff,
+                              float* coeff_out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float sq = (red[0] + red[1] + red[2] + red[3]) * lr * lr;
+    // min(1, sqrt(c / sq)); sq <= 0 or NaN -> 1 (fminf drops the NaN)
+    const float v = fminf(1.f, sqrtf(c / sq));
+    coeff[0] = v;
+    coeff[1] = sq;
+    if (coeff_out) coeff_out[0] = v;
+  }
+}
+
+__global__ void kapply_kernel(float* p, float* v, const float* d, long long n, float lr,
+                              float mom, const float* coeff) {
+  const float cf = coeff[0];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const float nv = mom * v[i] + cf * d[i];
+    v[i] = nv;
+    p[i] -= lr * nv;
+  }
+}
+
+}  // namespace acmi
+
+using namespace acmi;
+
+extern "C" {
+
+int acmi_kfac_ema(float* biased, float* factors, const float* stats, int64_t n, float decay,
+                  float debias, float stats_scale, acmi_stream_t stream) {
+  ACMI_REQUIRE(biased && factors && stats && n > 0, ACMI_ERR_ARG, "acmi_kfac_ema: bad args");
+  hipLaunchKernelGGL(ema_kernel, dim3(std::min<long long>(cdiv(n, 256), 2048)), dim3(256), 0,
+                     (hipStream_t)stream, biased, factors, stats, (long long)n, decay, debias,
+                     stats_scale);
+  ACMI_LAUNCH_CHECK("acmi_kfac_ema");
+  return ACMI_OK;
+}
+
+int64_t acmi_kfac_inverse_floats(int A, int C3) {
+  KLayout K;
+  if (!klayout(A, C3, &K)) return -1;
+  return K.inv_total;
+}
+
+static void inverse_plan(const KLayout& K, MatSet* s, long long* total) {
+  long long o = 16;  // traces
+  s->count = 12;
+  for (int m = 0; m < 12; ++m) {
+    const int l = m / 2;
+    const int n = (int)((m & 1) ? K.dout[l] : K.din[l]);
+    const int np = (n + GJB - 1) / GJB * GJB;
+    s->n[m] = n;
+    s->np[m] = np;
+    s->id[m] = m;
+    s->m_off[m] = o;
+    o += (long long)np * np;
+    s->row_off[m] = o;
+    o += (long long)GJB * np;
+    s->col_off[m] = o;
+    o += (long long)np * GJB;
+  }
+  *total = o;
+}
+
+int64_t acmi_kfac_inverse_ws_doubles(int A, int C3) {
+  KLayout K;
+  if (!klayout(A, C3, &K)) return -1;
+  MatSet s;
+  long long tot;
+  inverse_plan(K, &s, &tot);
+  return tot;
+}
+
+static TraceSet trace_set(const KLayout& K, const float* fac) {
+  TraceSet t;
+  t.fac = fac;
+  for (int f = 0; f < 11; ++f) {
+    t.off[f] = K.stat_off[f];
+    t.dim[f] = (int)(f < 5 ? K.din[f] : K.dout[f - 5]);
+  }
+  return t;
+}
+
+int acmi_kfac_inverse(int A, int C3, const float* factors, float damping, int conv_normalize,
+                      float* inv, double* ws, acmi_stream_t stream) {
+  KLayout K;
+  ACMI_REQUIRE(factors && inv && ws && klayout(A, C3, &K), ACMI_ERR_ARG,
+               "acmi_kfac_inverse: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  MatSet s;
+  long long tot;
+  inverse_plan(K, &s, &tot);
+  double* tr = ws;
+  hipLaunchKernelGGL(traces_kernel, dim3(11), dim3(256), 0, st, trace_set(K, factors), tr);
+  DampSet d;
+  d.fac = factors;
+  int maxnp = 0;
+  for (int m = 0; m < 12; ++m) {
+    const int l = m / 2;
+    const int af = l < 5 ? l : 4;  // fc_policy / fc_baseline share A_4
+    d.src_off[m] = (m & 1) ? K.stat_off[5 + l] : K.stat_off[af];
+    d.n[m] = s.n[m];
+    d.np[m] = s.np[m];
+    d.m_off[m] = s.m_off[m];
+    d.afac[m] = af;
+    d.gfac[m] = 5 + l;
+    d.lam[m] = conv_normalize ? damping / (float)CONV_LOCATIONS[l] : damping;
+    maxnp = std::max(maxnp, s.np[m]);
+  }
+  hipLaunchKernelGGL(damp_kernel, dim3(256, 12), dim3(256), 0, st, d, tr, ws);
+  const int maxsteps = maxnp / GJB;
+  for (int step = 0; step < maxsteps; ++step) {
+    MatSet a;
+    a.count = 0;
+    int anp = 0;
+    for (int m = 0; m < 12; ++m) {
+      if (s.np[m] / GJB > step) {
+        const int k = a.count++;
+        a.n[k] = s.n[m];
+        a.np[k] = s.np[m];
+        a.m_off[k] = s.m_off[m];
+        a.row_off[k] = s.row_off[m];
+        a.col_off[k] = s.col_off[m];
+        a.id[k] = m;
+        anp = std::max(anp, s.np[m]);
+      }
+    }
+    hipLaunchKernelGGL(gj_panel_kernel, dim3(cdiv(anp, PANEL_COLS), a.count), dim3(256), 0, st,
+                       a, ws, step);
+    hipLaunchKernelGGL(gj_update_kernel, dim3(cdiv(anp, 64), cdiv(anp, 64), a.count), dim3(256),
+                       0, st, a, ws, step);
+  }
+  OutSet o;
+  o.ws = ws;
+  for (int m = 0; m < 12; ++m) {
+    o.m_off[m] = s.m_off[m];
+    o.n[m] = s.n[m];
+    o.np[m] = s.np[m];
+    o.dst_off[m] = K.inv_off[m];
+  }
+  hipLaunchKernelGGL(gj_store_kernel, dim3(256, 12), dim3(256), 0, st, o, inv);
+  ACMI_LAUNCH_CHECK("acmi_kfac_inverse");
+  return ACMI_OK;
+}
+
+static void eig_plan(const KLayout& K, EigSet* s, long long* total) {
+  long long o = 64;  // flag + scratch for eigenvalue staging offsets
+  s->count = 11;
+  for (int f = 0; f < 11; ++f) {
+    const int n = (int)(f < 5 ? K.din[f] : K.dout[f - 5]);
+    s->n[f] = n;
+    s->ne[f] = (n + 1) / 2 * 2;
+    s->u_off[f] = o;
+    o += (long long)n * n;
+  }
+  // staging for column norms (same size as the output)
+  long long e = 0;
+  for (int f = 0; f < 11; ++f) e += s->n[f];
+  *total = o + e + 16;
+}
+
+int64_t acmi_kfac_eig_ws_doubles(int A, int C3) {
+  KLayout K;
+  if (!klayout(A, C3, &K)) return -1;
+  EigSet s;
+  long long tot;
+  eig_plan(K, &s, &tot);
+  return tot;
+}
+
+// NOTE: synchronises `stream` once per sweep to test convergence (diagnostic
+// path, not used inside the training step).
+int acmi_kfac_eigvals(int A, int C3, const float* factors, double* eigvals, double* ws,
+                      acmi_stream_t stream) {
+  KLayout K;
+  ACMI_REQUIRE(factors && eigvals && ws && klayout(A, C3, &K), ACMI_ERR_ARG,
+               "acmi_kfac_eigvals: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  EigSet s;
+  long long tot;
+  eig_plan(K, &s, &tot);
+  TraceSet t = trace_set(K, factors);
+  hipLaunchKernelGGL(eig_load_kernel, dim3(256, 11), dim3(256), 0, st, factors, s, t, ws);
+  int* flag = reinterpret_cast<int*>(ws);  // ws[0..1] doubles reused as an int flag
+  int maxne = 0, maxpairs = 0;
+  for (int f = 0; f < 11; ++f) {
+    maxne = std::max(maxne, s.ne[f]);
+    maxpairs = std::max(maxpairs, s.ne[f] / 2);
+  }
+  const int rounds = std::max(1, maxne - 1);
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    if (hipMemsetAsync(flag, 0, sizeof(int), st) != hipSuccess) {
+      set_error("acmi_kfac_eigvals: memset failed");
+      return ACMI_ERR_HIP;
+    }
+    for (int r = 0; r < rounds; ++r)
+      hipLaunchKernelGGL(eig_round_kernel, dim3(cdiv(maxpairs, 4), 11), dim3(256), 0, st, s, ws,
+                         r, flag, 1e-15);
+    int h = 0;
+    if (hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      set_error("acmi_kfac_eigvals: sync failed");
+      return ACMI_ERR_HIP;
+    }
+    if (!h) break;
+  }
+  // output offsets (device copy not needed: passed by value through a small buffer)
+  long long offs[11];
+  long long o = 0;
+  for (int f = 0; f < 11; ++f) {
+    offs[f] = o;
+    o += s.n[f];
+  }
+  long long* doffs = reinterpret_cast<long long*>(ws + 8);  // 11 int64 fit in ws[8..19)
+  // ws[8..19) lies inside the 64-double header reserved by eig_plan
+  if (hipMemcpyAsync(doffs, offs, sizeof(offs), hipMemcpyHostToDevice, st) != hipSuccess) {
+    set_error("acmi_kfac_eigvals: memcpy failed");
+    return ACMI_ERR_HIP;
+  }
+  double* staging = ws + tot - 16 - o;
+  hipLaunchKernelGGL(eig_store_kernel, dim3(11), dim3(256), 0, st, s, ws, doffs, eigvals,
+                     staging);
+  ACMI_LAUNCH_CHECK("acmi_kfac_eigvals");
+  if (hipStreamSynchronize(st) != hipSuccess) {
+    set_error("acmi_kfac_eigvals: final sync failed");
+    return ACMI_ERR_HIP;
+  }
+  return ACMI_OK;
+}
+
+int64_t acmi_kfac_step_ws_floats(int A, int C3) {
+  KLayout K;
+  if (!klayout(A, C3, &K)) return -1;
+  long long m = 0;
+  for (int l = 0; l < 6; ++l) m = std::max(m, K.din[l] * K.dout[l]);
+  return m + KRED + 16;
+}
+
+int acmi_kfac_step(int A, int C3, float* params, float* velocity, const float* grads,
+                   const float* inv, float lr, float momentum, float norm_constraint,
+                   float* precon, float* ws, float* coeff_out, acmi_stream_t stream) {
+  KLayout K;
+  ACMI_REQUIRE(params && velocity && grads && inv && precon && ws && klayout(A, C3, &K),
+               ACMI_ERR_ARG, "acmi_kfac_step: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  long long tmax = 0;
+  for (int l = 0; l < 6; ++l) tmax = std::max(tmax, K.din[l] * K.dout[l]);
+  float* t1 = ws;
+  float* part = ws + tmax;
+  float* coeff = part + KRED;
+  for (int l = 0; l < 6; ++l) {
+    const int din = (int)K.din[l], dout = (int)K.dout[l];
+    const float* ainv = inv + K.inv_off[2 * l];
+    const float* ginv = inv + K.inv_off[2 * l + 1];
+    const float* g = grads + K.poff[2 * l];  // [W; b] contiguous, din x dout
+    float* out = precon + K.poff[2 * l];
+    // t1 = Ainv g  (Ainv symmetric: A(k,i) = Ainv[k][i])
+    MatI<false> a1{ainv, din, din, din};
+    MatI<false> b1{g, dout, din, dout};
+    EpiStore e1{t1, dout};
+    // out = t1 Ginv
+    MatTKu a2{t1, dout, dout, din};
+    MatI<false> b2{ginv, dout, dout, dout};
+    EpiStore e2{out, dout};
+    if (dout >= 128) {
+      launch_gemm<128, 128, 32, 2, 2, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
+      launch_gemm<128, 128, 32, 2, 2, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
+    } else if (dout > 32) {
+      launch_gemm<128, 64, 32, 2, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
+      launch_gemm<128, 64, 32, 2, 1, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
+    } else {
+      launch_gemm<128, 32, 32, 1, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
+      launch_gemm<128, 32, 32, 1, 1, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
+    }
+  }
+  const long long n = K.nparams;
+  hipLaunchKernelGGL(kdot_partial_kernel, dim3(KRED), dim3(256), 0, s, grads, precon, n, part);
+  hipLaunchKernelGGL(kcoeff_kernel, dim3(1), dim3(256), 0, s, part, KRED, lr, norm_constraint,
+                     coeff, coeff_out);
+  hipLaunchKernelGGL(kapply_kernel, dim3(std::min<long long>(cdiv(n, 256), 2048)), dim3(256), 0,
+                     s, params, velocity, precon, n, lr, momentum, coeff);
+  ACMI_LAUNCH_CHECK("acmi_kfac_step");
+  return ACMI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,700 @@
+// Nature-CNN policy/value tower on gfx950: forward, backward fused with the
+// K-FAC input-factor statistics, and the sampled-loss output statistics.
+//
+// Reference: envs/atari/model.py:77-217 (graph), :219-246 (K-FAC layer
+// registration), nn.py:37-126 (layer math), policies.py:146-158 and
+// baselines.py:55-69 (predictive distributions), objectives.py:78 (the
+// tf.gradients of the shared loss).  See include/acmi.h for the contract.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "gemm.hpp"
+
+namespace acmi {
+
+static thread_local char g_err[512];
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+// ---------------------------------------------------------------------------
+// launch-site profiling: HIP events recorded on the launch stream around one
+// chosen kernel (acmi_prof_enable), summed by acmi_prof_collect.
+// ---------------------------------------------------------------------------
+static int g_prof_site = 0;
+static int g_prof_cap = 0;
+static int g_prof_n = 0;
+static hipEvent_t* g_prof_ev = nullptr;  // 2 * cap events
+
+static void prof_begin(int site, hipStream_t s) {
+  if (site != g_prof_site || g_prof_n >= g_prof_cap) return;
+  (void)hipEventRecord(g_prof_ev[2 * g_prof_n], s);
+}
+static void prof_end(int site, hipStream_t s) {
+  if (site != g_prof_site || g_prof_n >= g_prof_cap) return;
+  (void)hipEventRecord(g_prof_ev[2 * g_prof_n + 1], s);
+  ++g_prof_n;
+}
+
+// ---------------------------------------------------------------------------
+// layout
+// ---------------------------------------------------------------------------
+struct Layout {
+  int A, C3;
+  long long off[12];  // W, b per layer
+  long long total;
+  long long K[6], N[6];
+  long long din[6], dout[6];
+  long long stat_off[11], stat_total;
+  long long rows_per_img[6];  // output locations per image (conv L, fc 1)
+};
+
+static bool make_layout(int A, int C3, Layout* L) {
+  if (A < 1 || A > 64 || (C3 != 32 && C3 != 64)) return false;
+  L->A = A;
+  L->C3 = C3;
+  const long long K[6] = {8 * 8 * 4, 4 * 4 * 32, 3 * 3 * 64, 49LL * C3, 512, 512};
+  const long long N[6] = {32, 64, C3, 512, A, 1};
+  const long long R[6] = {400, 81, 49, 1, 1, 1};
+  long long o = 0;
+  for (int l = 0; l < 6; ++l) {
+    L->K[l] = K[l];
+    L->N[l] = N[l];
+    L->din[l] = K[l] + 1;
+    L->dout[l] = N[l];
+    L->rows_per_img[l] = R[l];
+    L->off[2 * l] = o;
+    o += K[l] * N[l];
+    L->off[2 * l + 1] = o;
+    o += N[l];
+  }
+  L->total = o;
+  long long s = 0;
+  for (int f = 0; f < 5; ++f) {
+    L->stat_off[f] = s;
+    s += L->din[f] * L->din[f];
+  }
+  for (int l = 0; l < 6; ++l) {
+    L->stat_off[5 + l] = s;
+    s += L->dout[l] * L->dout[l];
+  }
+  L->stat_total = s;
+  return true;
+}
+
+bool get_layout(int A, int C3, Layout* L) { return make_layout(A, C3, L); }
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+// fc heads weights as one [512][A+1] B operand: j<A -> pi.W, j==A -> v.W
+struct HeadsW {
+  static constexpr bool KCONTIG = false;
+  const float* wpi;
+  const float* wv;
+  int A;
+  __device__ __forceinline__ float el(int k, int j) const {
+    if (j < A) return wpi[k * A + j];
+    if (j == A) return wv[k];
+    return 0.f;
+  }
+  __device__ __forceinline__ float4 load4(int k, int j) const {
+    if (k >= 512) return f4zero();
+    return make_float4(el(k, j), el(k, j + 1), el(k, j + 2), el(k, j + 3));
+  }
+};
+
+// transposed heads weights: B(k = a, j) = a<A ? pi.W[j][a] : a==A ? v.W[j] : 0
+struct HeadsWT {
+  static constexpr bool KCONTIG = true;
+  const float* wpi;
+  const float* wv;
+  int A;
+  __device__ __forceinline__ float el(int a, int j) const {
+    if (a < A) return wpi[j * A + a];
+    if (a == A) return wv[j];
+    return 0.f;
+  }
+  __device__ __forceinline__ float4 load4(int k, int j) const {
+    if (j >= 512) return f4zero();
+    return make_float4(el(k, j), el(k + 1, j), el(k + 2, j), el(k + 3, j));
+  }
+};
+
+// conv/fc epilogue with an image remap so the rollout can write step t of an
+// env-major [N][T][rows] activation buffer in place.
+struct EpiAct {
+  float* out;
+  const float* bias;
+  int cols;         // output channels (row length)
+  int L;            // output rows per image
+  long long img_stride;  // floats between consecutive images in `out`
+  __device__ __forceinline__ void operator()(int i, int j, float v) const {
+    const int img = i / L;
+    const int p = i - img * L;
+    v = fmaxf(v + bias[j], 0.f);
+    out[(long long)img * img_stride + (long long)p * cols + j] = v;
+  }
+};
+
+struct EpiHeadsR {
+  float* logits;
+  int ld;
+  long long img_stride_l;  // rows
+  float* value;
+  long long img_stride_v;
+  const float* bpi;
+  const float* bv;
+  int A;
+  __device__ __forceinline__ void operator()(int i, int j, float v) const {
+    if (j < A) logits[(long long)i * img_stride_l * ld + j] = v + bpi[j];
+    else if (value) value[(long long)i * img_stride_v] = v + bv[0];
+  }
+};
+
+inline int roundup4(int x) { return (x + 3) & ~3; }
+
+// ---------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------
+template <int C3>
+static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
+                        long long img_stride, int B, const acmi_acts_t* a,
+                        int want_value, long long act_img_stride,
+                        hipStream_t s) {
+  // act_img_stride: images between consecutive batch rows in the activation
+  // buffers (1 = contiguous; T = rollout step t of an env-major buffer).
+  const long long st = act_img_stride;
+  {  // conv1: [B,84,84,4]u8 -> [B,20,20,32]
+    using Src = ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>;
+    RowsAsK<Src> opA{Src{obs, img_stride, B * 400}};
+    MatI<true> opB{P + L.off[0], 32, 256, 32};
+    EpiAct epi{a->a1, P + L.off[1], 32, 400, st * 400 * 32};
+    prof_begin(ACMI_PROF_CONV1_FWD, s);
+    launch_gemm<256, 32, 32, 2, 1, false, false>(opA, opB, epi, B * 400, 32, 256, 1, 0, s);
+    prof_end(ACMI_PROF_CONV1_FWD, s);
+  }
+  {  // conv2: -> [B,9,9,64]
+    using Src = ConvRows<float, 20, 20, 32, 4, 4, 2>;
+    RowsAsK<Src> opA{Src{a->a1, st * 400 * 32, B * 81}};
+    MatI<true> opB{P + L.off[2], 64, 512, 64};
+    EpiAct epi{a->a2, P + L.off[3], 64, 81, st * 81 * 64};
+    launch_gemm<128, 64, 32, 2, 1, false, false>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
+  }
+  {  // conv3: -> [B,7,7,C3]
+    using Src = ConvRows<float, 9, 9, 64, 3, 3, 1>;
+    RowsAsK<Src> opA{Src{a->a2, st * 81 * 64, B * 49}};
+    MatI<true> opB{P + L.off[4], C3, 576, C3};
+    EpiAct epi{a->a3, P + L.off[5], C3, 49, st * 49 * C3};
+    if constexpr (C3 == 32)
+      launch_gemm<256, 32, 32, 2, 1, false, false>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
+    else
+      launch_gemm<128, 64, 32, 2, 1, false, false>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
+  }
+  {  // fc4: [B,49*C3] -> [B,512]
+    const int K = 49 * C3;
+    // rows are images; with an image stride the dense row stride is st*K
+    RowsAsK<DenseRows> opA{DenseRows{a->a3, (int)(st * K), B, K}};
+    MatI<true> opB{P + L.off[6], 512, K, 512};
+    EpiAct epi{a->a4, P + L.off[7], 512, 1, st * 512};
+    launch_gemm<64, 128, 32, 1, 2, false, false>(opA, opB, epi, B, 512, K, 1, 0, s);
+  }
+  {  // heads: [B,512] -> logits [B,A], value [B]
+    RowsAsK<DenseRows> opA{DenseRows{a->a4, (int)(st * 512), B, 512}};
+    HeadsW opB{P + L.off[8], P + L.off[10], L.A};
+    EpiHeadsR epi{a->logits, a->ld_logits, st, want_value ? a->value : nullptr, st,
+                  P + L.off[9], P + L.off[11], L.A};
+    launch_gemm<128, 32, 32, 1, 1, false, false>(opA, opB, epi, B, L.A + 1, 512, 1, 0, s);
+  }
+  ACMI_LAUNCH_CHECK("acmi_forward");
+  return ACMI_OK;
+}
+
+// ---------------------------------------------------------------------------
+// split-K weight-gradient / factor reduction
+// ---------------------------------------------------------------------------
+// part: [nchunk][I+1][J] with J = kp + cout_pad + (kp ? 1 : 0).
+// grad (layer [W;b], (K+1) x cout, optionally split into two column groups
+// for the fused heads) and astat ((K+1)^2, symmetric, / rows).
+struct WgradDesc {
+  const float* part;
+  int nchunk;
+  int I;  // = K
+  int J;
+  int kp;       // 0 or K
+  int cout;
+  float* gradA;  // columns [0, nsplit)
+  int nsplit;
+  float* gradB;  // columns [nsplit, cout)
+  float* astat;  // nullable
+  int rows;
+};
+
+__global__ void finalize_wgrad_kernel(WgradDesc d) {
+  const int K = d.I;
+  const long long ngrad = (long long)(K + 1) * d.cout;
+  const long long nstat = d.astat ? (long long)(K + 1) * (K + 1) : 0;
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= ngrad + nstat) return;
+  const long long cs = (long long)(d.I + 1) * d.J;  // chunk stride
+  if (idx < ngrad) {
+    const int a = (int)(idx / d.cout);
+    const int n = (int)(idx - (long long)a * d.cout);
+    const int row = a < K ? a : d.I;
+    const float* p = d.part + (long long)row * d.J + d.kp + n;
+    float s = 0.f;
+    for (int c = 0; c < d.nchunk; ++c) s += p[c * cs];
+    if (n < d.nsplit) d.gradA[(long long)a * d.nsplit + n] = s;
+    else d.gradB[(long long)a * (d.cout - d.nsplit) + (n - d.nsplit)] = s;
+  } else {
+    const long long e = idx - ngrad;
+    const int a = (int)(e / (K + 1));
+    const int b = (int)(e - (long long)a * (K + 1));
+    const int lo = a < b ? a : b;
+    const int hi = a < b ? b : a;
+    float s;
+    if (hi == K && lo == K) {
+      s = (float)d.rows;
+    } else {
+      const int col = hi < K ? hi : d.J - 1;
+      const float* p = d.part + (long long)lo * d.J + col;
+      s = 0.f;
+      for (int c = 0; c < d.nchunk; ++c) s += p[c * cs];
+    }
+    d.astat[e] = s * (1.0f / (float)d.rows);
+  }
+}
+
+// G factor: part [nchunk][I+1][J] (I == J == n, no colsum row used)
+__global__ void finalize_cov_kernel(const float* part, int nchunk, int n,
+                                    int sub, float* out, int rows) {
+  // out is sub x sub, taken from the top-left of the n x n product
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= sub * sub) return;
+  const int a = idx / sub, b = idx - a * sub;
+  const int lo = a < b ? a : b, hi = a < b ? b : a;
+  const long long cs = (long long)(n + 1) * n;
+  const float* p = part + (long long)lo * n + hi;
+  float s = 0.f;
+  for (int c = 0; c < nchunk; ++c) s += p[c * cs];
+  out[idx] = s * (1.0f / (float)rows);
+}
+
+// G of the value head: element (A, A) of the heads product
+__global__ void finalize_cov_elem_kernel(const float* part, int nchunk, int n,
+                                         int a, float* out, int rows) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const long long cs = (long long)(n + 1) * n;
+  const float* p = part + (long long)a * n + a;
+  float s = 0.f;
+  for (int c = 0; c < nchunk; ++c) s += p[c * cs];
+  out[0] = s * (1.0f / (float)rows);
+}
+
+// choose the split-K chunking: ~target blocks overall, chunk % 32 == 0
+static void plan_chunks(long long rows, int tiles, int* nchunk, int* chunk) {
+  const long long target_blocks = 1536;
+  long long nc = target_blocks / (tiles > 0 ? tiles : 1);
+  if (nc < 1) nc = 1;
+  long long ch = (rows + nc - 1) / nc;
+  if (ch < 256) ch = 256;
+  ch = (ch + 31) / 32 * 32;
+  nc = (rows + ch - 1) / ch;
+  if (nc < 1) nc = 1;
+  *nchunk = (int)nc;
+  *chunk = (int)ch;
+}
+
+static long long partial_floats(long long I, long long J, long long rows) {
+  int nc, ch;
+  const int tiles = cdiv(I, 128) * cdiv(J, 128);
+  plan_chunks(rows, tiles, &nc, &ch);
+  return (long long)nc * (I + 1) * J;
+}
+
+// Launch [P;1]^T [P | dY | 1] (with_stats) or P^T [dY] (+colsum) over rows.
+template <class Src>
+static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
+                       int ldy, int cout, bool with_stats, float* part,
+                       long long part_cap, float* gradA, int nsplit,
+                       float* gradB, float* astat, hipStream_t s, int site = 0) {
+  const int cout_pad = roundup4(cout);
+  const int kp = with_stats ? K : 0;
+  const int I = K;
+  const int J = kp + cout_pad + (with_stats ? 1 : 0);
+  RowsAsI<Src> opA{src};
+  CatRowsI<Src> opB{src, kp, dy, ldy, cout, cout_pad, (int)rows};
+  int nc, ch;
+  if (with_stats) {
+    plan_chunks(rows, cdiv(I, 128) * cdiv(J, 128), &nc, &ch);
+  } else {
+    plan_chunks(rows, cdiv(I, 128) * cdiv(J, 32), &nc, &ch);
+  }
+  const long long need = (long long)nc * (I + 1) * J;
+  ACMI_REQUIRE(need <= part_cap, ACMI_ERR_WS, "wgrad workspace too small (%lld > %lld)",
+               need, part_cap);
+  EpiPartial epi{part, I, J};
+  prof_begin(site, s);
+  if (with_stats)
+    launch_gemm<128, 128, 32, 2, 2, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s);
+  else
+    launch_gemm<128, 32, 32, 1, 1, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s);
+  prof_end(site, s);
+  WgradDesc d{part, nc, I, J, kp, cout, gradA, nsplit, gradB, astat, (int)rows};
+  const long long total = (long long)(K + 1) * cout + (astat ? (long long)(K + 1) * (K + 1) : 0);
+  hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, d);
+  ACMI_LAUNCH_CHECK("wgrad_layer");
+  return ACMI_OK;
+}
+
+// G = g^T g / rows for g [rows][ld] (first n columns), via split-K
+static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
+                      float* part, long long part_cap, float* out,
+                      hipStream_t s, float* out_v = nullptr, int v_index = -1) {
+  DenseRows src{g, ld, (int)rows, roundup4(n)};
+  RowsAsI<DenseRows> op{src};
+  const int np = roundup4(n);
+  int nc, ch;
+  plan_chunks(rows, cdiv(np, 64) * cdiv(np, 64), &nc, &ch);
+  const long long need = (long long)nc * (np + 1) * np;
+  ACMI_REQUIRE(need <= part_cap, ACMI_ERR_WS, "gcov workspace too small");
+  EpiPartial epi{part, np, np};
+  launch_gemm<64, 64, 32, 1, 1, true, false>(op, op, epi, np, np, (int)rows, nc, ch, s);
+  hipLaunchKernelGGL(finalize_cov_kernel, dim3(cdiv((long long)sub * sub, 256)), dim3(256), 0,
+                     s, part, nc, np, sub, out, (int)rows);
+  if (out_v)
+    hipLaunchKernelGGL(finalize_cov_elem_kernel, dim3(1), dim3(64), 0, s, part, nc, np,
+                       v_index, out_v, (int)rows);
+  ACMI_LAUNCH_CHECK("gcov_layer");
+  return ACMI_OK;
+}
+
+static long long bwd_partial_cap(int B, int A, int C3) {
+  // the largest split-K partial over all layers (with stats)
+  long long m = 0;
+  const long long rowsL[5] = {400LL * B, 81LL * B, 49LL * B, B, B};
+  const long long Ks[5] = {256, 512, 576, 49LL * C3, 512};
+  const long long co[5] = {32, 64, C3, 512, A + 1};
+  for (int l = 0; l < 5; ++l) {
+    const long long J = Ks[l] + roundup4((int)co[l]) + 1;
+    m = std::max(m, partial_floats(Ks[l], J, rowsL[l]));
+  }
+  // G factors (64x64 tiles)
+  const long long gn[5] = {32, 64, C3, 512, roundup4(A + 1)};
+  const long long gr[5] = {400LL * B, 81LL * B, 49LL * B, B, B};
+  for (int l = 0; l < 5; ++l) {
+    int nc, ch;
+    plan_chunks(gr[l], cdiv(gn[l], 64) * cdiv(gn[l], 64), &nc, &ch);
+    m = std::max(m, (long long)nc * (gn[l] + 1) * gn[l]);
+  }
+  return m;
+}
+
+// ---------------------------------------------------------------------------
+// backward (dX chain) shared by the loss backward and the sampled backward
+// ---------------------------------------------------------------------------
+template <int C3>
+static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a,
+                    const acmi_bwd_t* bw, const float* dhead, int ldh,
+                    hipStream_t s) {
+  {  // heads -> d4 = (dhead W_h^T) * relu'(a4)
+    RowsAsK<DenseRows> opA{DenseRows{dhead, ldh, B, ldh}};
+    HeadsWT opB{P + L.off[8], P + L.off[10], L.A};
+    EpiReluGrad epi{bw->d4, a->a4, 512};
+    launch_gemm<128, 128, 8, 2, 2, false, false>(opA, opB, epi, B, 512, ldh, 1, 0, s);
+  }
+  {  // fc4 -> d3 = (d4 W4^T) * relu'(a3)
+    const int K3 = 49 * C3;
+    RowsAsK<DenseRows> opA{DenseRows{bw->d4, 512, B, 512}};
+    MatTK opB{P + L.off[6], 512, 512, K3};
+    EpiReluGrad epi{bw->d3, a->a3, K3};
+    launch_gemm<64, 128, 32, 1, 2, false, false>(opA, opB, epi, B, K3, 512, 1, 0, s);
+  }
+  {  // conv3 -> d2 (stride 1: one phase)
+    using Src = ConvTRows<9, 9, 3, 3, 1, C3>;
+    RowsAsK<Src> opA{Src{bw->d3, B * Src::L}};
+    ConvTWeights<3, 3, 1, 64, C3> opB{P + L.off[4]};
+    EpiConvTPhase<9, 9, 1, 64> epi{bw->d2, a->a2};
+    launch_gemm<128, 64, 32, 2, 1, false, false>(opA, opB, epi, B * Src::L, 64, Src::COLS, 1, 0, s);
+  }
+  {  // conv2 -> d1 (stride 2: four phases on blockIdx.z)
+    using Src = ConvTRows<20, 20, 4, 4, 2, 64>;
+    RowsAsK<Src> opA{Src{bw->d2, B * Src::L}};
+    ConvTWeights<4, 4, 2, 32, 64> opB{P + L.off[2]};
+    EpiConvTPhase<20, 20, 2, 32> epi{bw->d1, a->a1};
+    launch_gemm<256, 32, 32, 2, 1, false, false>(opA, opB, epi, B * Src::L, 32, Src::COLS, 4, 0, s);
+  }
+  ACMI_LAUNCH_CHECK("dx_chain");
+  return ACMI_OK;
+}
+
+template <int C3>
+static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
+                         long long img_stride, int B, const acmi_acts_t* a,
+                         const acmi_bwd_t* bw, float* grads, float* astat,
+                         float* ws, long long ws_cap, hipStream_t s) {
+  int rc = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s);
+  if (rc) return rc;
+  const bool st = astat != nullptr;
+  float* part = ws;
+  // heads: X = a4 (512), dY = dhead (A+1 columns: pi | v)
+  rc = wgrad_layer(DenseRows{a->a4, 512, B, 512}, 512, B, bw->dhead, bw->ldh, L.A + 1, st,
+                   part, ws_cap, grads + L.off[8], L.A, grads + L.off[10],
+                   st ? astat + L.stat_off[4] : nullptr, s);
+  if (rc) return rc;
+  // fc4: X = a3 flat
+  rc = wgrad_layer(DenseRows{a->a3, 49 * C3, B, 49 * C3}, 49 * C3, B, bw->d4, 512, 512, st,
+                   part, ws_cap, grads + L.off[6], 512, nullptr,
+                   st ? astat + L.stat_off[3] : nullptr, s);
+  if (rc) return rc;
+  // conv3: patches of a2
+  rc = wgrad_layer(ConvRows<float, 9, 9, 64, 3, 3, 1>{a->a2, 81 * 64, B * 49}, 576, 49LL * B,
+                   bw->d3, C3, C3, st, part, ws_cap, grads + L.off[4], C3, nullptr,
+                   st ? astat + L.stat_off[2] : nullptr, s);
+  if (rc) return rc;
+  // conv2: patches of a1
+  rc = wgrad_layer(ConvRows<float, 20, 20, 32, 4, 4, 2>{a->a1, 400 * 32, B * 81}, 512,
+                   81LL * B, bw->d2, 64, 64, st, part, ws_cap, grads + L.off[2], 64, nullptr,
+                   st ? astat + L.stat_off[1] : nullptr, s, ACMI_PROF_CONV2_WGRAD);
+  if (rc) return rc;
+  // conv1: patches of the u8 observations
+  rc = wgrad_layer(ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>{obs, img_stride, B * 400}, 256,
+                   400LL * B, bw->d1, 32, 32, st, part, ws_cap, grads + L.off[0], 32, nullptr,
+                   st ? astat + L.stat_off[0] : nullptr, s, ACMI_PROF_CONV1_WGRAD);
+  return rc;
+}
+
+// sampled-loss output gradients at the heads (kfac "gradients" mode):
+// g_pi = softmax(z) - onehot(y), y ~ Cat(z);  g_v = V - y_v = -eps, eps~N(0,1)
+__global__ void sampled_head_grad_kernel(const float* logits, int ld, int B, int A,
+                                         uint32_t seed, uint32_t sid, uint32_t ctr,
+                                         float* g, int ldg) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= B) return;
+  const float* z = logits + (long long)m * ld;
+  float mx = -INFINITY;
+  for (int a = 0; a < A; ++a) mx = fmaxf(mx, z[a]);
+  float se = 0.f;
+  for (int a = 0; a < A; ++a) se += expf(z[a] - mx);
+  const uint32_t h = key4(seed, sid, ctr, (uint32_t)m);
+  const float u = u01(h);
+  // inverse CDF draw
+  const float target = u * se;
+  float c = 0.f;
+  int y = A - 1;
+  for (int a = 0; a < A; ++a) {
+    c += expf(z[a] - mx);
+    if (target < c) { y = a; break; }
+  }
+  float* gr = g + (long long)m * ldg;
+  for (int a = 0; a < A; ++a) gr[a] = expf(z[a] - mx) / se - (a == y ? 1.f : 0.f);
+  // Box-Muller from two further counters
+  const float u1 = u01(mix32(h ^ 0x68e31da4U)) + (1.0f / 33554432.0f);
+  const float u2 = u01(mix32(h ^ 0xb5297a4dU));
+  const float eps = sqrtf(-2.f * logf(u1)) * cosf(6.2831853071795864f * u2);
+  gr[A] = -eps;
+  for (int a = A + 1; a < ldg; ++a) gr[a] = 0.f;
+}
+
+template <int C3>
+static int output_stats_impl(const Layout& L, const float* P, int B,
+                             const acmi_acts_t* a, const acmi_bwd_t* bw,
+                             uint32_t seed, uint32_t sid, uint32_t ctr,
+                             float* gstat, float* ws, long long ws_cap,
+                             hipStream_t s) {
+  const int ldg = roundup4(L.A + 1) < 8 ? 8 : roundup4(L.A + 1);
+  float* ghead = ws;  // [B][ldg]
+  float* part = ws + (long long)B * ldg;
+  const long long cap = ws_cap - (long long)B * ldg;
+  hipLaunchKernelGGL(sampled_head_grad_kernel, dim3(cdiv(B, 128)), dim3(128), 0, s,
+                     a->logits, a->ld_logits, B, L.A, seed, sid, ctr, ghead, ldg);
+  int rc = dx_chain<C3>(L, P, B, a, bw, ghead, ldg, s);
+  if (rc) return rc;
+  // heads: G_pi (A x A) from the first A columns, G_v = element (A, A)
+  rc = gcov_layer(ghead, ldg, L.A + 1, B, L.A, part, cap, gstat + L.stat_off[5 + 4], s,
+                  gstat + L.stat_off[5 + 5], L.A);
+  if (rc) return rc;
+  rc = gcov_layer(bw->d4, 512, 512, B, 512, part, cap, gstat + L.stat_off[5 + 3], s);
+  if (rc) return rc;
+  rc = gcov_layer(bw->d3, C3, C3, 49LL * B, C3, part, cap, gstat + L.stat_off[5 + 2], s);
+  if (rc) return rc;
+  rc = gcov_layer(bw->d2, 64, 64, 81LL * B, 64, part, cap, gstat + L.stat_off[5 + 1], s);
+  if (rc) return rc;
+  rc = gcov_layer(bw->d1, 32, 32, 400LL * B, 32, part, cap, gstat + L.stat_off[5 + 0], s);
+  return rc;
+}
+
+}  // namespace acmi
+
+using namespace acmi;
+
+extern "C" {
+
+const char* acmi_last_error(void) { return g_err; }
+int acmi_abi_version(void) { return ACMI_ABI_VERSION; }
+
+int64_t acmi_param_count(int A, int C3) {
+  Layout L;
+  if (!make_layout(A, C3, &L)) return -1;
+  return L.total;
+}
+
+int acmi_param_offsets(int A, int C3, int64_t* off) {
+  Layout L;
+  ACMI_REQUIRE(off && make_layout(A, C3, &L), ACMI_ERR_ARG, "bad A=%d/C3=%d", A, C3);
+  for (int i = 0; i < 12; ++i) off[i] = L.off[i];
+  return ACMI_OK;
+}
+
+int acmi_kfac_layout(int A, int C3, int64_t* din, int64_t* dout, int64_t* so, int64_t* total) {
+  Layout L;
+  ACMI_REQUIRE(make_layout(A, C3, &L), ACMI_ERR_ARG, "bad A=%d/C3=%d", A, C3);
+  for (int l = 0; l < 6; ++l) {
+    if (din) din[l] = L.din[l];
+    if (dout) dout[l] = L.dout[l];
+  }
+  for (int f = 0; f < 11; ++f)
+    if (so) so[f] = L.stat_off[f];
+  if (total) *total = L.stat_total;
+  return ACMI_OK;
+}
+
+static int forward_dispatch(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride,
+                            int B, const acmi_acts_t* acts, int want_value,
+                            long long act_stride, acmi_stream_t stream) {
+  Layout L;
+  ACMI_REQUIRE(net && acts && obs && net->params, ACMI_ERR_ARG, "acmi_forward: null argument");
+  ACMI_REQUIRE(make_layout(net->num_actions, net->conv3_filters, &L), ACMI_ERR_ARG,
+               "acmi_forward: bad A=%d/C3=%d", net->num_actions, net->conv3_filters);
+  ACMI_REQUIRE(B >= 0 && img_stride >= 84 * 84 * 4 && img_stride % 4 == 0, ACMI_ERR_ARG,
+               "acmi_forward: bad B=%d / img_stride=%lld", B, (long long)img_stride);
+  ACMI_REQUIRE(acts->a1 && acts->a2 && acts->a3 && acts->a4 && acts->logits &&
+                   acts->ld_logits >= net->num_actions && (!want_value || acts->value),
+               ACMI_ERR_ARG, "acmi_forward: bad activation buffers");
+  ACMI_REQUIRE(act_stride >= 1, ACMI_ERR_ARG, "bad activation stride");
+  if (B == 0) return ACMI_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (L.C3 == 32)
+    return forward_impl<32>(L, net->params, obs, img_stride, B, acts, want_value, act_stride, s);
+  return forward_impl<64>(L, net->params, obs, img_stride, B, acts, want_value, act_stride, s);
+}
+
+int acmi_forward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,
+                 const acmi_acts_t* acts, int want_value, acmi_stream_t stream) {
+  return forward_dispatch(net, obs, img_stride, B, acts, want_value, 1, stream);
+}
+
+/* Rollout variant: batch row b is image (b*act_img_stride) of the activation
+ * buffers (env-major [N][T] storage; pointers pre-offset by step t). */
+int acmi_forward_strided(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,
+                         const acmi_acts_t* acts, int want_value, int64_t act_img_stride,
+                         acmi_stream_t stream) {
+  return forward_dispatch(net, obs, img_stride, B, acts, want_value, act_img_stride, stream);
+}
+
+int64_t acmi_backward_ws_floats(int B, int A, int C3) {
+  Layout L;
+  if (!make_layout(A, C3, &L) || B < 0) return -1;
+  const int ldg = roundup4(A + 1) < 8 ? 8 : roundup4(A + 1);
+  return bwd_partial_cap(B, A, C3) + (long long)B * ldg + 64;
+}
+
+int acmi_backward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,
+                  const acmi_acts_t* acts, const acmi_bwd_t* bwd, float* grads,
+                  float* a_stats, float* ws, acmi_stream_t stream) {
+  Layout L;
+  ACMI_REQUIRE(net && acts && bwd && grads && ws && obs, ACMI_ERR_ARG,
+               "acmi_backward: null argument");
+  ACMI_REQUIRE(make_layout(net->num_actions, net->conv3_filters, &L), ACMI_ERR_ARG,
+               "acmi_backward: bad net");
+  ACMI_REQUIRE(B > 0 && img_stride >= 84 * 84 * 4 && img_stride % 4 == 0, ACMI_ERR_ARG,
+               "acmi_backward: bad B / img_stride");
+  ACMI_REQUIRE(bwd->ldh >= net->num_actions + 1 && bwd->ldh % 4 == 0, ACMI_ERR_ARG,
+               "acmi_backward: ldh must be >= A+1 and a multiple of 4 (zero padded)");
+  const long long cap = acmi_backward_ws_floats(B, net->num_actions, net->conv3_filters);
+  hipStream_t s = (hipStream_t)stream;
+  if (L.C3 == 32)
+    return backward_impl<32>(L, net->params, obs, img_stride, B, acts, bwd, grads, a_stats, ws,
+                             cap, s);
+  return backward_impl<64>(L, net->params, obs, img_stride, B, acts, bwd, grads, a_stats, ws,
+                           cap, s);
+}
+
+int acmi_kfac_output_stats(const acmi_net_t* net, int B, const acmi_acts_t* acts,
+                           const acmi_bwd_t* bwd, uint32_t seed, uint32_t stream_id,
+                           uint32_t counter, float* g_stats, float* ws, acmi_stream_t stream) {
+  Layout L;
+  ACMI_REQUIRE(net && acts && bwd && g_stats && ws, ACMI_ERR_ARG,
+               "acmi_kfac_output_stats: null argument");
+  ACMI_REQUIRE(make_layout(net->num_actions, net->conv3_filters, &L), ACMI_ERR_ARG, "bad net");
+  ACMI_REQUIRE(B > 0, ACMI_ERR_ARG, "bad B");
+  const long long cap = acmi_backward_ws_floats(B, net->num_actions, net->conv3_filters);
+  hipStream_t s = (hipStream_t)stream;
+  if (L.C3 == 32)
+    return output_stats_impl<32>(L, net->params, B, acts, bwd, seed, stream_id, counter,
+                                 g_stats, ws, cap, s);
+  return output_stats_impl<64>(L, net->params, B, acts, bwd, seed, stream_id, counter, g_stats,
+                               ws, cap, s);
+}
+
+int acmi_prof_enable(int site, int capacity) {
+  ACMI_REQUIRE(site >= 0 && capacity >= 0 && capacity <= 65536, ACMI_ERR_ARG,
+               "acmi_prof_enable: bad site/capacity");
+  if (g_prof_ev) {
+    for (int i = 0; i < 2 * g_prof_cap; ++i) (void)hipEventDestroy(g_prof_ev[i]);
+    delete[] g_prof_ev;
+    g_prof_ev = nullptr;
+  }
+  g_prof_site = 0;
+  g_prof_cap = 0;
+  g_prof_n = 0;
+  if (site == 0 || capacity == 0) return ACMI_OK;
+  g_prof_ev = new hipEvent_t[2 * capacity];
+  for (int i = 0; i < 2 * capacity; ++i) {
+    if (hipEventCreate(&g_prof_ev[i]) != hipSuccess) {
+      set_error("acmi_prof_enable: hipEventCreate failed");
+      return ACMI_ERR_HIP;
+    }
+  }
+  g_prof_site = site;
+  g_prof_cap = capacity;
+  return ACMI_OK;
+}
+
+int acmi_prof_collect(double* total_ms, int* count) {
+  ACMI_REQUIRE(total_ms && count, ACMI_ERR_ARG, "acmi_prof_collect: null argument");
+  double t = 0.0;
+  for (int i = 0; i < g_prof_n; ++i) {
+    if (hipEventSynchronize(g_prof_ev[2 * i + 1]) != hipSuccess) {
+      set_error("acmi_prof_collect: hipEventSynchronize failed");
+      return ACMI_ERR_HIP;
+    }
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, g_prof_ev[2 * i], g_prof_ev[2 * i + 1]);
+    t += ms;
+  }
+  *total_ms = t;
+  *count = g_prof_n;
+  g_prof_n = 0;
+  return ACMI_OK;
+}
+
+int acmi_gemm_f32(const float* A, const float* B, float* C, int M, int N, int K,
+                  acmi_stream_t stream) {
+  ACMI_REQUIRE(A && B && C && M > 0 && N > 0 && K > 0 && K % 4 == 0 && N % 4 == 0,
+               ACMI_ERR_ARG, "acmi_gemm_f32: need K%%4==0, N%%4==0");
+  RowsAsK<DenseRows> opA{DenseRows{A, K, M, K}};
+  MatI<true> opB{B, N, K, N};
+  EpiStore epi{C, N};
+  launch_gemm<128, 128, 32, 2, 2, false, false>(opA, opB, epi, M, N, K, 1, 0,
+                                                (hipStream_t)stream);
+  ACMI_LAUNCH_CHECK("acmi_gemm_f32");
+  return ACMI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,490 @@
+// Rollout-side and loss-side kernels: categorical sampling, n-step targets,
+// A2C loss + head gradients, first-order optimizers, batched synthetic Atari
+// stepper with the reference's frame-stack / auto-reset / episode-info
+// semantics.  Contracts and reference citations: include/acmi.h.
+#include <math.h>
+
+#include "common.hpp"
+
+namespace acmi {
+
+// ---------------------------------------------------------------------------
+// sampling (policies.py:86 Categorical.sample / :87 mode)
+// ---------------------------------------------------------------------------
+__global__ void sample_kernel(const float* logits, int ld, int B, int A, uint32_t seed,
+                              uint32_t sid, uint32_t ctr, const float* uniforms, int mode,
+                              int32_t* actions, int32_t* bad) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= B) return;
+  const float* z = logits + (long long)m * ld;
+  float mx = -INFINITY;
+  bool finite = true;
+  int amax = 0;
+  for (int a = 0; a < A; ++a) {
+    const float v = z[a];
+    finite = finite && isfinite(v);
+    if (v > mx) { mx = v; amax = a; }
+  }
+  if (!finite) {
+    actions[m] = -1;
+    atomicAdd(bad, 1);
+    return;
+  }
+  if (mode) {
+    actions[m] = amax;  // first maximal index, like argmax
+    return;
+  }
+  float se = 0.f;
+  for (int a = 0; a < A; ++a) se += expf(z[a] - mx);
+  const float u = uniforms ? uniforms[m] : u01(key4(seed, sid, ctr, (uint32_t)m));
+  const float target = u * se;
+  float c = 0.f;
+  int y = A - 1;
+  for (int a = 0; a < A; ++a) {
+    c += expf(z[a] - mx);
+    if (target < c) { y = a; break; }
+  }
+  actions[m] = y;
+}
+
+// per-row entropy and log pi(a) (Categorical.entropy / log_prob, policies.py:87-89)
+__global__ void categorical_kernel(const float* logits, int ld, int B, int A, const int32_t* actions,
+                                   float* ent, float* lpa) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= B) return;
+  const float* z = logits + (long long)m * ld;
+  float mx = -INFINITY;
+  for (int a = 0; a < A; ++a) mx = fmaxf(mx, z[a]);
+  float se = 0.f;
+  for (int a = 0; a < A; ++a) se += expf(z[a] - mx);
+  const float lse = mx + logf(se);
+  if (ent) {
+    float H = 0.f;
+    for (int a = 0; a < A; ++a) {
+      const float lp = z[a] - lse;
+      H -= expf(lp) * lp;
+    }
+    ent[m] = H;
+  }
+  if (lpa && actions) lpa[m] = z[actions[m]] - lse;
+}
+
+// ---------------------------------------------------------------------------
+// n-step targets (objectives.py:178-214), one thread per env, reverse-free:
+// target[t] = sum_{i=t..stop} r_i * gp[i-t]  (ascending i, mul+add, no FMA)
+// ---------------------------------------------------------------------------
+__global__ void returns_kernel(const float* r, const uint8_t* d, const float* v,
+                               const float* vb, int N, int T, const float* gp,
+                               const float* bp, float* tgt, float* adv) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const float* rn = r + (long long)n * T;
+  const uint8_t* dn = d + (long long)n * T;
+  // first terminal at or after t, scanning from the back
+  int next_term = T;  // index of the first terminal >= t (T = none)
+  for (int t = T - 1; t >= 0; --t) {
+    if (dn[t]) next_term = t;
+    const int stop = next_term < T ? next_term : T - 1;
+    float acc = 0.f;
+    for (int i = t; i <= stop; ++i) acc = __fadd_rn(acc, __fmul_rn(rn[i], gp[i - t]));
+    const float boot = next_term < T ? 0.f : __fmul_rn(bp[T - t], vb[n]);
+    const float target = __fadd_rn(acc, boot);
+    tgt[(long long)n * T + t] = target;
+    adv[(long long)n * T + t] = __fsub_rn(target, v[(long long)n * T + t]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// A2C loss + head gradients (objectives.py:123-154, :78)
+// ---------------------------------------------------------------------------
+constexpr int LOSS_BLOCK = 256;
+
+__global__ void a2c_loss_kernel(const float* logits, int ld, const float* values,
+                                const int32_t* actions, const float* targets,
+                                const float* adv, int M, int A, float beta, float vcoef,
+                                float gscale, float* dhead, int ldh, float* part) {
+  __shared__ float red[3][LOSS_BLOCK / 64];
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  float s_pl = 0.f, s_h = 0.f, s_v = 0.f;
+  if (m < M) {
+    const float* z = logits + (long long)m * ld;
+    float mx = -INFINITY;
+    for (int a = 0; a < A; ++a) mx = fmaxf(mx, z[a]);
+    float se = 0.f;
+    for (int a = 0; a < A; ++a) se += expf(z[a] - mx);
+    const float lse = mx + logf(se);
+    float H = 0.f;
+    for (int a = 0; a < A; ++a) {
+      const float lp = z[a] - lse;
+      H -= expf(lp) * lp;
+    }
+    const int act = actions[m];
+    const float lpa = z[act] - lse;
+    const float ad = adv[m];
+    const float diff = targets[m] - values[m];
+    s_pl = ad * lpa;
+    s_h = H;
+    s_v = 0.5f * diff * diff;
+    // dL/dz_k = -(1/M)[adv (onehot_k - p_k) - beta p_k (log p_k + H)]
+    const float inv = gscale / (float)M;
+    float* g = dhead + (long long)m * ldh;
+    for (int a = 0; a < A; ++a) {
+      const float lp = z[a] - lse;
+      const float p = expf(lp);
+      const float oh = a == act ? 1.f : 0.f;
+      g[a] = -inv * (ad * (oh - p) - beta * p * (lp + H));
+    }
+    // d(vcoef * L_v)/dV = vcoef * (V - target) / M
+    g[A] = vcoef * inv * (values[m] - targets[m]);
+    for (int a = A + 1; a < ldh; ++a) g[a] = 0.f;
+  }
+  s_pl = wave_sum(s_pl);
+  s_h = wave_sum(s_h);
+  s_v = wave_sum(s_v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = s_pl;
+    red[1][w] = s_h;
+    red[2][w] = s_v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, b = 0.f, c = 0.f;
+    for (int i = 0; i < LOSS_BLOCK / 64; ++i) {
+      a += red[0][i];
+      b += red[1][i];
+      c += red[2][i];
+    }
+    part[blockIdx.x * 3 + 0] = a;
+    part[blockIdx.x * 3 + 1] = b;
+    part[blockIdx.x * 3 + 2] = c;
+  }
+}
+
+__global__ void a2c_loss_final_kernel(const float* part, int nb, int M, float beta,
+                                      float* out) {
+  // one wave: deterministic fixed-order sums
+  float a = 0.f, b = 0.f, c = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 64) {
+    a += part[i * 3 + 0];
+    b += part[i * 3 + 1];
+    c += part[i * 3 + 2];
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  c = wave_sum(c);
+  if (threadIdx.x == 0) {
+    const float mean_pl = a / (float)M;
+    const float mean_h = b / (float)M;
+    out[0] = -(mean_pl + beta * mean_h);
+    out[1] = c / (float)M;
+    out[2] = mean_h;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// deterministic global sum of squares / dot product (two passes)
+// ---------------------------------------------------------------------------
+constexpr int RED_BLOCKS = 512;
+
+__global__ void dot_partial_kernel(const float* x, const float* y, long long n, float* part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    s += x[i] * y[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__device__ float block_final_sum(const float* part, int nb) {
+  // called by one full block of 256: fixed-order reduction
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return tot;
+}
+
+// scale[0] = clip factor (TF clip_by_global_norm), scale[1] = global norm
+__global__ void clip_scale_kernel(const float* part, int nb, float clip_norm, float* scale,
+                                  float* norm_out) {
+  const float ss = block_final_sum(part, nb);
+  if (threadIdx.x == 0) {
+    const float gn = sqrtf(ss);
+    float sc = 1.f;
+    if (clip_norm > 0.f) sc = clip_norm * fminf(1.f / gn, 1.f / clip_norm);
+    scale[0] = sc;
+    scale[1] = gn;
+    if (norm_out) norm_out[0] = gn;
+  }
+}
+
+__global__ void momentum_kernel(float* p, float* acc, const float* g, long long n, float lr,
+                                float mom, const float* scale) {
+  const float sc = scale[0];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const float a = mom * acc[i] + g[i] * sc;
+    acc[i] = a;
+    p[i] -= lr * a;
+  }
+}
+
+__global__ void rmsprop_kernel(float* p, float* ms, float* mom, const float* g, long long n,
+                               float lr, float decay, float momentum, float eps,
+                               const float* scale) {
+  const float sc = scale[0];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const float gi = g[i] * sc;
+    const float m2 = decay * ms[i] + (1.f - decay) * gi * gi;
+    ms[i] = m2;
+    const float mo = momentum * mom[i] + lr * gi / sqrtf(m2 + eps);
+    mom[i] = mo;
+    p[i] -= mo;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// batched synthetic Atari stepper (multi_env.py:121-137 + wrappers.py:201-235
+// + wrappers.py:263-323).  One workgroup per env; 1764 words of 4 pixels.
+// ---------------------------------------------------------------------------
+constexpr int FRAME_WORDS = 84 * 84 / 4;
+constexpr uint32_t RESET_TAG = 0xFFFFFFFFu;
+constexpr uint32_t LEN_TAG = 0xFFFFFFFEu;
+constexpr uint32_t REW_SALT = 0x85EBCA6Bu;
+constexpr uint32_t REW_LO = 838861u;      // round(0.05 * 2^24)
+constexpr uint32_t REW_HI = 15938355u;    // 2^24 - REW_LO
+
+__device__ __forceinline__ uint32_t word_hash(uint32_t base, uint32_t g) {
+  return mix32(base ^ (g * 0x9E3779B9u));
+}
+__device__ __forceinline__ int32_t episode_length(uint32_t seed, uint32_t e, uint32_t k) {
+  return 50 + (int32_t)(key4(seed, e, k, LEN_TAG) % 451u);
+}
+
+__global__ __launch_bounds__(256) void env_reset_kernel(acmi_env_state_t st, int env_offset,
+                                                        uint32_t seed, uint8_t* obs,
+                                                        long long stride) {
+  const int n = blockIdx.x;
+  const uint32_t e = (uint32_t)(env_offset + n);
+  const uint32_t base = key4(seed, e, 0u, RESET_TAG);
+  uint4* out = reinterpret_cast<uint4*>(obs + (long long)n * stride);
+  for (int g = threadIdx.x; g < FRAME_WORDS; g += blockDim.x) {
+    const uint32_t w = word_hash(base, (uint32_t)g);
+    uint4 o;
+    o.x = (w & 255u) * 0x01010101u;
+    o.y = ((w >> 8) & 255u) * 0x01010101u;
+    o.z = ((w >> 16) & 255u) * 0x01010101u;
+    o.w = (w >> 24) * 0x01010101u;
+    out[g] = o;
+  }
+  if (threadIdx.x == 0) {
+    st.episode[n] = 0;
+    st.step[n] = 0;
+    st.length[n] = episode_length(seed, e, 0u);
+    st.total[n] = 0.f;
+    st.done[n] = 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void env_step_kernel(
+    acmi_env_state_t st, int env_offset, uint32_t seed, const int32_t* actions,
+    const uint8_t* obs_in, long long in_stride, uint8_t* obs_out, long long out_stride,
+    float* rewards, uint8_t* terminals, float* ep_rewards, long long ld) {
+  const int n = blockIdx.x;
+  const uint32_t e = (uint32_t)(env_offset + n);
+  // every thread reads the (pre-step) state, then a barrier before thread 0
+  // writes the new state
+  const bool was_done = st.done[n] != 0;
+  int32_t k = st.episode[n];
+  int32_t t = st.step[n];
+  int32_t L = st.length[n];
+  float total = st.total[n];
+  __syncthreads();
+  if (was_done) {  // _AutoResetWrapper: reset lazily at the next step
+    k += 1;
+    t = 0;
+    L = episode_length(seed, e, (uint32_t)k);
+    total = 0.f;
+  }
+  t += 1;
+  const uint32_t a = (uint32_t)actions[n] & 255u;
+  const uint32_t base = key4(seed, e, (uint32_t)k, (uint32_t)t * 256u + a);
+  const uint32_t rh = mix32(base ^ REW_SALT) >> 8;
+  const float rew = rh < REW_LO ? -1.f : (rh >= REW_HI ? 1.f : 0.f);
+  const bool term = t >= L;
+  const uint32_t rbase = key4(seed, e, (uint32_t)k, RESET_TAG);
+  const uint4* in = reinterpret_cast<const uint4*>(obs_in + (long long)n * in_stride);
+  uint4* out = reinterpret_cast<uint4*>(obs_out + (long long)n * out_stride);
+  for (int g = threadIdx.x; g < FRAME_WORDS; g += blockDim.x) {
+    uint4 old;
+    if (was_done) {  // FrameStackWrapper.reset: the reset frame repeated 4x
+      const uint32_t w = word_hash(rbase, (uint32_t)g);
+      old.x = (w & 255u) * 0x01010101u;
+      old.y = ((w >> 8) & 255u) * 0x01010101u;
+      old.z = ((w >> 16) & 255u) * 0x01010101u;
+      old.w = (w >> 24) * 0x01010101u;
+    } else {
+      old = in[g];
+    }
+    const uint32_t f = word_hash(base, (uint32_t)g);
+    // np.roll(stack, -1, axis=-1); zero-fill on terminal; last channel = frame
+    uint4 o;
+    o.x = (term ? 0u : (old.x >> 8)) | ((f & 255u) << 24);
+    o.y = (term ? 0u : (old.y >> 8)) | (((f >> 8) & 255u) << 24);
+    o.z = (term ? 0u : (old.z >> 8)) | (((f >> 16) & 255u) << 24);
+    o.w = (term ? 0u : (old.w >> 8)) | ((f >> 24) << 24);
+    out[g] = o;
+  }
+  if (threadIdx.x == 0) {
+    total += rew;
+    rewards[n * ld] = rew;
+    terminals[n * ld] = term ? 1 : 0;
+    ep_rewards[n * ld] = term ? total : __int_as_float(0x7fc00000);
+    st.episode[n] = k;
+    st.step[n] = t;
+    st.length[n] = L;
+    st.total[n] = term ? 0.f : total;
+    st.done[n] = term ? 1 : 0;
+  }
+}
+
+}  // namespace acmi
+
+using namespace acmi;
+
+extern "C" {
+
+int acmi_sample_actions(const float* logits, int ld, int B, int A, uint32_t seed,
+                        uint32_t stream_id, uint32_t counter, const float* uniforms, int mode,
+                        int32_t* actions, int32_t* bad_rows, acmi_stream_t stream) {
+  ACMI_REQUIRE(logits && actions && bad_rows && B >= 0 && A >= 1 && ld >= A, ACMI_ERR_ARG,
+               "acmi_sample_actions: bad arguments");
+  if (B == 0) return ACMI_OK;
+  hipLaunchKernelGGL(sample_kernel, dim3(cdiv(B, 256)), dim3(256), 0, (hipStream_t)stream,
+                     logits, ld, B, A, seed, stream_id, counter, uniforms, mode, actions,
+                     bad_rows);
+  ACMI_LAUNCH_CHECK("acmi_sample_actions");
+  return ACMI_OK;
+}
+
+int acmi_categorical(const float* logits, int ld, int B, int A, const int32_t* actions,
+                     float* entropy, float* log_prob, acmi_stream_t stream) {
+  ACMI_REQUIRE(logits && B >= 0 && A >= 1 && ld >= A && (entropy || log_prob) && (!log_prob || actions),
+               ACMI_ERR_ARG, "acmi_categorical: bad arguments");
+  if (B == 0) return ACMI_OK;
+  hipLaunchKernelGGL(categorical_kernel, dim3(cdiv(B, 256)), dim3(256), 0, (hipStream_t)stream, logits, ld,
+                     B, A, actions, entropy, log_prob);
+  ACMI_LAUNCH_CHECK("acmi_categorical");
+  return ACMI_OK;
+}
+
+int acmi_returns(const float* rewards, const uint8_t* terminals, const float* values,
+                 const float* v_boot, int N, int T, const float* gamma_pow,
+                 const float* boot_pow, float* targets, float* adv, acmi_stream_t stream) {
+  ACMI_REQUIRE(rewards && terminals && values && v_boot && gamma_pow && boot_pow && targets &&
+                   adv && N >= 0 && T >= 1,
+               ACMI_ERR_ARG, "acmi_returns: bad arguments");
+  if (N == 0) return ACMI_OK;
+  hipLaunchKernelGGL(returns_kernel, dim3(cdiv(N, 64)), dim3(64), 0, (hipStream_t)stream,
+                     rewards, terminals, values, v_boot, N, T, gamma_pow, boot_pow, targets,
+                     adv);
+  ACMI_LAUNCH_CHECK("acmi_returns");
+  return ACMI_OK;
+}
+
+int64_t acmi_a2c_loss_ws_floats(int M) { return 3LL * cdiv(M, LOSS_BLOCK) + 16; }
+
+int acmi_a2c_loss(const float* logits, int ld, const float* values, const int32_t* actions,
+                  const float* targets, const float* adv, int M, int A, float beta, float vcoef,
+                  float grad_scale, float* dhead, int ldh, float* ws, float* loss_out,
+                  acmi_stream_t stream) {
+  ACMI_REQUIRE(logits && values && actions && targets && adv && dhead && ws && loss_out &&
+                   M > 0 && A >= 1 && ld >= A && ldh >= A + 1,
+               ACMI_ERR_ARG, "acmi_a2c_loss: bad arguments");
+  const int nb = cdiv(M, LOSS_BLOCK);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(a2c_loss_kernel, dim3(nb), dim3(LOSS_BLOCK), 0, s, logits, ld, values,
+                     actions, targets, adv, M, A, beta, vcoef, grad_scale, dhead, ldh, ws);
+  hipLaunchKernelGGL(a2c_loss_final_kernel, dim3(1), dim3(64), 0, s, ws, nb, M, beta,
+                     loss_out);
+  ACMI_LAUNCH_CHECK("acmi_a2c_loss");
+  return ACMI_OK;
+}
+
+int64_t acmi_opt_ws_floats(int64_t n) { (void)n; return RED_BLOCKS + 16; }
+
+static int clip_prologue(const float* g, long long n, float clip_norm, float* ws,
+                         float* norm_out, hipStream_t s) {
+  hipLaunchKernelGGL(dot_partial_kernel, dim3(RED_BLOCKS), dim3(256), 0, s, g, g, n, ws);
+  hipLaunchKernelGGL(clip_scale_kernel, dim3(1), dim3(256), 0, s, ws, RED_BLOCKS, clip_norm,
+                     ws + RED_BLOCKS, norm_out);
+  ACMI_LAUNCH_CHECK("clip_by_global_norm");
+  return ACMI_OK;
+}
+
+int acmi_momentum_apply(float* params, float* accum, const float* grads, int64_t n, float lr,
+                        float momentum, float clip_norm, float* ws, float* norm_out,
+                        acmi_stream_t stream) {
+  ACMI_REQUIRE(params && accum && grads && ws && n > 0, ACMI_ERR_ARG,
+               "acmi_momentum_apply: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  int rc = clip_prologue(grads, n, clip_norm, ws, norm_out, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(momentum_kernel, dim3(std::min<long long>(cdiv(n, 256), 2048)), dim3(256),
+                     0, s, params, accum, grads, (long long)n, lr, momentum, ws + RED_BLOCKS);
+  ACMI_LAUNCH_CHECK("acmi_momentum_apply");
+  return ACMI_OK;
+}
+
+int acmi_rmsprop_apply(float* params, float* ms, float* mom, const float* grads, int64_t n,
+                       float lr, float decay, float momentum, float eps, float clip_norm,
+                       float* ws, float* norm_out, acmi_stream_t stream) {
+  ACMI_REQUIRE(params && ms && mom && grads && ws && n > 0, ACMI_ERR_ARG,
+               "acmi_rmsprop_apply: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  int rc = clip_prologue(grads, n, clip_norm, ws, norm_out, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rmsprop_kernel, dim3(std::min<long long>(cdiv(n, 256), 2048)), dim3(256),
+                     0, s, params, ms, mom, grads, (long long)n, lr, decay, momentum, eps,
+                     ws + RED_BLOCKS);
+  ACMI_LAUNCH_CHECK("acmi_rmsprop_apply");
+  return ACMI_OK;
+}
+
+int acmi_env_reset(const acmi_env_state_t* st, int N, int env_offset, uint32_t seed,
+                   uint8_t* obs_out, int64_t out_stride, acmi_stream_t stream) {
+  ACMI_REQUIRE(st && obs_out && N >= 0 && out_stride >= 84 * 84 * 4 && out_stride % 16 == 0,
+               ACMI_ERR_ARG, "acmi_env_reset: bad arguments");
+  if (N == 0) return ACMI_OK;
+  hipLaunchKernelGGL(env_reset_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, *st,
+                     env_offset, seed, obs_out, (long long)out_stride);
+  ACMI_LAUNCH_CHECK("acmi_env_reset");
+  return ACMI_OK;
+}
+
+int acmi_env_step(const acmi_env_state_t* st, int N, int env_offset, uint32_t seed,
+                  const int32_t* actions, const uint8_t* obs_in, int64_t in_stride,
+                  uint8_t* obs_out, int64_t out_stride, float* rewards, uint8_t* terminals,
+                  float* episode_rewards, int64_t ld, acmi_stream_t stream) {
+  ACMI_REQUIRE(st && actions && obs_in && obs_out && rewards && terminals && episode_rewards &&
+                   N >= 0 && in_stride % 16 == 0 && out_stride % 16 == 0 && ld >= 1,
+               ACMI_ERR_ARG, "acmi_env_step: bad arguments");
+  if (N == 0) return ACMI_OK;
+  hipLaunchKernelGGL(env_step_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, *st,
+                     env_offset, seed, actions, obs_in, (long long)in_stride, obs_out,
+                     (long long)out_stride, rewards, terminals, episode_rewards,
+                     (long long)ld);
+  ACMI_LAUNCH_CHECK("acmi_env_step");
+  return ACMI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,172 @@
+"""ACKTR (or A2C) env-steps/s on synthetic Breakout 84x84x4 — the BASELINE.json metric.
+
+One step = one full training iteration of the reference loop (a2c_acktr.py:104-137):
+``agent.interact`` (T-step device rollout: tower forward, sampling, batched stepper)
++ ``session.run(optimize_op)`` (targets, losses, backward fused with the K-FAC
+A statistics, sampled-loss backward for the G statistics, RCCL all-reduce when
+N > 1, EMA, the damped inverses every 10th update, the preconditioned trust-region
+momentum step).  The global step starts after the 30-update cold start (the timed
+iterations are steady-state K-FAC iterations, inverse included at its natural 1/10
+rate).  Weak scaling: every GPU runs --envs-per-gpu envs (default 512 = the 8x512
+shard of BASELINE.json configs[3]).
+
+  python bench.py --gpus N --steps K --warmup W
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, 'actor-critic_amd'), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32-input MFMA peak
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=5)
+    p.add_argument('--algo', choices=['acktr', 'a2c'], default='acktr')
+    p.add_argument('--envs-per-gpu', type=int, default=512)
+    p.add_argument('--nsteps', type=int, default=None, help='rollout length T (ACKTR 20, A2C 5)')
+    p.add_argument('--num-actions', type=int, default=4, help='Breakout: 4')
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--cpu-iters', type=int, default=3)
+    p.add_argument('--quiet', action='store_true')
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    from actorcritic import _lib, parallel
+    from actorcritic import session as sess
+    from actorcritic.agents import MultiEnvAgent
+    from actorcritic.envs.atari.model import AtariModel
+    from actorcritic.envs.atari.wrappers import SyntheticAtariEnvs
+    from actorcritic.examples.atari.a2c_acktr import create_optimizer
+    from actorcritic.multi_env import MultiEnv
+    from actorcritic.nn import linear_decay
+    from actorcritic.objectives import A2CObjective
+
+    world, rank = parallel.init_from_env()
+    if world != args.gpus and rank == 0:
+        print('warning: --gpus {} but WORLD_SIZE {}'.format(args.gpus, world), file=sys.stderr)
+    dev = torch.device('cuda', torch.cuda.current_device())
+    acktr = args.algo == 'acktr'
+    N = args.envs_per_gpu
+    T = args.nsteps or (20 if acktr else 5)
+    C3 = 32 if acktr else 64
+    A = args.num_actions
+
+    sess.reset_default_graph()
+    env = MultiEnv(SyntheticAtariEnvs(N, num_actions=A, seed=1234, env_offset=rank * N, device=dev))
+    model = AtariModel(env.observation_space, env.action_space, C3, random_seed=7, device=dev)
+    agent = MultiEnvAgent(env, model, T)
+    objective = A2CObjective(model, discount_factor=0.99, entropy_regularization_strength=0.01)
+    gs = sess.get_or_create_global_step()
+    max_step = 10000000 / (N * T * world)
+    lr = linear_decay(0.25, 0.025, gs, max_step) if acktr else linear_decay(7e-4, 7e-5, gs, max_step)
+    optimizer = create_optimizer(acktr, model, lr)
+    op = objective.optimize_shared(optimizer, baseline_loss_weight=0.5, global_step=gs)
+    if acktr:
+        gs.assign(30)  # steady state: past the cold start (kfac_utils.py:42-44)
+
+    def iteration(s, marks=None):
+        if marks is not None:
+            marks[0].record()
+        obs, act, rew, term, nxt, infos = agent.interact(s)
+        if marks is not None:
+            marks[1].record()
+        s.run(op, feed_dict={model.observations_placeholder: obs, model.bootstrap_observations_placeholder: nxt,
+                             model.actions_placeholder: act, model.rewards_placeholder: rew,
+                             model.terminals_placeholder: term}, host=False)
+        if marks is not None:
+            marks[2].record()
+
+    with sess.Session(dev) as s:
+        for _ in range(args.warmup):
+            iteration(s)
+        torch.cuda.synchronize()
+        parallel.barrier()
+        torch.cuda.synchronize()
+        site = _lib.PROF_CONV1_WGRAD
+        _lib.call('acmi_prof_enable', site, max(1, args.steps))
+        marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        inv_flags = []
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            iteration(s, marks[k])
+            inv_flags.append(bool(getattr(optimizer, 'last_flags', (0, 0, 0))[2]) if acktr else False)
+        torch.cuda.synchronize()
+        parallel.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        tot_ms, cnt = ctypes.c_double(), ctypes.c_int()
+        _lib.call('acmi_prof_collect', ctypes.byref(tot_ms), ctypes.byref(cnt))
+        _lib.call('acmi_prof_enable', 0, 0)
+    elapsed = parallel.max_over_ranks(elapsed, dev)
+    roll_ms = [m[0].elapsed_time(m[1]) for m in marks]
+    upd_ms = [m[1].elapsed_time(m[2]) for m in marks]
+    env_steps = N * T * args.steps * world
+    value = env_steps / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+    upd_inv = [u for u, f in zip(upd_ms, inv_flags) if f]
+    upd_plain = [u for u, f in zip(upd_ms, inv_flags) if not f]
+    mean = lambda xs: (sum(xs) / len(xs)) if xs else None
+
+    # dominant kernel: conv1 weight gradient fused with the K-FAC A factor,
+    # [P;1]^T [P | dY | 1] over M*400 patch rows: algorithmic 2*400*257*(257+32)
+    # FLOP per sample (A factor 257^2 + dW 257x32 per conv1 location)
+    M = N * T
+    kern_flops = 2.0 * 400 * 257 * (257 + 32) * M if acktr else 2.0 * 400 * 257 * 32 * M
+    kern_ms = tot_ms.value / max(1, cnt.value)
+    achieved = kern_flops / (kern_ms * 1e-3) / 1e12 if cnt.value else None
+    roofline = {'bound': 'mfma', 'kernel': 'conv1 wgrad+A-factor reduction GEMM (f32 MFMA)',
+                'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                'frac': (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None, 'traffic': None,
+                'launches': cnt.value, 'avg_ms': kern_ms, 'flops_per_launch': kern_flops}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+        import cpu_baseline
+        r = cpu_baseline.run(n_envs=32, n_steps=20 if acktr else 5, iters=args.cpu_iters, A=A, C3=C3)
+        cpu = {'value': r['env_steps_per_s'], 'unit': 'env-steps/s', 'cores': r['threads'], 'kind': 'port',
+               'sample': '{} iterations of the reference {} config ({} envs x {} steps), numpy float32 '
+                         'oracle port, inverse amortised 1/10'.format(r['iters'], args.algo.upper(),
+                                                                      r['n_envs'], r['n_steps']),
+               'update_ms': r['update_ms']}
+
+    if rank == 0:
+        out = {
+            'metric': 'env-steps/sec (whole node) + ACKTR update ms, Breakout 84x84x4',
+            'value': value, 'unit': 'env-steps/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': ms_per_step, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+            'dtype': 'fp32', 'data': 'synthetic (hashed 84x84 u8 frames, random-init orthogonal weights)',
+            'config': {'workload': 'Breakout {} {} envs/GPU x {} steps (BASELINE configs[3] shard)'.format(
+                args.algo.upper(), N, T), 'algo': args.algo, 'envs_per_gpu': N, 'num_steps': T,
+                'global_envs': N * world, 'num_actions': A, 'conv3_filters': C3,
+                'parallelism': 'dp{}'.format(world)},
+            'update_ms': mean(upd_ms), 'update_ms_inverse_iters': mean(upd_inv),
+            'update_ms_plain_iters': mean(upd_plain), 'rollout_ms': mean(roll_ms),
+            'roofline': roofline, 'cpu_baseline': cpu,
+        }
+        if cpu:
+            out['speedup_vs_cpu'] = value / cpu['value']
+        print(json.dumps(out))
+    parallel.destroy()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,306 @@
+/*
+ * acmi.h — C-ABI of libacmi, the MI355X-native (gfx950) A2C/ACKTR hot path.
+ *
+ * Drop-in boundary for the reference's TF graph + kfac ops on the rollout and
+ * update path of jrobine/actor-critic.  Every entry point
+ *   - takes caller-owned DEVICE buffers (plain pointers, sizes, no torch types),
+ *   - is stream-ordered on `stream` (a hipStream_t), asynchronous, never
+ *     allocates and never synchronises (so a caller may capture it in a graph),
+ *   - returns 0 (ACMI_OK) or a negative ACMI_ERR_* code; the message is in
+ *     acmi_last_error() (thread-local).
+ *
+ * Reference interface each entry point replaces is cited as path:line into
+ * /root/reference.  Layouts: NHWC u8 observations,
+ * HWIO conv weights, [in,out] FC weights (reference nn.py:8-84), fp32 math.
+ */
+#ifndef ACMI_H_
+#define ACMI_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACMI_ABI_VERSION 1
+
+enum {
+  ACMI_OK = 0,
+  ACMI_ERR_ARG = -1,   /* bad shape / null pointer / unsupported size   */
+  ACMI_ERR_HIP = -2,   /* a HIP launch failed                             */
+  ACMI_ERR_WS = -3,    /* caller workspace too small                      */
+};
+
+typedef void* acmi_stream_t; /* hipStream_t */
+
+const char* acmi_last_error(void);
+int acmi_abi_version(void);
+
+/* ------------------------------------------------------------------------
+ * Model layout.  Replaces AtariModel._build_params
+ * (actorcritic/envs/atari/model.py:129-170, nn.py:8-84).
+ * The flat fp32 parameter vector holds, in order:
+ *   conv1.W[8][8][4][32] conv1.b[32] conv2.W[4][4][32][64] conv2.b[64]
+ *   conv3.W[3][3][64][C3] conv3.b[C3] fc4.W[49*C3][512] fc4.b[512]
+ *   pi.W[512][A] pi.b[A] v.W[512][1] v.b[1]
+ * so each layer's homogeneous weight matrix [W; b] ((K+1) x Cout, the K-FAC
+ * block of envs/atari/model.py:219-246) is one contiguous row-major slice.
+ * ---------------------------------------------------------------------- */
+#define ACMI_NUM_LAYERS 6   /* conv1 conv2 conv3 fc4 fc_policy fc_baseline */
+#define ACMI_NUM_AFACT 5    /* fc_policy and fc_baseline share one A factor */
+#define ACMI_NUM_GFACT 6
+
+typedef struct acmi_net {
+  int num_actions;     /* A  (Breakout 4, full Atari 18); 1 <= A <= 64    */
+  int conv3_filters;   /* C3 (32 ACKTR, 64 A2C: a2c_acktr.py:51-53)       */
+  const float* params; /* device, acmi_param_count() floats               */
+} acmi_net_t;
+
+int64_t acmi_param_count(int num_actions, int conv3_filters);
+/* off[2*l] = W offset, off[2*l+1] = b offset of layer l (12 entries)       */
+int acmi_param_offsets(int num_actions, int conv3_filters, int64_t* off12);
+
+/* K-FAC block geometry: din[l] = K_l + 1 (homogeneous), dout[l] = Cout_l.
+ * stat_off[0..4] = offsets of A factors (din^2 each, A4 shared by l=4,5),
+ * stat_off[5..10] = offsets of G factors (dout^2), *total = floats overall. */
+int acmi_kfac_layout(int num_actions, int conv3_filters, int64_t* din6,
+                     int64_t* dout6, int64_t* stat_off11, int64_t* total);
+
+/* ------------------------------------------------------------------------
+ * Forward.  Replaces the TF graph of AtariModel.__init__/_build_layers
+ * (envs/atari/model.py:77-217): u8/255 normalise (:92-95), conv1 8x8 s4,
+ * conv2 4x4 s2, conv3 3x3 s1 (VALID, +bias, ReLU), NHWC flatten, fc4 512
+ * ReLU, policy logits and value heads.  `obs` holds B NHWC u8 images
+ * [84][84][4]; image b starts at obs + b*img_stride (bytes), which lets the
+ * rollout read step t of a [N][T][84][84][4] buffer in place.
+ * ---------------------------------------------------------------------- */
+typedef struct acmi_acts {
+  float* a1;     /* [B][20][20][32] post-ReLU                               */
+  float* a2;     /* [B][9][9][64]                                           */
+  float* a3;     /* [B][7][7][C3]  (= the NHWC-flattened fc4 input)         */
+  float* a4;     /* [B][512]                                                */
+  float* logits; /* [B][ld_logits]                                          */
+  float* value;  /* [B]  (may be NULL when want_value == 0)                 */
+  int ld_logits;
+} acmi_acts_t;
+
+int acmi_forward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride,
+                 int B, const acmi_acts_t* acts, int want_value,
+                 acmi_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Categorical sampling.  Replaces Categorical.sample (tf.multinomial) and
+ * the squeeze of policies.py:86, model.py:135-151.  Counter-based RNG:
+ * u = u01(key4(seed, stream_id, counter, row)); when `uniforms` is non-NULL
+ * it supplies u[row] instead (parity tests).  Inverse-CDF over softmax in
+ * f32.  A row with a NaN/inf logit yields action -1 and sets *bad_rows
+ * (device int, accumulated) — the reference would instead emit index A and
+ * fail later in sparse_softmax_cross_entropy (README.md:53-54).
+ * mode != 0 -> argmax (Categorical.mode, model.py:153-169).
+ * ---------------------------------------------------------------------- */
+int acmi_sample_actions(const float* logits, int ld, int B, int A,
+                        uint32_t seed, uint32_t stream_id, uint32_t counter,
+                        const float* uniforms, int mode, int32_t* actions,
+                        int32_t* bad_rows, acmi_stream_t stream);
+
+/* Per-row Categorical.entropy and log_prob(actions) (policies.py:87-89);
+ * either output may be NULL (log_prob needs actions). */
+int acmi_categorical(const float* logits, int ld, int B, int A,
+                     const int32_t* actions, float* entropy, float* log_prob,
+                     acmi_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * n-step targets and advantage.  Replaces objectives.py:123-130 with the
+ * py_func closures _discount (:178-202) and _discount_bootstrap (:205-214).
+ * Batch-major [N][T].  gamma_pow[k] = f32(gamma)**f32(k) (numpy float32
+ * power, exactly the D-matrix entries of objectives.py:183-187), k < T;
+ * boot_pow[k] = k-fold sequential f32 product of f32(gamma) (the float32
+ * cumprod of objectives.py:211), k <= T.  Both tables are host-computed.
+ * target[n,t] = sum_{i=t..stop} r[n,i]*gamma_pow[i-t] (ascending i, no FMA,
+ *              stop = first terminal >= t)  +  boot_pow[T-t]*v_boot[n] (if no
+ *              terminal in t..T-1);   adv = target - value.
+ * ---------------------------------------------------------------------- */
+int acmi_returns(const float* rewards, const uint8_t* terminals,
+                 const float* values, const float* v_boot, int N, int T,
+                 const float* gamma_pow, const float* boot_pow, float* targets,
+                 float* adv, acmi_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * A2C losses and their gradient w.r.t. the head outputs.  Replaces
+ * objectives.py:132-154 and the head part of tf.gradients of
+ * L = L_pi + vcoef*L_v (objectives.py:78).  M = N*T rows.
+ *   L_pi = -(mean(adv*logpi(a)) + beta*mean(H)),  L_v = mean((target-V)^2/2)
+ * dhead[m][0..A-1] = dL/dlogits, dhead[m][A] = dL/dV, row stride ldh >= A+1,
+ * each scaled by grad_scale (1/world_size for data-parallel means).
+ * loss_out[0..2] = (L_pi, L_v, mean entropy) — deterministic two-pass sums.
+ * ws: >= acmi_a2c_loss_ws_floats(M) floats.
+ * ---------------------------------------------------------------------- */
+int64_t acmi_a2c_loss_ws_floats(int M);
+int acmi_a2c_loss(const float* logits, int ld, const float* values,
+                  const int32_t* actions, const float* targets,
+                  const float* adv, int M, int A, float beta, float vcoef,
+                  float grad_scale, float* dhead, int ldh, float* ws,
+                  float* loss_out, acmi_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Backward through the tower (the rest of tf.gradients, objectives.py:78)
+ * fused with the K-FAC input-factor statistics (kfac cov_update_thunks,
+ * kfac_utils.py:39,44; registration envs/atari/model.py:219-246):
+ *   grads  <- dL/dparams in the param layout (overwritten)
+ *   a_stats (nullable) <- for l = 0..4: A_l = mean over rows of [x;1][x;1]^T
+ *           (conv: x = the (kh,kw,cin) input patch at every output location,
+ *            rows = B*locations; fc: x = the input row; A_4 = fc4 output).
+ * dhead: [B][ldh] from acmi_a2c_loss.  d1..d4 are [B]x(layer output) scratch.
+ * ws: >= acmi_backward_ws_floats(B, A, C3) floats.
+ * ---------------------------------------------------------------------- */
+typedef struct acmi_bwd {
+  float* d1; /* [B][20][20][32] */
+  float* d2; /* [B][9][9][64]   */
+  float* d3; /* [B][7][7][C3]   */
+  float* d4; /* [B][512]        */
+  const float* dhead;
+  int ldh;
+} acmi_bwd_t;
+
+int64_t acmi_backward_ws_floats(int B, int num_actions, int conv3_filters);
+int acmi_backward(const acmi_net_t* net, const uint8_t* obs,
+                  int64_t img_stride, int B, const acmi_acts_t* acts,
+                  const acmi_bwd_t* bwd, float* grads, float* a_stats,
+                  float* ws, acmi_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * K-FAC output-factor statistics (kfac "gradients" estimation mode over the
+ * predictive distributions registered at policies.py:146-158 and
+ * baselines.py:55-69): y_pi ~ Categorical(logits) and y_v ~ N(V, 1) are
+ * sampled with the counter RNG (seed, stream_id, counter); the per-example
+ * gradients of -log p(y) w.r.t. each registered layer output are
+ * back-propagated (dX only) and G_l = mean over rows of g g^T is written to
+ * g_stats (layout of acmi_kfac_layout, G part).  Reuses bwd->d1..d4 and ws.
+ * ---------------------------------------------------------------------- */
+int acmi_kfac_output_stats(const acmi_net_t* net, int B,
+                           const acmi_acts_t* acts, const acmi_bwd_t* bwd,
+                           uint32_t seed, uint32_t stream_id, uint32_t counter,
+                           float* g_stats, float* ws, acmi_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * K-FAC running factors: zero-initialised EMA with zero-debias (kfac
+ * FisherFactor cov update with cov_ema_decay, a2c_acktr.py:245):
+ *   biased = decay*biased + (1-decay)*stats;  factors = biased * debias
+ * (debias = 1/(1-decay^t), host-computed).  n floats.
+ * ---------------------------------------------------------------------- */
+int acmi_kfac_ema(float* biased, float* factors, const float* stats,
+                  int64_t n, float decay, float debias, float stats_scale,
+                  acmi_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Damped inverses (kfac inv_update_thunks, kfac_utils.py:46-50): per layer
+ *   lambda_l = damping / (conv_normalize && l<3 ? locations_l : 1)
+ *   pi_l = sqrt((tr A_l / din_l) / (tr G_l / dout_l))
+ *   Ainv_l = (A_l + pi_l*sqrt(lambda_l) I)^-1,  Ginv_l = (G_l + sqrt(lambda_l)/pi_l I)^-1
+ * computed in fp64 (block Gauss-Jordan, SPD, no pivoting) and stored f32.
+ * inv layout: for l = 0..5: Ainv_l (din^2) then Ginv_l (dout^2).
+ * ws: >= acmi_kfac_inverse_ws_doubles(...) doubles.
+ * ---------------------------------------------------------------------- */
+int64_t acmi_kfac_inverse_floats(int num_actions, int conv3_filters);
+int64_t acmi_kfac_inverse_ws_doubles(int num_actions, int conv3_filters);
+int acmi_kfac_inverse(int num_actions, int conv3_filters,
+                      const float* factors, float damping, int conv_normalize,
+                      float* inv, double* ws, acmi_stream_t stream);
+
+/* Eigendecomposition of every damped-factor input (fp64 cyclic Jacobi):
+ * eigenvalues (ascending) of A_l / G_l written to `eigvals` in the factor
+ * layout order (diagnostic and parity path; north_star "KFAC eigenvalues"). */
+int64_t acmi_kfac_eig_ws_doubles(int num_actions, int conv3_filters);
+int acmi_kfac_eigvals(int num_actions, int conv3_filters, const float* factors,
+                      double* eigvals, double* ws, acmi_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Natural-gradient step (KfacOptimizer.apply_gradients, kfac_utils.py:53,
+ * a2c_acktr.py:243-246):  Delta_l = Ainv_l [dW_l; db_l] Ginv_l;
+ *   coeff = min(1, sqrt(norm_constraint / (lr^2 * sum_l <g_l, Delta_l>)));
+ *   v = momentum*v + coeff*Delta;   params -= lr*v.
+ * coeff is computed on the device (no host round trip); *coeff_out gets it.
+ * ws: >= acmi_kfac_step_ws_floats() floats.
+ * ---------------------------------------------------------------------- */
+int64_t acmi_kfac_step_ws_floats(int num_actions, int conv3_filters);
+int acmi_kfac_step(int num_actions, int conv3_filters, float* params,
+                   float* velocity, const float* grads, const float* inv,
+                   float lr, float momentum, float norm_constraint,
+                   float* precon, float* ws, float* coeff_out,
+                   acmi_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * First-order optimizers.  ClipGlobalNormOptimizer (nn.py:159-189) + TF1
+ * MomentumOptimizer (cold start, a2c_acktr.py:240-241) / RMSPropOptimizer
+ * (a2c_acktr.py:250-251, decay .9, momentum 0, eps 1e-10, ms init 1).
+ * clip_norm <= 0 disables clipping.  norm_out (nullable) <- global norm.
+ * ---------------------------------------------------------------------- */
+int64_t acmi_opt_ws_floats(int64_t n);
+int acmi_momentum_apply(float* params, float* accum, const float* grads,
+                        int64_t n, float lr, float momentum, float clip_norm,
+                        float* ws, float* norm_out, acmi_stream_t stream);
+int acmi_rmsprop_apply(float* params, float* ms, float* mom,
+                       const float* grads, int64_t n, float lr, float decay,
+                       float momentum, float eps, float clip_norm, float* ws,
+                       float* norm_out, acmi_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Batched synthetic Atari stepper — replaces MultiEnv.step/reset over
+ * SubprocessEnv (multi_env.py:49-81, 121-137, 140-362) with the semantics
+ * of FrameStackWrapper (wrappers.py:201-235) and EpisodeInfoWrapper
+ * (wrappers.py:263-323).  Frames are 84x84 u8 from mix32 of
+ * (seed, env, episode, step, action); rewards in {-1,0,1} w.p. .05/.9/.05;
+ * episode length 50 + (hash % 451).  State arrays are per env ([N]).
+ * Stacks are NHWC [84][84][4] u8; env n reads obs_in + n*in_stride and
+ * writes obs_out + n*out_stride (in-place allowed).
+ * ---------------------------------------------------------------------- */
+typedef struct acmi_env_state {
+  int32_t* episode;   /* episode index                                    */
+  int32_t* step;      /* steps taken in the current episode               */
+  int32_t* length;    /* terminal step of the current episode             */
+  float* total;       /* EpisodeInfoWrapper.total_reward                   */
+  uint8_t* done;      /* _AutoResetWrapper._terminated                     */
+} acmi_env_state_t;
+
+int acmi_env_reset(const acmi_env_state_t* st, int N, int env_offset,
+                   uint32_t seed, uint8_t* obs_out, int64_t out_stride,
+                   acmi_stream_t stream);
+/* rewards/terminals/episode_rewards: element n at [n*ld]; episode_rewards
+ * gets the episode total at a terminal step and NaN otherwise.           */
+int acmi_env_step(const acmi_env_state_t* st, int N, int env_offset,
+                  uint32_t seed, const int32_t* actions, const uint8_t* obs_in,
+                  int64_t in_stride, uint8_t* obs_out, int64_t out_stride,
+                  float* rewards, uint8_t* terminals, float* episode_rewards,
+                  int64_t ld, acmi_stream_t stream);
+
+/* Rollout variant of acmi_forward: batch row b reads image b of `obs` and
+ * writes activation row b*act_img_stride (env-major [N][T] buffers, the
+ * pointers in *acts pre-offset by step t), so step t of a T-step rollout
+ * lands where the update expects it and the update re-uses it. */
+int acmi_forward_strided(const acmi_net_t* net, const uint8_t* obs,
+                         int64_t img_stride, int B, const acmi_acts_t* acts,
+                         int want_value, int64_t act_img_stride,
+                         acmi_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Building blocks exposed for parity tests and the bench (not needed by a
+ * reference-shaped caller).
+ * ---------------------------------------------------------------------- */
+/* C[M][N] = A[M][K] @ B[K][N], row-major fp32, f32-input MFMA */
+int acmi_gemm_f32(const float* A, const float* B, float* C, int M, int N,
+                  int K, acmi_stream_t stream);
+
+/* Launch-site timing for the bench: while enabled, HIP events are recorded on
+ * the launch stream around every launch of `site` (up to `capacity`);
+ * acmi_prof_collect synchronises them and returns the summed milliseconds
+ * and the count, then rearms.  site 0 disables.  Not graph-capture safe. */
+#define ACMI_PROF_CONV1_WGRAD 1 /* conv1 [P;1]^T [P | dY | 1] reduction GEMM */
+#define ACMI_PROF_CONV2_WGRAD 2
+#define ACMI_PROF_CONV1_FWD 3
+int acmi_prof_enable(int site, int capacity);
+int acmi_prof_collect(double* total_ms, int* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACMI_H_ */

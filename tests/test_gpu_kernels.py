@@ -1,0 +1,241 @@
+"""Kernel-level parity of libacmi against plain PyTorch float64 references on the CPU.
+
+These are the early numerics checks for the f32 MFMA GEMM engine (forward, input
+gradients, fused weight-gradient/A-factor reductions), the fp64 damped inverse, the
+trust-region step and the optimizers.  Tolerances are written per check.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from actorcritic import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _net(params, A, C3):
+    return _lib.Net(A, C3, params.data_ptr())
+
+
+def _layout(A, C3):
+    off = (ctypes.c_int64 * 12)()
+    _lib.call('acmi_param_offsets', A, C3, off)
+    return list(off), _lib.load().acmi_param_count(A, C3)
+
+
+def _split(params, A, C3):
+    off, n = _layout(A, C3)
+    shapes = [(8, 8, 4, 32), (32,), (4, 4, 32, 64), (64,), (3, 3, 64, C3), (C3,), (49 * C3, 512), (512,),
+              (512, A), (A,), (512, 1), (1,)]
+    ends = off[1:] + [n]
+    return [params[o:e].reshape(s) for o, e, s in zip(off, ends, shapes)]
+
+
+def torch_forward(params, obs_u8, A, C3):
+    """float64 CPU reference of envs/atari/model.py:92-217 (NHWC, VALID)."""
+    w1, b1, w2, b2, w3, b3, w4, b4, wp, bp, wv, bv = [t.double().cpu() for t in _split(params, A, C3)]
+    x = obs_u8.cpu().double() / 255.0
+    x = x.permute(0, 3, 1, 2)
+
+    def conv(x, w, b, s):
+        return torch.relu(torch.nn.functional.conv2d(x, w.permute(3, 2, 0, 1), b, stride=s))
+
+    a1 = conv(x, w1, b1, 4)
+    a2 = conv(a1, w2, b2, 2)
+    a3 = conv(a2, w3, b3, 1)
+    a3f = a3.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+    a4 = torch.relu(a3f @ w4 + b4)
+    logits = a4 @ wp + bp
+    value = (a4 @ wv + bv)[:, 0]
+    nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous()
+    return nhwc(a1), nhwc(a2), a3f, a4, logits, value
+
+
+def rand_params(A, C3, device, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    n = _lib.load().acmi_param_count(A, C3)
+    p = torch.empty(n, dtype=torch.float32)
+    off, _ = _layout(A, C3)
+    fans = [256, 1, 512, 1, 576, 1, 49 * C3, 1, 512, 1, 512, 1]
+    ends = off[1:] + [n]
+    for o, e, f in zip(off, ends, fans):
+        p[o:e] = torch.randn(e - o, generator=g) * (scale * (2.0 / f) ** 0.5 if f > 1 else 0.1)
+    return p.to(device)
+
+
+def alloc_acts(B, A, C3, device):
+    z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=device)
+    t = dict(a1=z(B, 20, 20, 32), a2=z(B, 9, 9, 64), a3=z(B, 7, 7, C3), a4=z(B, 512), logits=z(B, A),
+             value=z(B))
+    acts = _lib.Acts(*[t[k].data_ptr() for k in ('a1', 'a2', 'a3', 'a4', 'logits', 'value')], A)
+    return t, acts
+
+
+@pytest.mark.parametrize('M,N,K', [(128, 128, 32), (300, 260, 200), (1, 4, 4), (1000, 64, 1568)])
+def test_gemm_f32(lib, cuda, M, N, K):
+    g = torch.Generator().manual_seed(1)
+    a = torch.randn(M, K, generator=g)
+    b = torch.randn(K, N, generator=g)
+    c = torch.zeros(M, N, device=cuda)
+    a_d, b_d = a.to(cuda), b.to(cuda)  # keep device copies alive until the kernel has run
+    _lib.call('acmi_gemm_f32', _lib.ptr(a_d), _lib.ptr(b_d), _lib.ptr(c), M, N, K, _lib.stream_handle())
+    torch.cuda.synchronize()
+    ref = a.double() @ b.double()
+    err = (c.cpu().double() - ref).abs().max().item()
+    # exact-f32 fmaf chain: error ~ K * eps * max|a||b|
+    assert err <= 2e-6 * K * ref.abs().max().item() / max(1.0, K ** 0.5), err
+
+
+@pytest.mark.parametrize('A,C3,B', [(4, 32, 3), (18, 64, 5), (4, 32, 67)])
+def test_forward_matches_torch(lib, cuda, A, C3, B):
+    params = rand_params(A, C3, cuda)
+    g = torch.Generator().manual_seed(2)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8)
+    t, acts = alloc_acts(B, A, C3, cuda)
+    net = _net(params, A, C3)
+    obs_d = obs.to(cuda)
+    _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs_d), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+              _lib.stream_handle())
+    torch.cuda.synchronize()
+    ref = torch_forward(params, obs, A, C3)
+    names = ['a1', 'a2', 'a3', 'a4', 'logits', 'value']
+    for name, r in zip(names, ref):
+        got = t[name].cpu().double().reshape(r.shape)
+        rel = (got - r).abs().max().item() / max(1e-6, r.abs().max().item())
+        assert rel < 1e-5, (name, rel)
+
+
+def test_backward_and_astats_match_torch(lib, cuda):
+    A, C3, B = 4, 32, 6
+    params = rand_params(A, C3, cuda, seed=3)
+    g = torch.Generator().manual_seed(4)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8)
+    t, acts = alloc_acts(B, A, C3, cuda)
+    net = _net(params, A, C3)
+    obs_d = obs.to(cuda)
+    _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs_d), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+              _lib.stream_handle())
+    ldh = 8
+    dhead = torch.zeros(B, ldh)
+    dhead[:, :A + 1] = torch.randn(B, A + 1, generator=g)
+    dhead_d = dhead.to(cuda)
+    z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=cuda)
+    d = dict(d1=z(B, 20, 20, 32), d2=z(B, 9, 9, 64), d3=z(B, 7, 7, C3), d4=z(B, 512))
+    bwd = _lib.Bwd(d['d1'].data_ptr(), d['d2'].data_ptr(), d['d3'].data_ptr(), d['d4'].data_ptr(),
+                   dhead_d.data_ptr(), ldh)
+    n = params.numel()
+    grads = z(n)
+    din = (ctypes.c_int64 * 6)()
+    dout = (ctypes.c_int64 * 6)()
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, din, dout, so, ctypes.byref(tot))
+    astat = z(tot.value)
+    ws = z(lib.acmi_backward_ws_floats(B, A, C3))
+    _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs_d), 84 * 84 * 4, B, ctypes.byref(acts),
+              ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), _lib.stream_handle())
+    torch.cuda.synchronize()
+    # reference gradients by autograd in float64
+    p64 = params.cpu().double().requires_grad_(True)
+    a1, a2, a3f, a4, logits, value = torch_forward(p64, obs, A, C3)
+    loss = (logits * dhead[:, :A].double()).sum() + (value * dhead[:, A].double()).sum()
+    loss.backward()
+    ref = p64.grad
+    got = grads.cpu().double()
+    off, _ = _layout(A, C3)
+    ends = off[1:] + [n]
+    for i, (o, e) in enumerate(zip(off, ends)):
+        r = ref[o:e]
+        rel = (got[o:e] - r).abs().max().item() / max(1e-12, r.abs().max().item())
+        assert rel < 2e-5, ('param block', i, rel)
+    # A factors: mean over rows of [x;1][x;1]^T
+    x = obs.double() / 255.0
+
+    def patches(x, k, s):
+        p = x.unfold(1, k, s).unfold(2, k, s)  # B, OH, OW, C, KH, KW
+        return p.permute(0, 1, 2, 4, 5, 3).reshape(-1, k * k * x.shape[-1])
+
+    ins = [patches(x, 8, 4), patches(a1.detach(), 4, 2), patches(a2.detach(), 3, 1), a3f.detach(), a4.detach()]
+    a_host = astat.cpu().double()
+    for f, xin in enumerate(ins):
+        xb = torch.cat([xin, torch.ones(xin.shape[0], 1, dtype=xin.dtype)], 1)
+        r = xb.t() @ xb / xb.shape[0]
+        got_f = a_host[so[f]:so[f] + din[f] * din[f]].reshape(din[f], din[f])
+        rel = (got_f - r).abs().max().item() / r.abs().max().item()
+        assert rel < 2e-5, ('A factor', f, rel)
+
+
+def test_kfac_inverse_matches_numpy(lib, cuda):
+    A, C3 = 4, 32
+    din = (ctypes.c_int64 * 6)()
+    dout = (ctypes.c_int64 * 6)()
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, din, dout, so, ctypes.byref(tot))
+    rng = np.random.default_rng(5)
+    fac = np.zeros(tot.value, np.float32)
+    mats = []
+    for f in range(11):
+        n = din[f] if f < 5 else dout[f - 5]
+        x = rng.standard_normal((max(n // 2, 1) + 3, n)).astype(np.float64)
+        m = (x.T @ x / x.shape[0]).astype(np.float32)
+        fac[so[f]:so[f] + n * n] = m.ravel()
+        mats.append(m.astype(np.float64))
+    fac_d = torch.from_numpy(fac).to(cuda)
+    inv = torch.zeros(lib.acmi_kfac_inverse_floats(A, C3), device=cuda)
+    ws = torch.zeros(lib.acmi_kfac_inverse_ws_doubles(A, C3), dtype=torch.float64, device=cuda)
+    damping = 0.01
+    _lib.call('acmi_kfac_inverse', A, C3, _lib.ptr(fac_d), ctypes.c_float(damping), 0, _lib.ptr(inv), _lib.ptr(ws),
+              _lib.stream_handle())
+    torch.cuda.synchronize()
+    inv_h = inv.cpu().numpy().astype(np.float64)
+    o = 0
+    for l in range(6):
+        af = min(l, 4)
+        Am, Gm = mats[af], mats[5 + l]
+        da, dg = Am.shape[0], Gm.shape[0]
+        pi = np.sqrt((np.trace(Am) / da) / (np.trace(Gm) / dg))
+        ref_a = np.linalg.inv(Am + pi * np.sqrt(damping) * np.eye(da))
+        ref_g = np.linalg.inv(Gm + np.sqrt(damping) / pi * np.eye(dg))
+        got_a = inv_h[o:o + da * da].reshape(da, da)
+        o += da * da
+        got_g = inv_h[o:o + dg * dg].reshape(dg, dg)
+        o += dg * dg
+        for got, ref in ((got_a, ref_a), (got_g, ref_g)):
+            rel = np.abs(got - ref).max() / np.abs(ref).max()
+            assert rel < 1e-5, (l, rel)
+
+
+def test_kfac_eigvals_match_numpy(lib, cuda):
+    A, C3 = 4, 32
+    din = (ctypes.c_int64 * 6)()
+    dout = (ctypes.c_int64 * 6)()
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, din, dout, so, ctypes.byref(tot))
+    rng = np.random.default_rng(6)
+    fac = np.zeros(tot.value, np.float32)
+    mats = []
+    for f in range(11):
+        n = din[f] if f < 5 else dout[f - 5]
+        x = rng.standard_normal((n + 5, n))
+        m = (x.T @ x / x.shape[0]).astype(np.float32)
+        fac[so[f]:so[f] + n * n] = m.ravel()
+        mats.append(m.astype(np.float64))
+    fac_d = torch.from_numpy(fac).to(cuda)
+    nev = sum(m.shape[0] for m in mats)
+    ev = torch.zeros(nev, dtype=torch.float64, device=cuda)
+    ws = torch.zeros(lib.acmi_kfac_eig_ws_doubles(A, C3), dtype=torch.float64, device=cuda)
+    _lib.call('acmi_kfac_eigvals', A, C3, _lib.ptr(fac_d), _lib.ptr(ev), _lib.ptr(ws), _lib.stream_handle())
+    got = ev.cpu().numpy()
+    o = 0
+    for m in mats:
+        n = m.shape[0]
+        ref = np.linalg.eigvalsh(0.5 * (m + m.T))
+        rel = np.abs(got[o:o + n] - ref).max() / np.abs(ref).max()
+        assert rel < 1e-10, rel
+        # north_star: eigenvalues within 1e-4 relative (each eigenvalue)
+        assert np.all(np.abs(got[o:o + n] - ref) <= 1e-4 * np.abs(ref) + 1e-12 * np.abs(ref).max())
+        o += n

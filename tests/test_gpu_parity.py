@@ -1,0 +1,334 @@
+"""GPU parity of the HIP path against the oracle (oracle/oracle.py) and the golden
+fixtures of the reference (tests/golden).  Everything calls libacmi through the
+C-ABI (directly or through the actorcritic API).  Tolerances:
+  * integer / byte work (stepper, sampling with given uniforms, schedule): bit-exact,
+  * n-step targets: bit-exact vs the float32 oracle, <= 4 ulp vs the reference closures,
+  * logits / values / losses: rel 1e-5 (fp32 vs float64),
+  * K-FAC factors: rel 2e-5; inverses rel 1e-4; preconditioned gradients rel-L2 <= 1e-3
+    (north_star), eigenvalues rel 1e-4.
+"""
+import ctypes
+import json
+import os
+import sys
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from actorcritic import _lib
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, 'golden')
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), 'oracle'))
+import oracle  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(x, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(x))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+def test_returns_kernel_matches_golden(lib, cuda):
+    d = np.load(os.path.join(GOLD, 'returns.npz'))
+    meta = json.loads(str(d['meta']))
+    for i, m in enumerate(meta):
+        c = {k[len('c{}_'.format(i)):]: d[k] for k in d.files if k.startswith('c{}_'.format(i))}
+        N, T = m['N'], m['T']
+        gp, bp = oracle.gamma_tables(0.99, T)
+        r, te, v, vb = dev(c['rewards']), dev(c['terminals'].astype(np.uint8)), dev(c['values']), dev(c['v_boot'])
+        gp_d, bp_d = dev(gp), dev(bp)
+        tg = torch.zeros(N, T, device=cuda)
+        adv = torch.zeros(N, T, device=cuda)
+        _lib.call('acmi_returns', _lib.ptr(r), _lib.ptr(te), _lib.ptr(v), _lib.ptr(vb), N, T, _lib.ptr(gp_d),
+                  _lib.ptr(bp_d), _lib.ptr(tg), _lib.ptr(adv), _lib.stream_handle())
+        got = tg.cpu().numpy()
+        mine = oracle.targets_f32(c['rewards'], c['terminals'], c['v_boot'], 0.99)
+        np.testing.assert_array_equal(got, mine)  # bit-exact vs the float32 restatement
+        ulp = np.spacing(np.float32(np.abs(c['targets_f32']).max()))
+        assert np.abs(got - c['targets_f32']).max() <= 4 * ulp, m
+        np.testing.assert_array_equal(adv.cpu().numpy(), (got - c['values']).astype(np.float32))
+
+
+def test_stepper_matches_reference_wrapper_trace(lib, cuda):
+    from actorcritic.envs.atari.wrappers import SyntheticAtariEnvs
+    rec = json.load(open(os.path.join(GOLD, 'framestack_autoreset.json')))
+    envs = rec['envs']
+    N = max(envs) + 1
+    env = SyntheticAtariEnvs(N, num_actions=4, seed=rec['seed'], env_offset=0)
+    obs = env.reset().cpu().numpy()
+    for e in envs:
+        assert zlib.crc32(obs[e].tobytes()) == rec['env{}'.format(e)]['crc'][0]
+    steps = len(rec['env{}'.format(envs[0])]['actions'])
+    ep_seen = {e: [] for e in envs}
+    for t in range(steps):
+        a = np.zeros(N, np.int32)
+        for e in envs:
+            a[e] = rec['env{}'.format(e)]['actions'][t]
+        o, r, d, info = env.step(a)
+        o, r, d = o.cpu().numpy(), r.cpu().numpy(), d.cpu().numpy()
+        ep = info.episode_rewards.cpu().numpy()[:, 0]
+        for e in envs:
+            g = rec['env{}'.format(e)]
+            assert zlib.crc32(o[e].tobytes()) == g['crc'][t + 1], (e, t)
+            assert r[e] == g['rewards'][t] and bool(d[e]) == g['terminals'][t], (e, t)
+            ep_seen[e].append(None if np.isnan(ep[e]) else float(ep[e]))
+    for row, e in zip(rec['episode_rewards'], envs):
+        assert ep_seen[e] == [None if v is None else pytest.approx(v) for v in row]
+
+
+def test_sampling_exact_with_given_uniforms_and_calibrated(lib, cuda):
+    rng = np.random.default_rng(3)
+    B, A = 4096, 6
+    logits = (rng.standard_normal((B, A)) * 2).astype(np.float32)
+    u = rng.random(B).astype(np.float32)
+    lg, ud = dev(logits), dev(u)
+    out = torch.zeros(B, dtype=torch.int32, device=cuda)
+    bad = torch.zeros(1, dtype=torch.int32, device=cuda)
+    _lib.call('acmi_sample_actions', _lib.ptr(lg), A, B, A, 0, 0, 0, _lib.ptr(ud), 0, _lib.ptr(out), _lib.ptr(bad),
+              _lib.stream_handle())
+    np.testing.assert_array_equal(out.cpu().numpy(), oracle.sample_f32(logits, u))
+    # counter RNG: exactly the oracle's uniforms, and calibrated frequencies
+    _lib.call('acmi_sample_actions', _lib.ptr(lg), A, B, A, 5, 1, 9, None, 0, _lib.ptr(out), _lib.ptr(bad),
+              _lib.stream_handle())
+    np.testing.assert_array_equal(out.cpu().numpy(),
+                                  oracle.sample_f32(logits, oracle.sample_uniforms(5, 1, 9, B)))
+    z = np.zeros((B, A), np.float32)
+    _lib.call('acmi_sample_actions', _lib.ptr(dev(z)), A, B, A, 5, 1, 10, None, 0, _lib.ptr(out), _lib.ptr(bad),
+              _lib.stream_handle())
+    counts = np.bincount(out.cpu().numpy(), minlength=A)
+    chi2 = ((counts - B / A) ** 2 / (B / A)).sum()
+    assert chi2 < 25.0  # df=5, p ~ 1e-4
+    # mode and NaN detection
+    _lib.call('acmi_sample_actions', _lib.ptr(lg), A, B, A, 0, 0, 0, None, 1, _lib.ptr(out), _lib.ptr(bad),
+              _lib.stream_handle())
+    np.testing.assert_array_equal(out.cpu().numpy(), logits.argmax(1))
+    logits[7, 2] = np.nan
+    _lib.call('acmi_sample_actions', _lib.ptr(dev(logits)), A, B, A, 0, 0, 0, None, 0, _lib.ptr(out),
+              _lib.ptr(bad), _lib.stream_handle())
+    assert int(bad.item()) == 1 and int(out[7].item()) == -1
+
+
+def test_a2c_loss_and_categorical_match_oracle(lib, cuda):
+    rng = np.random.default_rng(4)
+    M, A = 1000, 18
+    logits = rng.standard_normal((M, A)).astype(np.float32)
+    values = rng.standard_normal(M).astype(np.float32)
+    actions = rng.integers(0, A, M).astype(np.int32)
+    targets = rng.standard_normal(M).astype(np.float32)
+    adv = (targets - values).astype(np.float32)
+    ldh = 20
+    dhead = torch.zeros(M, ldh, device=cuda)
+    ws = torch.zeros(lib.acmi_a2c_loss_ws_floats(M), device=cuda)
+    out = torch.zeros(4, device=cuda)
+    L, V, AC, TG, AD = dev(logits), dev(values), dev(actions), dev(targets), dev(adv)
+    _lib.call('acmi_a2c_loss', _lib.ptr(L), A, _lib.ptr(V), _lib.ptr(AC), _lib.ptr(TG), _lib.ptr(AD), M, A,
+              0.01, 0.5, 1.0, _lib.ptr(dhead), ldh, _lib.ptr(ws), _lib.ptr(out), _lib.stream_handle())
+    ref = oracle.a2c_loss_and_head_grads(logits, values, actions, targets)
+    got = out.cpu().numpy()
+    assert got[0] == pytest.approx(ref['policy_loss'], rel=1e-5, abs=1e-7)
+    assert got[1] == pytest.approx(ref['baseline_loss'], rel=1e-5)
+    assert got[2] == pytest.approx(ref['mean_entropy'], rel=1e-5)
+    dh = dhead.cpu().numpy()
+    np.testing.assert_allclose(dh[:, :A], ref['dlogits'], rtol=1e-4, atol=1e-9)
+    np.testing.assert_allclose(dh[:, A], ref['dvalue'], rtol=1e-5, atol=1e-10)
+    assert not dh[:, A + 1:].any()
+    ent = torch.zeros(M, device=cuda)
+    lp = torch.zeros(M, device=cuda)
+    _lib.call('acmi_categorical', _lib.ptr(L), A, M, A, _lib.ptr(AC), _lib.ptr(ent), _lib.ptr(lp),
+              _lib.stream_handle())
+    np.testing.assert_allclose(ent.cpu().numpy(), oracle.entropy(logits.astype(np.float64)), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(lp.cpu().numpy(),
+                               oracle.log_softmax(logits.astype(np.float64))[np.arange(M), actions], rtol=1e-5,
+                               atol=1e-6)
+
+
+def test_first_order_optimizers_match_oracle(lib, cuda):
+    rng = np.random.default_rng(6)
+    n = 100003
+    p = rng.standard_normal(n).astype(np.float32)
+    g = rng.standard_normal(n).astype(np.float32)
+    acc = rng.standard_normal(n).astype(np.float32)
+    ws = torch.zeros(lib.acmi_opt_ws_floats(n), device=cuda)
+    norm = torch.zeros(1, device=cuda)
+    P, G, ACC = dev(p), dev(g), dev(acc)
+    _lib.call('acmi_momentum_apply', _lib.ptr(P), _lib.ptr(ACC), _lib.ptr(G), n, 3e-4, 0.9, 0.5, _lib.ptr(ws),
+              _lib.ptr(norm), _lib.stream_handle())
+    rp, racc = oracle.momentum_apply(p.astype(np.float64), acc.astype(np.float64), g.astype(np.float64), 3e-4, 0.9,
+                                     0.5)
+    np.testing.assert_allclose(P.cpu().numpy(), rp, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(ACC.cpu().numpy(), racc, rtol=1e-5, atol=1e-7)
+    assert norm.item() == pytest.approx(np.linalg.norm(g.astype(np.float64)), rel=1e-5)
+    P, G = dev(p), dev(g)
+    ms = torch.ones(n, device=cuda)
+    mom = torch.zeros(n, device=cuda)
+    _lib.call('acmi_rmsprop_apply', _lib.ptr(P), _lib.ptr(ms), _lib.ptr(mom), _lib.ptr(G), n, 7e-4, 0.9, 0.0, 1e-10,
+              0.5, _lib.ptr(ws), _lib.ptr(norm), _lib.stream_handle())
+    rp, rms, rmom = oracle.rmsprop_apply(p.astype(np.float64), np.ones(n), np.zeros(n), g.astype(np.float64), 7e-4,
+                                         0.5)
+    np.testing.assert_allclose(P.cpu().numpy(), rp, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(ms.cpu().numpy(), rms, rtol=1e-5)
+
+
+def _build(N=3, T=4, A=4, C3=32, seed=5):
+    from actorcritic import session as sess
+    from actorcritic.agents import MultiEnvAgent
+    from actorcritic.envs.atari.model import AtariModel
+    from actorcritic.envs.atari.wrappers import SyntheticAtariEnvs
+    from actorcritic.examples.atari.a2c_acktr import create_optimizer
+    from actorcritic.multi_env import MultiEnv
+    from actorcritic.nn import linear_decay
+    from actorcritic.objectives import A2CObjective
+    sess.reset_default_graph()
+    env = MultiEnv(SyntheticAtariEnvs(N, num_actions=A, seed=seed))
+    params = oracle.init_params(A, C3, seed=1)
+    model = AtariModel(env.observation_space, env.action_space, C3, params=params, random_seed=3)
+    agent = MultiEnvAgent(env, model, T)
+    obj = A2CObjective(model)
+    gs = sess.get_or_create_global_step()
+    opt = create_optimizer(C3 == 32, model, linear_decay(0.25, 0.025, gs, 1000) if C3 == 32 else 7e-4)
+    op = obj.optimize_shared(opt, 0.5, global_step=gs)
+    return env, model, agent, obj, gs, opt, op, params
+
+
+def _feed(model, data):
+    obs, act, rew, term, nxt, _ = data
+    return {model.observations_placeholder: obs, model.bootstrap_observations_placeholder: nxt,
+            model.actions_placeholder: act, model.rewards_placeholder: rew, model.terminals_placeholder: term}
+
+
+def test_rollout_matches_oracle_env_and_tower(lib, cuda):
+    from actorcritic import session as sess
+    N, T, A = 3, 6, 4
+    env, model, agent, obj, gs, opt, op, params = _build(N, T, A)
+    with sess.Session() as s:
+        data = agent.interact(s)
+    obs, act, rew, term, nxt, infos = [x for x in data]
+    o = obs.cpu().numpy()
+    # the stepper: replay the sampled actions through the oracle envs
+    envs = [oracle.SyntheticAtari(5, e) for e in range(N)]
+    for e in range(N):
+        np.testing.assert_array_equal(o[e, 0], envs[e].reset())
+        for t in range(T):
+            ob, r, d, ep = envs[e].step(int(act[e, t]))
+            nxt_ref = ob
+            if t + 1 < T:
+                np.testing.assert_array_equal(o[e, t + 1], ob)
+            assert float(rew[e, t]) == r and bool(term[e, t]) == d
+        np.testing.assert_array_equal(nxt[e].cpu().numpy(), nxt_ref)
+    # the tower activations cached by the rollout (row n*T + t)
+    fwd = model.engine.lookup_rollout(obs)
+    ref = oracle.forward(params, o.reshape(-1, 84, 84, 4), A, 32)
+    for name, got in (('logits', fwd.flat_logits), ('value', fwd.flat_value), ('a4', fwd.acts.a4),
+                      ('a1', fwd.acts.a1)):
+        r = ref[name].reshape(got.shape)
+        rel = np.abs(got.cpu().double().numpy() - r).max() / np.abs(r).max()
+        assert rel < 1e-5, (name, rel)
+    # the actions are the oracle's inverse-CDF draws of the rollout's counters
+    lg = fwd.flat_logits.cpu().numpy().reshape(N, T, A)
+    for t in range(T):
+        u = oracle.sample_uniforms(3, 0, t, N)
+        np.testing.assert_array_equal(act[:, t].cpu().numpy(), oracle.sample_f32(lg[:, t], u))
+
+
+def test_acktr_update_matches_oracle(lib, cuda):
+    """One steady-state ACKTR update at gs=40 (covariance update + inverse + apply)
+    against the float64 oracle on the same rollout."""
+    from actorcritic import session as sess
+    N, T, A, C3 = 3, 5, 4, 32
+    env, model, agent, obj, gs, opt, op, params = _build(N, T, A, C3)
+    gs.assign(40)
+    with sess.Session() as s:
+        data = agent.interact(s)
+        feed = _feed(model, data)
+        fwd = model.engine.lookup_rollout(data[0])
+        logits32 = fwd.flat_logits.cpu().numpy().copy()
+        p_before = model.params.cpu().numpy().astype(np.float64)
+        s.run(op, feed_dict=feed)
+        torch.cuda.synchronize()
+    obs, act, rew, term, nxt, _ = [x for x in data]
+    M = N * T
+    full = oracle.forward(p_before, obs.cpu().numpy().reshape(M, 84, 84, 4), A, C3)
+    vb = oracle.forward(p_before, nxt.cpu().numpy(), A, C3)['value']
+    tg = oracle.targets_f64(rew.cpu().numpy(), term.cpu().numpy(), vb, 0.99).reshape(-1)
+    lg = oracle.a2c_loss_and_head_grads(full['logits'], full['value'], act.cpu().numpy().reshape(-1), tg)
+    grads, _, afac = oracle.backward(p_before, full, lg['dlogits'], lg['dvalue'], A, C3, with_a_factors=True)
+    g_pi, g_v, y = oracle.sampled_head_grads(logits32, 0x4b464143, 0, 40)
+    gfac = oracle.g_factors(p_before, full, g_pi, g_v, A, C3)
+    st = opt.state
+    L = model.engine.layout
+    fac = st['factors'].cpu().numpy().astype(np.float64)
+    for f in range(5):
+        d = L.din[f]
+        got = fac[L.stat_off[f]:L.stat_off[f] + d * d].reshape(d, d)
+        rel = np.abs(got - afac[f]).max() / np.abs(afac[f]).max()
+        assert rel < 2e-5, ('A', f, rel)  # first EMA step with zero-debias == the batch statistics
+    for l in range(6):
+        d = L.dout[l]
+        got = fac[L.stat_off[5 + l]:L.stat_off[5 + l] + d * d].reshape(d, d)
+        rel = np.abs(got - gfac[l]).max() / np.abs(gfac[l]).max()
+        assert rel < 5e-5, ('G', l, rel)
+    inv = oracle.damped_inverses(afac, gfac, 0.01)
+    new_p, vel, precon, coeff = oracle.kfac_step(p_before, np.zeros_like(p_before), grads, inv,
+                                                 oracle.linear_decay(0.25, 0.025, 40, 1000), 0.9, 1e-4, A, C3)
+    got_pre = st['precon'].cpu().numpy().astype(np.float64)
+    rel_l2 = np.linalg.norm(got_pre - precon) / np.linalg.norm(precon)
+    assert rel_l2 < 1e-3, rel_l2  # north_star: preconditioned gradients within 1e-3 rel-L2
+    assert float(st['coeff'][0]) == pytest.approx(coeff, rel=1e-3)
+    got_p = model.params.cpu().numpy().astype(np.float64)
+    assert np.linalg.norm(got_p - new_p) / np.linalg.norm(new_p - p_before) < 1e-3
+    assert gs.value == 41
+
+
+def test_cold_start_schedule_and_a2c_update(lib, cuda):
+    from actorcritic import session as sess
+    env, model, agent, obj, gs, opt, op, params = _build(2, 3)
+    flags = []
+    with sess.Session() as s:
+        for _ in range(3):
+            data = agent.interact(s)
+            s.run(op, feed_dict=_feed(model, data))
+            flags.append(opt.last_flags)
+    assert flags == [(True, False, False)] * 3 and gs.value == 6
+    assert torch.isfinite(model.params).all()
+    # A2C: RMSProp + clip, one update vs the oracle
+    env, model, agent, obj, gs, opt, op, params = _build(2, 5, C3=64)
+    with sess.Session() as s:
+        data = agent.interact(s)
+        p0 = model.params.cpu().numpy().astype(np.float64)
+        s.run(op, feed_dict=_feed(model, data))
+    obs, act, rew, term, nxt, _ = data
+    full = oracle.forward(p0, obs.cpu().numpy().reshape(-1, 84, 84, 4), 4, 64)
+    vb = oracle.forward(p0, nxt.cpu().numpy(), 4, 64)['value']
+    tg = oracle.targets_f64(rew.cpu().numpy(), term.cpu().numpy(), vb, 0.99).reshape(-1)
+    lg = oracle.a2c_loss_and_head_grads(full['logits'], full['value'], act.cpu().numpy().reshape(-1), tg)
+    grads, _ = oracle.backward(p0, full, lg['dlogits'], lg['dvalue'], 4, 64)
+    rp, _, _ = oracle.rmsprop_apply(p0, np.ones_like(p0), np.zeros_like(p0), grads, 7e-4, 0.5)
+    got = model.params.cpu().numpy().astype(np.float64)
+    assert np.linalg.norm(got - rp) / np.linalg.norm(rp - p0) < 1e-3
+
+
+def test_losses_and_fetches_through_session(lib, cuda):
+    from actorcritic import session as sess
+    N, T = 3, 4
+    env, model, agent, obj, gs, opt, op, params = _build(N, T)
+    with sess.Session() as s:
+        data = agent.interact(s)
+        feed = _feed(model, data)
+        pl, bl, me, ent, lp = s.run([obj.policy_loss, obj.baseline_loss, obj.mean_entropy, model.policy.entropy,
+                                     model.policy.log_prob], feed_dict=feed)
+    obs, act, rew, term, nxt, _ = data
+    full = oracle.forward(params, obs.cpu().numpy().reshape(-1, 84, 84, 4), 4, 32)
+    vb = oracle.forward(params, nxt.cpu().numpy(), 4, 32)['value']
+    tg = oracle.targets_f64(rew.cpu().numpy(), term.cpu().numpy(), vb, 0.99).reshape(-1)
+    ref = oracle.a2c_loss_and_head_grads(full['logits'], full['value'], act.cpu().numpy().reshape(-1), tg)
+    assert pl == pytest.approx(ref['policy_loss'], rel=1e-4, abs=1e-6)
+    assert bl == pytest.approx(ref['baseline_loss'], rel=1e-4)
+    assert me == pytest.approx(ref['mean_entropy'], rel=1e-5)
+    assert ent.shape == (N, T) and lp.shape == (N, T)
+    np.testing.assert_allclose(ent.reshape(-1), oracle.entropy(full['logits']), rtol=1e-5)

@@ -1,0 +1,124 @@
+"""The oracle pinned against the reference's own code (tests/golden, made by
+oracle/make_golden.py from /root/reference): n-step targets, the frame-stack /
+auto-reset / episode-info semantics, and the MultiEnvAgent layout."""
+import json
+import os
+import sys
+import zlib
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, 'golden')
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), 'oracle'))
+import oracle  # noqa: E402
+
+
+def _returns_cases():
+    d = np.load(os.path.join(GOLD, 'returns.npz'))
+    meta = json.loads(str(d['meta']))
+    for i, m in enumerate(meta):
+        yield m, {k[len('c{}_'.format(i)):]: d[k] for k in d.files if k.startswith('c{}_'.format(i))}
+
+
+def test_gamma_tables_are_the_reference_matrices_bit_for_bit():
+    for m, c in _returns_cases():
+        gp, bp = oracle.gamma_tables(0.99, m['T'])
+        D, bf = c['D'], c['boot_factors']
+        for n in range(m['N']):
+            for i in range(m['T']):
+                for j in range(i + 1):
+                    if D[n, i, j] != 0:
+                        assert D[n, i, j] == gp[i - j]
+            for t in range(m['T']):
+                if bf[n, t] != 0:
+                    assert bf[n, t] == bp[m['T'] - t]
+                    assert not c['terminals'][n, t:].any()
+                else:
+                    assert c['terminals'][n, t:].any()
+
+
+def test_targets_f32_within_4ulp_of_reference_closures():
+    # tolerance: <= 4 ulp of max |target| against the reference closures
+    # with np.matmul standing in for tf.matmul
+    for m, c in _returns_cases():
+        got = oracle.targets_f32(c['rewards'], c['terminals'], c['v_boot'], 0.99)
+        ref = c['targets_f32']
+        ulp = np.spacing(np.float32(np.abs(ref).max()))
+        assert np.abs(got - ref).max() <= 4 * ulp, m
+        exact = oracle.targets_f64(c['rewards'], c['terminals'], c['v_boot'], 0.99)
+        assert np.abs(exact - c['targets_f64']).max() <= 1e-4 * max(1.0, np.abs(exact).max())
+
+
+def test_framestack_autoreset_trace_matches_reference_wrappers():
+    rec = json.load(open(os.path.join(GOLD, 'framestack_autoreset.json')))
+    for e in rec['envs']:
+        r = rec['env{}'.format(e)]
+        env = oracle.SyntheticAtari(rec['seed'], e)
+        o = env.reset()
+        assert zlib.crc32(o.tobytes()) == r['crc'][0]
+        saw_terminal = False
+        kept = np.load(os.path.join(GOLD, 'framestack_env{}.npz'.format(e)))
+        for t, a in enumerate(r['actions']):
+            o, rw, d, ep = env.step(a)
+            assert zlib.crc32(o.tobytes()) == r['crc'][t + 1], t
+            assert rw == r['rewards'][t] and d == r['terminals'][t]
+            key = 'obs_t{}'.format(t + 1)
+            if key in kept.files:
+                np.testing.assert_array_equal(o, kept[key])
+            if d:
+                saw_terminal = True
+                # terminal observation is [0, 0, 0, frame] (wrappers.py:226-229)
+                assert not o[..., :3].any()
+        assert saw_terminal
+
+
+def test_episode_rewards_match_reference_info_batch():
+    rec = json.load(open(os.path.join(GOLD, 'framestack_autoreset.json')))
+    ep_ref = rec['episode_rewards']
+    for row, e in zip(ep_ref, rec['envs']):
+        env = oracle.SyntheticAtari(rec['seed'], e)
+        env.reset()
+        for t, a in enumerate(rec['env{}'.format(e)]['actions']):
+            _, _, _, ep = env.step(a)
+            if row[t] is None:
+                assert np.isnan(ep)
+            else:
+                assert ep == pytest.approx(row[t])
+
+
+def test_agent_layout_matches_reference(monkeypatch):
+    from actorcritic.agents import MultiEnvAgent, transpose_list
+    gold = json.load(open(os.path.join(GOLD, 'agent_layout.json')))
+    assert transpose_list([[1, 2, 3, 4], [5, 6, 7, 8], [9, 10, 11, 12]]) == gold['transpose_list']
+
+    class FakeMultiEnv:
+        batched = None
+
+        def __init__(self, n):
+            self.n, self.t = n, 0
+
+        def reset(self):
+            return ['obs(e{},t0)'.format(e) for e in range(self.n)]
+
+        def step(self, actions):
+            self.t += 1
+            obs = ['obs(e{},t{})'.format(e, self.t) for e in range(self.n)]
+            return obs, [float(a) for a in actions], [a % 3 == 0 for a in actions], [{'a': a} for a in actions]
+
+    class FakeModel:
+        def __init__(self):
+            self.batches = []
+
+        def sample_actions(self, batch, session):
+            self.batches.append(batch)
+            return [10 * i + len(self.batches) for i in range(len(batch))]
+
+    model = FakeModel()
+    agent = MultiEnvAgent(FakeMultiEnv(3), model, 4)
+    first = [list(x) for x in agent.interact(None)]
+    second = [list(x) for x in agent.interact(None)]
+    assert json.loads(json.dumps(model.batches)) == gold['sample_batches']
+    assert json.loads(json.dumps(first)) == gold['first']
+    assert json.loads(json.dumps(second)) == gold['second']
