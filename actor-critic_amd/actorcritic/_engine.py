@@ -80,14 +80,21 @@ class Activations(object):
         self.a4 = z(B, 512)
         self.logits = z(B, layout.A)
         self.value = z(B)
+        self.ws = None
         self.struct = self.view(0, 1)
 
-    def view(self, row, stride):
-        """Acts struct whose batch row b is image row + b*stride (rollout step view)."""
+    def view(self, row, stride, ws_rows=None):
+        """Acts struct whose batch row b is image row + b*stride (rollout step view);
+        ws_rows: batch size the forward workspace must serve (default B / stride)."""
         el = lambda t, per: t.data_ptr() + 4 * row * per
         A = self.logits.shape[1]
+        rows = ws_rows if ws_rows is not None else max(1, self.B // stride)
+        need = int(_lib.load().acmi_forward_ws_floats(rows))
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.zeros(max(need, 1), dtype=torch.float32, device=self.a1.device)
         return _lib.Acts(el(self.a1, 400 * 32), el(self.a2, 81 * 64), el(self.a3, self.a3[0].numel()),
-                         el(self.a4, 512), el(self.logits, A), el(self.value, 1), A)
+                         el(self.a4, 512), el(self.logits, A), el(self.value, 1), A, self.ws.data_ptr(),
+                         self.ws.numel())
 
 
 class UpdateState(object):

@@ -29,7 +29,8 @@ class Net(ctypes.Structure):
 
 class Acts(ctypes.Structure):
     _fields_ = [('a1', c_vp), ('a2', c_vp), ('a3', c_vp), ('a4', c_vp),
-                ('logits', c_vp), ('value', c_vp), ('ld_logits', c_int)]
+                ('logits', c_vp), ('value', c_vp), ('ld_logits', c_int),
+                ('ws', c_vp), ('ws_floats', c_i64)]
 
 
 class Bwd(ctypes.Structure):
@@ -50,6 +51,7 @@ _SIGS = {
     'acmi_kfac_layout': (c_int, [c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
                                  ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     'acmi_forward': (c_int, [ctypes.POINTER(Net), c_vp, c_i64, c_int, ctypes.POINTER(Acts), c_int, c_vp]),
+    'acmi_forward_ws_floats': (c_i64, [c_int]),
     'acmi_forward_strided': (c_int, [ctypes.POINTER(Net), c_vp, c_i64, c_int, ctypes.POINTER(Acts), c_int,
                                      c_i64, c_vp]),
     'acmi_sample_actions': (c_int, [c_vp, c_int, c_int, c_int, c_u32, c_u32, c_u32, c_vp, c_int, c_vp,
@@ -88,6 +90,7 @@ _SIGS = {
 PROF_CONV1_WGRAD = 1
 PROF_CONV2_WGRAD = 2
 PROF_CONV1_FWD = 3
+PROF_CONV1_AFACTOR = 4
 
 EXPORTED = tuple(_SIGS)
 

@@ -1,0 +1,225 @@
+// conv1 K-FAC input factor from the raw u8 observations, in exact integer
+// arithmetic on the i8 matrix cores.
+//
+// The conv1 A factor is A = mean_r [p;1][p;1]^T over every conv1 location r,
+// p = the 8x8x4 patch of u/255 (envs/atari/model.py:92-95, :227-229).  With
+// x = u - 128 in [-128, 127] (one XOR 0x80 per byte):
+//     sum_r u_a u_b = sum_r x_a x_b + 128 (Sx_a + Sx_b) + 128^2 R,
+//     Sx_a = sum_r x_a,
+// so the 256x256 Gram block is an i8 x i8 -> i32 product (v_mfma_i32_32x32x32_i8,
+// 2x the bf16 rate, 16x the f32 MFMA rate).  Every partial is an exact integer
+// (a 16384-row chunk is < 2^31), chunks are summed in int64, and only the final
+// division by 255^2 R rounds — the factor is exact to f32 rounding, tighter than
+// the fp32 reference computation.  Only the upper-triangular 128x128 tile pairs
+// (0,0), (0,1), (1,1) are computed.
+//
+// Operand lane map (verified on gfx950, scripts/probes/mfma_i8_probe.hip):
+// lane l holds A[row l&31][k = 16(l>>5) + j] and B[k = 16(l>>5) + j][col l&31],
+// j = 0..15; D uses the standard 32x32 map.
+#include "common.hpp"
+
+namespace acmi {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+constexpr int AF_BK = 64;          // rows per stage (two 32-deep MFMA steps)
+constexpr int AF_LINE = 80;        // bytes per LDS column line: 64 rows + 16 pad
+constexpr int AF_TILE = 128 * AF_LINE;
+constexpr int AF_CHUNK = 16384;    // rows per block: |partial| < 2^31
+constexpr int AF_OBS_W = 84;
+
+__global__ __launch_bounds__(256) void conv1_afactor_i8_kernel(const uint8_t* obs,
+                                                               long long img_stride,
+                                                               int rows, int* part,
+                                                               int* colsum) {
+  const int pair = blockIdx.x;  // tile pairs (0,0) (0,1) (1,1)
+  const int ta = pair == 2 ? 1 : 0;
+  const int tb = pair == 0 ? 0 : 1;
+  const bool diag = ta == tb;
+  const int chunk = blockIdx.y;
+  const int r_begin = chunk * AF_CHUNK;
+  const int r_end = min(rows, r_begin + AF_CHUNK);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2][2][AF_TILE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  // staging map: 4 rows (4*q4 .. +3) x 8 columns (8*cg .. +7) per thread
+  const int q4 = tid & 15;
+  const int cg = tid >> 4;
+  // column c = 128 t + 8 cg -> (kh, kw0): 8 bytes = pixels kw0, kw0+1, 4 channels each
+  auto col_off = [&](int t) {
+    const int c = 128 * t + 8 * cg;
+    const int kh = c >> 5;
+    const int kw0 = (c & 31) >> 2;
+    return (kh * AF_OBS_W + kw0) * 4;
+  };
+  const int coffA = col_off(ta);
+  const int coffB = col_off(tb);
+
+  uint2 ra[4], rb[4];
+  auto fetch = [&](int r0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = r0 + 4 * q4 + q;
+      if (r < r_end) {
+        const int img = r / 400;
+        const int p = r - img * 400;
+        const int oh = p / 20;
+        const int ow = p - oh * 20;
+        const uint8_t* base = obs + (long long)img * img_stride + (oh * 4 * AF_OBS_W + ow * 4) * 4;
+        uint2 a = *reinterpret_cast<const uint2*>(base + coffA);
+        ra[q] = make_uint2(a.x ^ 0x80808080u, a.y ^ 0x80808080u);
+        if (!diag) {
+          uint2 b = *reinterpret_cast<const uint2*>(base + coffB);
+          rb[q] = make_uint2(b.x ^ 0x80808080u, b.y ^ 0x80808080u);
+        }
+      } else {
+        ra[q] = make_uint2(0u, 0u);  // x = 0: contributes nothing
+        rb[q] = make_uint2(0u, 0u);
+      }
+    }
+  };
+  // 4 rows x 4 bytes -> 4 column words of 4 consecutive rows (v_perm_b32)
+  auto transpose4 = [](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t* out) {
+    const uint32_t p01l = __builtin_amdgcn_perm(w1, w0, 0x05010400u);
+    const uint32_t p01h = __builtin_amdgcn_perm(w1, w0, 0x07030602u);
+    const uint32_t p23l = __builtin_amdgcn_perm(w3, w2, 0x05010400u);
+    const uint32_t p23h = __builtin_amdgcn_perm(w3, w2, 0x07030602u);
+    out[0] = __builtin_amdgcn_perm(p23l, p01l, 0x05040100u);
+    out[1] = __builtin_amdgcn_perm(p23l, p01l, 0x07060302u);
+    out[2] = __builtin_amdgcn_perm(p23h, p01h, 0x05040100u);
+    out[3] = __builtin_amdgcn_perm(p23h, p01h, 0x07060302u);
+  };
+  auto commit = [&](int buf) {
+    uint32_t cols[8];
+    transpose4(ra[0].x, ra[1].x, ra[2].x, ra[3].x, cols);
+    transpose4(ra[0].y, ra[1].y, ra[2].y, ra[3].y, cols + 4);
+    uint8_t* dst = lds[buf][0];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      *reinterpret_cast<uint32_t*>(dst + (8 * cg + j) * AF_LINE + 4 * q4) = cols[j];
+    if (!diag) {
+      transpose4(rb[0].x, rb[1].x, rb[2].x, rb[3].x, cols);
+      transpose4(rb[0].y, rb[1].y, rb[2].y, rb[3].y, cols + 4);
+      uint8_t* dstb = lds[buf][1];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        *reinterpret_cast<uint32_t*>(dstb + (8 * cg + j) * AF_LINE + 4 * q4) = cols[j];
+    }
+  };
+
+  v16i acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0;
+  int csum = 0;
+
+  const int nst = r_end > r_begin ? (r_end - r_begin + AF_BK - 1) / AF_BK : 0;
+  if (nst > 0) {
+    fetch(r_begin);
+    commit(0);
+  }
+  __syncthreads();
+  const int half = lane >> 5;
+  for (int st = 0; st < nst; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nst) fetch(r_begin + (st + 1) * AF_BK);
+    const uint8_t* As = lds[cur][0];
+    const uint8_t* Bs = lds[cur][diag ? 0 : 1];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      v4i a[2], b[2];
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+        a[tm] = *reinterpret_cast<const v4i*>(As + (64 * wm + 32 * tm + (lane & 31)) * AF_LINE + 32 * s + 16 * half);
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn)
+        b[tn] = *reinterpret_cast<const v4i*>(Bs + (64 * wn + 32 * tn + (lane & 31)) * AF_LINE + 32 * s + 16 * half);
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[tm], b[tn], acc[tm][tn], 0, 0, 0);
+    }
+    if (diag && tid < 128) {  // column sums of x over the staged rows
+      const uint32_t* line = reinterpret_cast<const uint32_t*>(As + tid * AF_LINE);
+#pragma unroll
+      for (int w = 0; w < AF_BK / 4; ++w) csum = __builtin_amdgcn_sdot4((int)line[w], 0x01010101, csum, false);
+    }
+    if (st + 1 < nst) commit(cur ^ 1);
+    __syncthreads();
+  }
+
+  int* out = part + (long long)chunk * 65536;
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) {
+      const int col = 128 * tb + 64 * wn + 32 * tn + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = 128 * ta + 64 * wm + 32 * tm + (r & 3) + 8 * (r >> 2) + 4 * half;
+        out[row * 256 + col] = acc[tm][tn][r];
+      }
+    }
+  if (diag && tid < 128) colsum[(long long)chunk * 256 + 128 * ta + tid] = csum;
+}
+
+// A (257 x 257, f32) from the exact integer sums; element (a, b), a,b <= 256
+__global__ void conv1_afactor_finalize(const int* part, const int* colsum, int nchunk, int rows,
+                                       float* astat) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 257 * 257) return;
+  const int a = idx / 257, b = idx - a * 257;
+  const int lo = a < b ? a : b, hi = a < b ? b : a;
+  const long long R = rows;
+  double v;
+  if (hi == 256 && lo == 256) {
+    v = 1.0;
+  } else {
+    long long sx_lo = 0;
+    for (int c = 0; c < nchunk; ++c) sx_lo += colsum[(long long)c * 256 + lo];
+    if (hi == 256) {
+      v = (double)(sx_lo + 128 * R) / (255.0 * (double)R);
+    } else {
+      long long sx_hi = 0, cx = 0;
+      for (int c = 0; c < nchunk; ++c) {
+        sx_hi += colsum[(long long)c * 256 + hi];
+        cx += part[(long long)c * 65536 + lo * 256 + hi];
+      }
+      const long long uu = cx + 128 * (sx_lo + sx_hi) + 16384 * R;
+      v = (double)uu / (65025.0 * (double)R);
+    }
+  }
+  astat[idx] = (float)v;
+}
+
+long long conv1_afactor_ws_ints(long long rows) {
+  const long long nchunk = (rows + AF_CHUNK - 1) / AF_CHUNK;
+  return nchunk * (65536 + 256);
+}
+
+int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* astat, int* ws,
+                     long long ws_ints, hipStream_t s) {
+  const long long rows = 400LL * B;
+  const int nchunk = (int)((rows + AF_CHUNK - 1) / AF_CHUNK);
+  ACMI_REQUIRE(conv1_afactor_ws_ints(rows) <= ws_ints, ACMI_ERR_WS,
+               "conv1 A-factor workspace too small");
+  ACMI_REQUIRE(img_stride % 8 == 0, ACMI_ERR_ARG, "conv1 A factor needs 8-byte aligned images");
+  int* part = ws;
+  int* colsum = ws + (long long)nchunk * 65536;
+  hipLaunchKernelGGL(conv1_afactor_i8_kernel, dim3(3, nchunk), dim3(256), 0, s, obs, img_stride,
+                     (int)rows, part, colsum);
+  hipLaunchKernelGGL(conv1_afactor_finalize, dim3(cdiv(257 * 257, 256)), dim3(256), 0, s, part,
+                     colsum, nchunk, (int)rows, astat);
+  ACMI_LAUNCH_CHECK("conv1_afactor_u8");
+  return ACMI_OK;
+}
+
+}  // namespace acmi

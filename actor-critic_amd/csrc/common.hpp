@@ -84,4 +84,9 @@ __device__ __forceinline__ float wave_max(float v) {
 
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// afactor_u8.hip: exact-integer conv1 A factor on the i8 matrix cores
+long long conv1_afactor_ws_ints(long long rows);
+int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* astat, int* ws,
+                     long long ws_ints, hipStream_t s);
+
 }  // namespace acmi

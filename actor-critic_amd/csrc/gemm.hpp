@@ -16,10 +16,10 @@
 // dtype.  Block = 256 threads = 4 waves; each wave owns a
 // (32*WTM) x (32*WTN) sub-tile held in WTM*WTN 16-register accumulators.
 //
-// Operand concept (template parameter Op):
-//   static constexpr bool KCONTIG;   // load4 returns 4 consecutive k (true)
-//                                    // or 4 consecutive i/j (false)
-//   __device__ float4 load4(int k, int i) const;   // zero outside bounds
+// Operand concept (template parameter Op; loaders in gemm_ops.hpp):
+//   static constexpr bool KCONTIG;   // float4 runs along k (true) or i/j
+//   R row(int) const; C col(int) const; St stage(R, C, bool) const;
+//   float4 finish(St)   (deferred masking, see gemm_ops.hpp)
 // LDS images are [k][i] for both operands so the MFMA fragment read
 // (lane l: row k = l>>5, col i = l&31) is one conflict-free ds_read_b32 per
 // operand per k-step.  K-contiguous operands are written transposed with a
@@ -27,240 +27,11 @@
 // 16-byte aligned stride (ds_write_b128).
 #pragma once
 
-#include "common.hpp"
+#include "gemm_ops.hpp"
 
 namespace acmi {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
-
-// exact u8 / 255.0f (one rounding), verified exhaustively for 0..255
-__device__ __forceinline__ float u8norm(uint32_t u) {
-  const float x = (float)u;
-  const float inv = 1.0f / 255.0f;
-  const float q = x * inv;
-  const float r = __builtin_fmaf(-q, 255.0f, x);
-  return __builtin_fmaf(r, inv, q);
-}
-
-// ---------------------------------------------------------------------------
-// Row sources: get4(r, c) returns elements c..c+3 of logical row r.
-// ---------------------------------------------------------------------------
-
-// Patches of NHWC images for a VALID conv; row r = (img, oh, ow),
-// column c = (kh, kw, ch) with ch fastest (== HWIO flatten == TF
-// extract_image_patches order).  T = uint8_t normalises by 1/255.
-template <typename T, int H, int W, int C, int KH, int KW, int S>
-struct ConvRows {
-  static constexpr int OH = (H - KH) / S + 1;
-  static constexpr int OW = (W - KW) / S + 1;
-  static constexpr int L = OH * OW;
-  static constexpr int COLS = KH * KW * C;
-  static_assert(C % 4 == 0, "channel runs must hold float4");
-  const T* x;
-  long long img_stride;  // elements of T between images
-  int rows;              // images * L
-
-  __device__ __forceinline__ float4 get4(int r, int c) const {
-    if (r >= rows || c >= COLS) return f4zero();
-    const int img = r / L;
-    const int p = r - img * L;
-    const int oh = p / OW;
-    const int ow = p - oh * OW;
-    const int kh = c / (KW * C);
-    const int rem = c - kh * (KW * C);
-    const int kw = rem / C;
-    const int ch = rem - kw * C;
-    const T* src = x + (long long)img * img_stride +
-                   ((oh * S + kh) * W + (ow * S + kw)) * C + ch;
-    if constexpr (sizeof(T) == 1) {
-      const uint32_t u = *reinterpret_cast<const uint32_t*>(src);
-      return make_float4(u8norm(u & 255u), u8norm((u >> 8) & 255u),
-                         u8norm((u >> 16) & 255u), u8norm(u >> 24));
-    } else {
-      return *reinterpret_cast<const float4*>(src);
-    }
-  }
-};
-
-// Dense row-major [rows][cols] with leading dimension ld (ld % 4 == 0).
-struct DenseRows {
-  const float* x;
-  int ld;
-  int rows;
-  int cols;  // multiple of 4 or rows zero-padded to ld
-  __device__ __forceinline__ float4 get4(int r, int c) const {
-    if (r >= rows || c >= cols) return f4zero();
-    return *reinterpret_cast<const float4*>(x + (long long)r * ld + c);
-  }
-};
-
-// Gradient of a VALID conv w.r.t. its input, one stride phase (ph, pw) per
-// blockIdx.z: row r = (img, ih', iw') -> input pixel (S*ih'+ph, S*iw'+pw);
-// column c = (kh', kw', co) -> tap (ph+S*kh', pw+S*kw'), output pixel
-// (ih'-kh', iw'-kw').  Only taps that hit the phase are enumerated, so the
-// stride-2 conv2 gradient does no zero work except at the borders.
-template <int IH, int IW, int KH, int KW, int S, int COUT>
-struct ConvTRows {
-  static constexpr int OH = (IH - KH) / S + 1;
-  static constexpr int OW = (IW - KW) / S + 1;
-  static_assert(IH % S == 0 && IW % S == 0 && KH % S == 0 && KW % S == 0,
-                "phase decomposition needs divisible extents");
-  static constexpr int PH = IH / S;   // phase grid extent
-  static constexpr int PW = IW / S;
-  static constexpr int KHP = KH / S;  // taps per phase
-  static constexpr int KWP = KW / S;
-  static constexpr int COLS = KHP * KWP * COUT;
-  static constexpr int L = PH * PW;   // rows per image per phase
-  static_assert(COUT % 4 == 0, "");
-  const float* dy;  // [img][OH][OW][COUT]
-  int rows;         // images * L
-
-  __device__ __forceinline__ float4 get4(int r, int c) const {
-    if (r >= rows || c >= COLS) return f4zero();
-    const int img = r / L;
-    const int p = r - img * L;
-    const int ihp = p / PW;
-    const int iwp = p - ihp * PW;
-    const int khp = c / (KWP * COUT);
-    const int rem = c - khp * (KWP * COUT);
-    const int kwp = rem / COUT;
-    const int co = rem - kwp * COUT;
-    const int oh = ihp - khp;
-    const int ow = iwp - kwp;
-    if (oh < 0 || ow < 0 || oh >= OH || ow >= OW) return f4zero();
-    return *reinterpret_cast<const float4*>(
-        dy + (((long long)img * OH + oh) * OW + ow) * COUT + co);
-  }
-};
-
-// ---------------------------------------------------------------------------
-// Operands
-// ---------------------------------------------------------------------------
-
-// A(k, i) = src row i, column k   (forward-style; k contiguous)
-template <class Src>
-struct RowsAsK {
-  static constexpr bool KCONTIG = true;
-  Src src;
-  __device__ __forceinline__ float4 load4(int k, int i) const { return src.get4(i, k); }
-};
-
-// A(k, i) = src row k, column i   (reduction-style; i contiguous)
-template <class Src>
-struct RowsAsI {
-  static constexpr bool KCONTIG = false;
-  Src src;
-  __device__ __forceinline__ float4 load4(int k, int i) const { return src.get4(k, i); }
-};
-
-// B(k, j) over row k of [P | dY | 1]:  j < kp -> P(k, j) (kp = 0 skips P),
-// kp <= j < kp + cout_pad -> dY(k, j-kp) (zero past cout), j == kp+cout_pad
-// -> 1 (homogeneous column, only for rows k < rows).
-template <class Src>
-struct CatRowsI {
-  static constexpr bool KCONTIG = false;
-  Src src;
-  int kp;
-  const float* dy;
-  int ldy;
-  int cout;
-  int cout_pad;  // multiple of 4
-  int rows;
-  __device__ __forceinline__ float4 load4(int k, int j) const {
-    if (k >= rows) return f4zero();
-    if (j < kp) return src.get4(k, j);
-    const int jj = j - kp;
-    if (jj < cout_pad) {
-      const float* p = dy + (long long)k * ldy + jj;
-      if (jj + 3 < cout) return *reinterpret_cast<const float4*>(p);
-      float4 v = f4zero();
-      if (jj + 0 < cout) v.x = p[0];
-      if (jj + 1 < cout) v.y = p[1];
-      if (jj + 2 < cout) v.z = p[2];
-      return v;
-    }
-    if (jj == cout_pad) return make_float4(1.f, 0.f, 0.f, 0.f);
-    return f4zero();
-  }
-};
-
-// B(k, j) = M[k][j], row-major with leading dimension ld (dims K x N).
-template <bool ALIGNED>
-struct MatI {
-  static constexpr bool KCONTIG = false;
-  const float* m;
-  int ld;
-  int K;
-  int N;
-  __device__ __forceinline__ float4 load4(int k, int j) const {
-    if (k >= K || j >= N) return f4zero();
-    const float* p = m + (long long)k * ld + j;
-    if (ALIGNED && j + 3 < N) return *reinterpret_cast<const float4*>(p);
-    float4 v = f4zero();
-    v.x = p[0];
-    if (j + 1 < N) v.y = p[1];
-    if (j + 2 < N) v.z = p[2];
-    if (j + 3 < N) v.w = p[3];
-    return v;
-  }
-};
-
-// B(k, j) = M[j][k]  (transposed access; k contiguous; dims K x N; ld%4==0)
-struct MatTK {
-  static constexpr bool KCONTIG = true;
-  const float* m;
-  int ld;
-  int K;  // multiple of 4
-  int N;
-  __device__ __forceinline__ float4 load4(int k, int j) const {
-    if (k >= K || j >= N) return f4zero();
-    return *reinterpret_cast<const float4*>(m + (long long)j * ld + k);
-  }
-};
-
-// A(k, i) = M[i][k]  (transposed access, any ld/alignment; dims K x N)
-struct MatTKu {
-  static constexpr bool KCONTIG = true;
-  const float* m;
-  int ld;
-  int K;
-  int N;
-  __device__ __forceinline__ float4 load4(int k, int j) const {
-    if (j >= N || k >= K) return f4zero();
-    const float* p = m + (long long)j * ld + k;
-    float4 v = f4zero();
-    v.x = p[0];
-    if (k + 1 < K) v.y = p[1];
-    if (k + 2 < K) v.z = p[2];
-    if (k + 3 < K) v.w = p[3];
-    return v;
-  }
-};
-
-// Conv weight as the B operand of the input gradient, one stride phase per
-// blockIdx.z:  B(k = (kh',kw',co), j = ci) = W[ph+S*kh'][pw+S*kw'][ci][co].
-template <int KH, int KW, int S, int CIN, int COUT>
-struct ConvTWeights {
-  static constexpr bool KCONTIG = true;
-  static constexpr int KHP = KH / S;
-  static constexpr int KWP = KW / S;
-  static constexpr int K = KHP * KWP * COUT;
-  const float* w;  // HWIO
-  __device__ __forceinline__ float4 load4(int k, int j) const {
-    if (k >= K || j >= CIN) return f4zero();
-    const int ph = blockIdx.z / S;
-    const int pw = blockIdx.z - ph * S;
-    const int khp = k / (KWP * COUT);
-    const int rem = k - khp * (KWP * COUT);
-    const int kwp = rem / COUT;
-    const int co = rem - kwp * COUT;
-    const int kh = ph + S * khp;
-    const int kw = pw + S * kwp;
-    return *reinterpret_cast<const float4*>(w + ((kh * KW + kw) * CIN + j) * COUT + co);
-  }
-};
 
 // ---------------------------------------------------------------------------
 // The kernel
@@ -280,12 +51,18 @@ struct Tile {
 // may use blockIdx.z for their own purposes (stride phases).
 // COLSUM: blocks with blockIdx.x == 0 also return sum_k B(k, j) through
 // epi.colsum(j, v) (the homogeneous row of [P;1]^T [..]).
+// sym_cols > 0 (requires BM == BN): the product's top-left sym_cols x sym_cols
+// block is symmetric and only its upper triangle is consumed, so blocks
+// strictly below the diagonal whose column tile lies inside it exit at once.
 template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM,
           class OpA, class OpB, class Epi>
 __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
                                                    int I, int J, int K,
-                                                   int k_chunk) {
+                                                   int k_chunk, int sym_cols) {
   using TL = Tile<BM, BN, BK, WTM, WTN>;
+  if (BM == BN && sym_cols > 0 && blockIdx.y < blockIdx.x &&
+      (int)(blockIdx.y + 1) * BN <= sym_cols)
+    return;
   constexpr int SA = OpA::KCONTIG ? BM + 1 : BM + 4;
   constexpr int SB = OpB::KCONTIG ? BN + 1 : BN + 4;
   constexpr int NA = BM * BK / 4 / 256;
@@ -308,34 +85,55 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
   }
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-  float4 ra[NA];
-  float4 rb[NB];
+  typename OpA::St ra[NA];
+  typename OpB::St rb[NB];
 
-  auto fetch = [&](int k0) {
+  // per-thread element coordinates: KCONTIG operands keep their row (i) fixed
+  // across K-tiles, the others their column (i) -> hoist that address part
+  constexpr int AK = OpA::KCONTIG ? BK / 4 : BM / 4;  // float4 slots per staging row
+  constexpr int BKs = OpB::KCONTIG ? BK / 4 : BN / 4;
+  typename OpA::R rowA[OpA::KCONTIG ? NA : 1];
+  typename OpA::C colA;
+  typename OpB::R rowB[OpB::KCONTIG ? NB : 1];
+  typename OpB::C colB;
+  if constexpr (OpA::KCONTIG) {
 #pragma unroll
-    for (int v = 0; v < NA; ++v) {
-      const int idx = tid + 256 * v;
-      if constexpr (OpA::KCONTIG) {
-        const int i = idx / (BK / 4);
-        const int k = (idx - i * (BK / 4)) * 4;
-        ra[v] = (k0 + k < kend) ? opA.load4(k0 + k, i0 + i) : f4zero();
-      } else {
-        const int k = idx / (BM / 4);
-        const int i = (idx - k * (BM / 4)) * 4;
-        ra[v] = (k0 + k < kend) ? opA.load4(k0 + k, i0 + i) : f4zero();
+    for (int v = 0; v < NA; ++v) rowA[v] = opA.row(i0 + (tid + 256 * v) / AK);
+  } else {
+    colA = opA.col(i0 + (tid % AK) * 4);
+  }
+  if constexpr (OpB::KCONTIG) {
+#pragma unroll
+    for (int v = 0; v < NB; ++v) rowB[v] = opB.row(j0 + (tid + 256 * v) / BKs);
+  } else {
+    colB = opB.col(j0 + (tid % BKs) * 4);
+  }
+
+  // loads are unconditional (operands clamp out-of-range addresses); the K
+  // bound and the operand masks are applied at commit (finish)
+  auto fetch = [&](int k0) {
+    if constexpr (OpA::KCONTIG) {
+      const int k = k0 + (tid % AK) * 4;  // same k for every v (256 % AK == 0)
+      const auto c = opA.col(k);
+#pragma unroll
+      for (int v = 0; v < NA; ++v) ra[v] = opA.stage(rowA[v], c, k < kend);
+    } else {
+#pragma unroll
+      for (int v = 0; v < NA; ++v) {
+        const int k = k0 + (tid + 256 * v) / AK;
+        ra[v] = opA.stage(opA.row(k), colA, k < kend);
       }
     }
+    if constexpr (OpB::KCONTIG) {
+      const int k = k0 + (tid % BKs) * 4;
+      const auto c = opB.col(k);
 #pragma unroll
-    for (int v = 0; v < NB; ++v) {
-      const int idx = tid + 256 * v;
-      if constexpr (OpB::KCONTIG) {
-        const int j = idx / (BK / 4);
-        const int k = (idx - j * (BK / 4)) * 4;
-        rb[v] = (k0 + k < kend) ? opB.load4(k0 + k, j0 + j) : f4zero();
-      } else {
-        const int k = idx / (BN / 4);
-        const int j = (idx - k * (BN / 4)) * 4;
-        rb[v] = (k0 + k < kend) ? opB.load4(k0 + k, j0 + j) : f4zero();
+      for (int v = 0; v < NB; ++v) rb[v] = opB.stage(rowB[v], c, k < kend);
+    } else {
+#pragma unroll
+      for (int v = 0; v < NB; ++v) {
+        const int k = k0 + (tid + 256 * v) / BKs;
+        rb[v] = opB.stage(opB.row(k), colB, k < kend);
       }
     }
   };
@@ -346,33 +144,35 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
 #pragma unroll
     for (int v = 0; v < NA; ++v) {
       const int idx = tid + 256 * v;
+      const float4 x = finish(ra[v]);
       if constexpr (OpA::KCONTIG) {
         const int i = idx / (BK / 4);
         const int k = (idx - i * (BK / 4)) * 4;
-        As[(k + 0) * SA + i] = ra[v].x;
-        As[(k + 1) * SA + i] = ra[v].y;
-        As[(k + 2) * SA + i] = ra[v].z;
-        As[(k + 3) * SA + i] = ra[v].w;
+        As[(k + 0) * SA + i] = x.x;
+        As[(k + 1) * SA + i] = x.y;
+        As[(k + 2) * SA + i] = x.z;
+        As[(k + 3) * SA + i] = x.w;
       } else {
         const int k = idx / (BM / 4);
         const int i = (idx - k * (BM / 4)) * 4;
-        *reinterpret_cast<float4*>(As + k * SA + i) = ra[v];
+        *reinterpret_cast<float4*>(As + k * SA + i) = x;
       }
     }
 #pragma unroll
     for (int v = 0; v < NB; ++v) {
       const int idx = tid + 256 * v;
+      const float4 x = finish(rb[v]);
       if constexpr (OpB::KCONTIG) {
         const int j = idx / (BK / 4);
         const int k = (idx - j * (BK / 4)) * 4;
-        Bs[(k + 0) * SB + j] = rb[v].x;
-        Bs[(k + 1) * SB + j] = rb[v].y;
-        Bs[(k + 2) * SB + j] = rb[v].z;
-        Bs[(k + 3) * SB + j] = rb[v].w;
+        Bs[(k + 0) * SB + j] = x.x;
+        Bs[(k + 1) * SB + j] = x.y;
+        Bs[(k + 2) * SB + j] = x.z;
+        Bs[(k + 3) * SB + j] = x.w;
       } else {
         const int k = idx / (BN / 4);
         const int j = (idx - k * (BN / 4)) * 4;
-        *reinterpret_cast<float4*>(Bs + k * SB + j) = rb[v];
+        *reinterpret_cast<float4*>(Bs + k * SB + j) = x;
       }
     }
   };
@@ -397,9 +197,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
   const int brow = wn * WTN * 32 + (lane & 31);
   const int khalf = lane >> 5;
 
+  // The loop body is one basic block: the next tile's fetch is unconditional
+  // (past kend it reads clamped addresses and is zeroed), so its loads stay in
+  // flight across the MFMAs and are only waited for at the LDS commit.
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) fetch(kbeg + (kt + 1) * BK);
+    fetch(kbeg + (kt + 1) * BK);
+    // keep the scheduler from hoisting the commit's finish() (which waits for
+    // the loads) into the MFMA block
+    __builtin_amdgcn_sched_barrier(0);
     const float* As = lds + cur * ABUF;
     const float* Bs = lds + 2 * ABUF + cur * BBUF;
 #pragma unroll
@@ -415,13 +221,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
         for (int tn = 0; tn < WTN; ++tn)
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[tm], b[tn], acc[tm][tn], 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
+    commit(cur ^ 1);
     if constexpr (COLSUM) {
       if (do_colsum) {
 #pragma unroll 8
         for (int kk = 0; kk < BK; ++kk) csum += Bs[kk * SB + tid];
       }
     }
-    if (kt + 1 < nk) commit(cur ^ 1);
     __syncthreads();
   }
 
@@ -528,10 +335,10 @@ struct EpiPartial {
 template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM,
           class OpA, class OpB, class Epi>
 inline void launch_gemm(const OpA& a, const OpB& b, const Epi& e, int I, int J,
-                        int K, int zdim, int k_chunk, hipStream_t s) {
+                        int K, int zdim, int k_chunk, hipStream_t s, int sym_cols = 0) {
   dim3 grid(cdiv(I, BM), cdiv(J, BN), zdim);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WTM, WTN, SPLITK, COLSUM, OpA, OpB, Epi>),
-                     grid, dim3(256), 0, s, a, b, e, I, J, K, k_chunk);
+                     grid, dim3(256), 0, s, a, b, e, I, J, K, k_chunk, sym_cols);
 }
 
 }  // namespace acmi

@@ -92,37 +92,27 @@ bool get_layout(int A, int C3, Layout* L) { return make_layout(A, C3, L); }
 // ---------------------------------------------------------------------------
 // small helpers
 // ---------------------------------------------------------------------------
-// fc heads weights as one [512][A+1] B operand: j<A -> pi.W, j==A -> v.W
-struct HeadsW {
-  static constexpr bool KCONTIG = false;
-  const float* wpi;
-  const float* wv;
-  int A;
-  __device__ __forceinline__ float el(int k, int j) const {
-    if (j < A) return wpi[k * A + j];
-    if (j == A) return wv[k];
-    return 0.f;
-  }
-  __device__ __forceinline__ float4 load4(int k, int j) const {
-    if (k >= 512) return f4zero();
-    return make_float4(el(k, j), el(k, j + 1), el(k, j + 2), el(k, j + 3));
-  }
-};
-
 // transposed heads weights: B(k = a, j) = a<A ? pi.W[j][a] : a==A ? v.W[j] : 0
 struct HeadsWT {
   static constexpr bool KCONTIG = true;
+  using R = int;  // j
+  using C = int;  // a
   const float* wpi;
   const float* wv;
   int A;
+  // branch-free: both candidate loads come from clamped addresses
   __device__ __forceinline__ float el(int a, int j) const {
-    if (a < A) return wpi[j * A + a];
-    if (a == A) return wv[j];
-    return 0.f;
+    const bool okj = j < 512;
+    const float p = wpi[okj && a < A ? j * A + a : 0];
+    const float v = wv[okj ? j : 0];
+    return (okj && a < A) ? p : ((okj && a == A) ? v : 0.f);
   }
-  __device__ __forceinline__ float4 load4(int k, int j) const {
-    if (j >= 512) return f4zero();
-    return make_float4(el(k, j), el(k + 1, j), el(k + 2, j), el(k + 3, j));
+  __device__ __forceinline__ R row(int j) const { return j; }
+  __device__ __forceinline__ C col(int a) const { return a; }
+  using St = float4;  // tiny operand (K = ldh): masked at load time
+  __device__ __forceinline__ St stage(const R& j, const C& k, bool in) const {
+    const float4 v = make_float4(el(k, j), el(k + 1, j), el(k + 2, j), el(k + 3, j));
+    return in ? v : f4zero();
   }
 };
 
@@ -142,22 +132,59 @@ struct EpiAct {
   }
 };
 
-struct EpiHeadsR {
-  float* logits;
-  int ld;
-  long long img_stride_l;  // rows
-  float* value;
-  long long img_stride_v;
-  const float* bpi;
-  const float* bv;
-  int A;
-  __device__ __forceinline__ void operator()(int i, int j, float v) const {
-    if (j < A) logits[(long long)i * img_stride_l * ld + j] = v + bpi[j];
-    else if (value) value[(long long)i * img_stride_v] = v + bv[0];
-  }
-};
 
 inline int roundup4(int x) { return (x + 3) & ~3; }
+
+// policy/value heads, one wave per row: the 512-long dot products of a4 with
+// the A+1 head columns, lane-strided partial sums + a butterfly (fixed order).
+__global__ __launch_bounds__(256) void heads_kernel(const float* a4, long long a4_stride, int B,
+                                                    const float* wpi, const float* bpi,
+                                                    const float* wv, const float* bv, int A,
+                                                    float* logits, long long l_stride,
+                                                    float* value, long long v_stride) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= B) return;
+  const float* x = a4 + (long long)row * a4_stride;
+  float xv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) xv[e] = x[lane + 64 * e];
+  for (int a = 0; a < A; ++a) {
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += xv[e] * wpi[(lane + 64 * e) * A + a];
+    s = wave_sum(s);
+    if (lane == 0) logits[(long long)row * l_stride + a] = s + bpi[a];
+  }
+  if (value) {
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += xv[e] * wv[lane + 64 * e];
+    s = wave_sum(s);
+    if (lane == 0) value[(long long)row * v_stride] = s + bv[0];
+  }
+}
+
+// fc4 split-K: partial slabs [z][B+1][512] -> relu(sum_z + bias) (fixed z order)
+__global__ void fc_splitk_finalize(const float* part, int nz, int B, const float* bias,
+                                   float* out, long long row_stride) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)B * 512) return;
+  const int i = (int)(idx / 512), j = (int)(idx - (long long)i * 512);
+  const long long zs = (long long)(B + 1) * 512;
+  float s = 0.f;
+  for (int z = 0; z < nz; ++z) s += part[z * zs + idx];
+  out[(long long)i * row_stride + j] = fmaxf(s + bias[j], 0.f);
+}
+
+// split factor for fc4 at small batch (64 x 128 tiles over 512 columns)
+static void fc4_plan(int B, int K, int* nz, int* chunk) {
+  const int blocks = cdiv(B, 64) * 4;
+  int sp = blocks >= 256 ? 1 : std::min(8, cdiv(256, blocks));
+  int ch = (cdiv(K, sp) + 31) / 32 * 32;
+  *chunk = ch;
+  *nz = cdiv(K, ch);
+}
 
 // ---------------------------------------------------------------------------
 // forward
@@ -192,7 +219,7 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     MatI<true> opB{P + L.off[4], C3, 576, C3};
     EpiAct epi{a->a3, P + L.off[5], C3, 49, st * 49 * C3};
     if constexpr (C3 == 32)
-      launch_gemm<256, 32, 32, 2, 1, false, false>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
+      launch_gemm<128, 32, 32, 1, 1, false, false>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
     else
       launch_gemm<128, 64, 32, 2, 1, false, false>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
   }
@@ -201,16 +228,23 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     // rows are images; with an image stride the dense row stride is st*K
     RowsAsK<DenseRows> opA{DenseRows{a->a3, (int)(st * K), B, K}};
     MatI<true> opB{P + L.off[6], 512, K, 512};
-    EpiAct epi{a->a4, P + L.off[7], 512, 1, st * 512};
-    launch_gemm<64, 128, 32, 1, 2, false, false>(opA, opB, epi, B, 512, K, 1, 0, s);
+    int nz, chunk;
+    fc4_plan(B, K, &nz, &chunk);
+    if (nz > 1 && a->ws && a->ws_floats >= (long long)nz * (B + 1) * 512) {
+      // small (rollout) batches: split K over blockIdx.z, fixed-order reduce
+      EpiPartial epi{a->ws, B, 512};
+      launch_gemm<64, 128, 32, 1, 2, true, false>(opA, opB, epi, B, 512, K, nz, chunk, s);
+      hipLaunchKernelGGL(fc_splitk_finalize, dim3(cdiv((long long)B * 512, 256)), dim3(256), 0, s,
+                         a->ws, nz, B, P + L.off[7], a->a4, st * 512);
+    } else {
+      EpiAct epi{a->a4, P + L.off[7], 512, 1, st * 512};
+      launch_gemm<64, 128, 32, 1, 2, false, false>(opA, opB, epi, B, 512, K, 1, 0, s);
+    }
   }
-  {  // heads: [B,512] -> logits [B,A], value [B]
-    RowsAsK<DenseRows> opA{DenseRows{a->a4, (int)(st * 512), B, 512}};
-    HeadsW opB{P + L.off[8], P + L.off[10], L.A};
-    EpiHeadsR epi{a->logits, a->ld_logits, st, want_value ? a->value : nullptr, st,
-                  P + L.off[9], P + L.off[11], L.A};
-    launch_gemm<128, 32, 32, 1, 1, false, false>(opA, opB, epi, B, L.A + 1, 512, 1, 0, s);
-  }
+  // heads: [B,512] -> logits [B,A], value [B]
+  hipLaunchKernelGGL(heads_kernel, dim3(cdiv(B, 4)), dim3(256), 0, s, a->a4, st * 512, B,
+                     P + L.off[8], P + L.off[9], P + L.off[10], P + L.off[11], L.A, a->logits,
+                     st * a->ld_logits, want_value ? a->value : nullptr, st);
   ACMI_LAUNCH_CHECK("acmi_forward");
   return ACMI_OK;
 }
@@ -270,19 +304,23 @@ __global__ void finalize_wgrad_kernel(WgradDesc d) {
   }
 }
 
-// G factor: part [nchunk][I+1][J] (I == J == n, no colsum row used)
+// G factor: part [nchunk][I+1][J] (I == J == n, no colsum row used); one
+// wave per output element sums the chunks in a fixed (lane-strided, then
+// butterfly) order, so the result is deterministic.
 __global__ void finalize_cov_kernel(const float* part, int nchunk, int n,
                                     int sub, float* out, int rows) {
   // out is sub x sub, taken from the top-left of the n x n product
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (idx >= sub * sub) return;
   const int a = idx / sub, b = idx - a * sub;
   const int lo = a < b ? a : b, hi = a < b ? b : a;
   const long long cs = (long long)(n + 1) * n;
   const float* p = part + (long long)lo * n + hi;
   float s = 0.f;
-  for (int c = 0; c < nchunk; ++c) s += p[c * cs];
-  out[idx] = s * (1.0f / (float)rows);
+  for (int c = lane; c < nchunk; c += 64) s += p[c * cs];
+  s = wave_sum(s);
+  if (lane == 0) out[idx] = s * (1.0f / (float)rows);
 }
 
 // G of the value head: element (A, A) of the heads product
@@ -297,8 +335,8 @@ __global__ void finalize_cov_elem_kernel(const float* part, int nchunk, int n,
 }
 
 // choose the split-K chunking: ~target blocks overall, chunk % 32 == 0
-static void plan_chunks(long long rows, int tiles, int* nchunk, int* chunk) {
-  const long long target_blocks = 1536;
+static void plan_chunks(long long rows, int tiles, int* nchunk, int* chunk,
+                        long long target_blocks = 1536) {
   long long nc = target_blocks / (tiles > 0 ? tiles : 1);
   if (nc < 1) nc = 1;
   long long ch = (rows + nc - 1) / nc;
@@ -310,11 +348,47 @@ static void plan_chunks(long long rows, int tiles, int* nchunk, int* chunk) {
   *chunk = (int)ch;
 }
 
-static long long partial_floats(long long I, long long J, long long rows) {
-  int nc, ch;
-  const int tiles = cdiv(I, 128) * cdiv(J, 128);
-  plan_chunks(rows, tiles, &nc, &ch);
-  return (long long)nc * (I + 1) * J;
+// tiles of an I x J product with T x T tiles that are not skipped by the
+// symmetric-block rule of gemm_kernel (sym_cols)
+static int live_tiles(int I, int J, int sym_cols, int T) {
+  const int ti = cdiv(I, T), tj = cdiv(J, T);
+  int n = 0;
+  for (int x = 0; x < ti; ++x)
+    for (int y = 0; y < tj; ++y)
+      if (!(sym_cols > 0 && y < x && (y + 1) * T <= sym_cols)) ++n;
+  return n;
+}
+
+struct WgradPlan {
+  int I, J, kp, cout_pad, nc, ch;
+  long long floats;
+};
+
+static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows) {
+  WgradPlan p;
+  p.cout_pad = roundup4(cout);
+  p.kp = with_stats ? K : 0;
+  p.I = K;
+  p.J = p.kp + p.cout_pad + (with_stats ? 1 : 0);
+  if (with_stats)
+    plan_chunks(rows, live_tiles(p.I, p.J, K, 128), &p.nc, &p.ch);
+  else
+    plan_chunks(rows, cdiv(p.I, 128) * cdiv(p.J, 32), &p.nc, &p.ch);
+  p.floats = (long long)p.nc * (p.I + 1) * p.J;
+  return p;
+}
+
+struct GcovPlan {
+  int np, nc, ch;
+  long long floats;
+};
+
+static GcovPlan gcov_plan(int n, long long rows) {
+  GcovPlan p;
+  p.np = roundup4(n);
+  plan_chunks(rows, live_tiles(p.np, p.np, p.np, 64), &p.nc, &p.ch, 512);
+  p.floats = (long long)p.nc * (p.np + 1) * p.np;
+  return p;
 }
 
 // Launch [P;1]^T [P | dY | 1] (with_stats) or P^T [dY] (+colsum) over rows.
@@ -323,25 +397,18 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
                        int ldy, int cout, bool with_stats, float* part,
                        long long part_cap, float* gradA, int nsplit,
                        float* gradB, float* astat, hipStream_t s, int site = 0) {
-  const int cout_pad = roundup4(cout);
-  const int kp = with_stats ? K : 0;
-  const int I = K;
-  const int J = kp + cout_pad + (with_stats ? 1 : 0);
+  const WgradPlan pl = wgrad_plan(K, cout, with_stats, rows);
+  const int I = pl.I, J = pl.J, kp = pl.kp, nc = pl.nc, ch = pl.ch;
   RowsAsI<Src> opA{src};
-  CatRowsI<Src> opB{src, kp, dy, ldy, cout, cout_pad, (int)rows};
-  int nc, ch;
-  if (with_stats) {
-    plan_chunks(rows, cdiv(I, 128) * cdiv(J, 128), &nc, &ch);
-  } else {
-    plan_chunks(rows, cdiv(I, 128) * cdiv(J, 32), &nc, &ch);
-  }
-  const long long need = (long long)nc * (I + 1) * J;
-  ACMI_REQUIRE(need <= part_cap, ACMI_ERR_WS, "wgrad workspace too small (%lld > %lld)",
-               need, part_cap);
+  CatRowsI<Src> opB{src, kp, dy, ldy, cout, pl.cout_pad, (int)rows};
+  if constexpr (!std::is_same<typename Src::elem_t, float>::value)
+    ACMI_REQUIRE(!with_stats, ACMI_ERR_ARG, "u8 patch sources take the integer A-factor path");
+  ACMI_REQUIRE(pl.floats <= part_cap, ACMI_ERR_WS, "wgrad workspace too small (%lld > %lld)",
+               pl.floats, part_cap);
   EpiPartial epi{part, I, J};
   prof_begin(site, s);
-  if (with_stats)
-    launch_gemm<128, 128, 32, 2, 2, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s);
+  if (with_stats)  // only the upper triangle of the symmetric [P]^T[P] block
+    launch_gemm<128, 128, 32, 2, 2, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s, K);
   else
     launch_gemm<128, 32, 32, 1, 1, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s);
   prof_end(site, s);
@@ -356,16 +423,14 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
 static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
                       float* part, long long part_cap, float* out,
                       hipStream_t s, float* out_v = nullptr, int v_index = -1) {
-  DenseRows src{g, ld, (int)rows, roundup4(n)};
+  const GcovPlan pl = gcov_plan(n, rows);
+  const int np = pl.np, nc = pl.nc, ch = pl.ch;
+  DenseRows src{g, ld, (int)rows, np};
   RowsAsI<DenseRows> op{src};
-  const int np = roundup4(n);
-  int nc, ch;
-  plan_chunks(rows, cdiv(np, 64) * cdiv(np, 64), &nc, &ch);
-  const long long need = (long long)nc * (np + 1) * np;
-  ACMI_REQUIRE(need <= part_cap, ACMI_ERR_WS, "gcov workspace too small");
+  ACMI_REQUIRE(pl.floats <= part_cap, ACMI_ERR_WS, "gcov workspace too small");
   EpiPartial epi{part, np, np};
-  launch_gemm<64, 64, 32, 1, 1, true, false>(op, op, epi, np, np, (int)rows, nc, ch, s);
-  hipLaunchKernelGGL(finalize_cov_kernel, dim3(cdiv((long long)sub * sub, 256)), dim3(256), 0,
+  launch_gemm<64, 64, 32, 1, 1, true, false>(op, op, epi, np, np, (int)rows, nc, ch, s, np);
+  hipLaunchKernelGGL(finalize_cov_kernel, dim3(cdiv((long long)sub * sub, 4)), dim3(256), 0,
                      s, part, nc, np, sub, out, (int)rows);
   if (out_v)
     hipLaunchKernelGGL(finalize_cov_elem_kernel, dim3(1), dim3(64), 0, s, part, nc, np,
@@ -378,20 +443,15 @@ static long long bwd_partial_cap(int B, int A, int C3) {
   // the largest split-K partial over all layers (with stats)
   long long m = 0;
   const long long rowsL[5] = {400LL * B, 81LL * B, 49LL * B, B, B};
-  const long long Ks[5] = {256, 512, 576, 49LL * C3, 512};
-  const long long co[5] = {32, 64, C3, 512, A + 1};
+  const int Ks[5] = {256, 512, 576, 49 * C3, 512};
+  const int co[5] = {32, 64, C3, 512, A + 1};
   for (int l = 0; l < 5; ++l) {
-    const long long J = Ks[l] + roundup4((int)co[l]) + 1;
-    m = std::max(m, partial_floats(Ks[l], J, rowsL[l]));
+    m = std::max(m, wgrad_plan(Ks[l], co[l], true, rowsL[l]).floats);
+    m = std::max(m, wgrad_plan(Ks[l], co[l], false, rowsL[l]).floats);
+    // G factors of the same layer's output
+    m = std::max(m, gcov_plan(co[l], rowsL[l]).floats);
   }
-  // G factors (64x64 tiles)
-  const long long gn[5] = {32, 64, C3, 512, roundup4(A + 1)};
-  const long long gr[5] = {400LL * B, 81LL * B, 49LL * B, B, B};
-  for (int l = 0; l < 5; ++l) {
-    int nc, ch;
-    plan_chunks(gr[l], cdiv(gn[l], 64) * cdiv(gn[l], 64), &nc, &ch);
-    m = std::max(m, (long long)nc * (gn[l] + 1) * gn[l]);
-  }
+  m = std::max(m, conv1_afactor_ws_ints(rowsL[0]));
   return m;
 }
 
@@ -411,7 +471,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
   {  // fc4 -> d3 = (d4 W4^T) * relu'(a3)
     const int K3 = 49 * C3;
     RowsAsK<DenseRows> opA{DenseRows{bw->d4, 512, B, 512}};
-    MatTK opB{P + L.off[6], 512, 512, K3};
+    MatTK<true> opB{P + L.off[6], 512, 512, K3};
     EpiReluGrad epi{bw->d3, a->a3, K3};
     launch_gemm<64, 128, 32, 1, 2, false, false>(opA, opB, epi, B, K3, 512, 1, 0, s);
   }
@@ -463,9 +523,16 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
                    st ? astat + L.stat_off[1] : nullptr, s, ACMI_PROF_CONV2_WGRAD);
   if (rc) return rc;
   // conv1: patches of the u8 observations
+  // conv1: weight gradient on the f32 engine; its A factor from the u8 frames on
+  // the i8 matrix cores (exact integer sums, afactor_u8.hip)
   rc = wgrad_layer(ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>{obs, img_stride, B * 400}, 256,
-                   400LL * B, bw->d1, 32, 32, st, part, ws_cap, grads + L.off[0], 32, nullptr,
-                   st ? astat + L.stat_off[0] : nullptr, s, ACMI_PROF_CONV1_WGRAD);
+                   400LL * B, bw->d1, 32, 32, false, part, ws_cap, grads + L.off[0], 32, nullptr,
+                   nullptr, s, ACMI_PROF_CONV1_WGRAD);
+  if (rc || !st) return rc;
+  prof_begin(ACMI_PROF_CONV1_AFACTOR, s);
+  rc = conv1_afactor_u8(obs, img_stride, B, astat + L.stat_off[0], reinterpret_cast<int*>(ws),
+                        ws_cap, s);
+  prof_end(ACMI_PROF_CONV1_AFACTOR, s);
   return rc;
 }
 
@@ -595,6 +662,15 @@ int acmi_forward_strided(const acmi_net_t* net, const uint8_t* obs, int64_t img_
                          const acmi_acts_t* acts, int want_value, int64_t act_img_stride,
                          acmi_stream_t stream) {
   return forward_dispatch(net, obs, img_stride, B, acts, want_value, act_img_stride, stream);
+}
+
+int64_t acmi_forward_ws_floats(int B) {
+  if (B <= 0) return 0;
+  int nz, chunk;
+  fc4_plan(B, 49 * 64, &nz, &chunk);
+  int nz2, chunk2;
+  fc4_plan(B, 49 * 32, &nz2, &chunk2);
+  return (long long)std::max(nz, nz2) * (B + 1) * 512;
 }
 
 int64_t acmi_backward_ws_floats(int B, int A, int C3) {

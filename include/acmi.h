@@ -82,7 +82,11 @@ typedef struct acmi_acts {
   float* logits; /* [B][ld_logits]                                          */
   float* value;  /* [B]  (may be NULL when want_value == 0)                 */
   int ld_logits;
+  float* ws;     /* optional split-K workspace (NULL: no split), floats:  */
+  int64_t ws_floats; /* >= acmi_forward_ws_floats(B) enables it            */
 } acmi_acts_t;
+
+int64_t acmi_forward_ws_floats(int B);
 
 int acmi_forward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride,
                  int B, const acmi_acts_t* acts, int want_value,
@@ -297,6 +301,7 @@ int acmi_gemm_f32(const float* A, const float* B, float* C, int M, int N,
 #define ACMI_PROF_CONV1_WGRAD 1 /* conv1 [P;1]^T [P | dY | 1] reduction GEMM */
 #define ACMI_PROF_CONV2_WGRAD 2
 #define ACMI_PROF_CONV1_FWD 3
+#define ACMI_PROF_CONV1_AFACTOR 4 /* exact-integer i8-MFMA conv1 A factor */
 int acmi_prof_enable(int site, int capacity);
 int acmi_prof_collect(double* total_ms, int* count);
 

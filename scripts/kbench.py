@@ -1,0 +1,73 @@
+"""Kernel micro-benchmarks (HIP events) for tuning: plain GEMM, and the update's
+backward (wgrad + A-factor reductions) at the bench workload size.
+
+  python scripts/kbench.py gemm 4096
+  python scripts/kbench.py backward 10240
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'actor-critic_amd'))
+
+import torch  # noqa: E402
+
+from actorcritic import _lib  # noqa: E402
+
+
+def timeit(fn, reps=10, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def gemm(n):
+    lib = _lib.load()
+    A = torch.randn(n, n, device='cuda')
+    B = torch.randn(n, n, device='cuda')
+    C = torch.empty(n, n, device='cuda')
+    ms = timeit(lambda: _lib.call('acmi_gemm_f32', _lib.ptr(A), _lib.ptr(B), _lib.ptr(C), n, n, n,
+                                  _lib.stream_handle()))
+    print('gemm {}^3: {:.3f} ms  {:.1f} TFLOP/s'.format(n, ms, 2 * n ** 3 / ms / 1e9))
+
+
+def backward(M, with_stats=True, site=1):
+    from actorcritic._engine import NetEngine, OBS_BYTES
+    eng = NetEngine(4, 32)
+    obs = torch.randint(0, 256, (M, 84, 84, 4), dtype=torch.uint8, device='cuda')
+    acts = eng.activations(M)
+    eng.forward(obs.data_ptr(), M, acts.struct)
+    st = eng.update_state(M)
+    st.dhead.normal_()
+    st.dhead[:, 5:] = 0
+
+    class F:
+        pass
+    f = F()
+    f.obs, f.M, f.acts = obs, M, acts
+    _lib.call('acmi_prof_enable', site, 64)
+    ms = timeit(lambda: eng.backward(f, st, with_stats))
+    tot, cnt = ctypes.c_double(), ctypes.c_int()
+    _lib.call('acmi_prof_collect', ctypes.byref(tot), ctypes.byref(cnt))
+    _lib.call('acmi_prof_enable', 0, 0)
+    print('backward M={} stats={}: {:.3f} ms; site {} kernel avg {:.3f} ms over {}'.format(
+        M, with_stats, ms, site, tot.value / max(1, cnt.value), cnt.value))
+
+
+if __name__ == '__main__':
+    what = sys.argv[1]
+    if what == 'gemm':
+        gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 4096)
+    elif what == 'backward':
+        M = int(sys.argv[2]) if len(sys.argv) > 2 else 10240
+        for site in (1, 2, 4):
+            backward(M, True, site)
+        backward(M, False, 1)
