@@ -334,30 +334,9 @@ __global__ void finalize_cov_elem_kernel(const float* part, int nchunk, int n,
   out[0] = s * (1.0f / (float)rows);
 }
 
-// choose the split-K chunking: ~target blocks overall, chunk % 32 == 0
-static void plan_chunks(long long rows, int tiles, int* nchunk, int* chunk,
-                        long long target_blocks = 1536) {
-  long long nc = target_blocks / (tiles > 0 ? tiles : 1);
-  if (nc < 1) nc = 1;
-  long long ch = (rows + nc - 1) / nc;
-  if (ch < 256) ch = 256;
-  ch = (ch + 31) / 32 * 32;
-  nc = (rows + ch - 1) / ch;
-  if (nc < 1) nc = 1;
-  *nchunk = (int)nc;
-  *chunk = (int)ch;
-}
-
-// tiles of an I x J product with T x T tiles that are not skipped by the
-// symmetric-block rule of gemm_kernel (sym_cols)
-static int live_tiles(int I, int J, int sym_cols, int T) {
-  const int ti = cdiv(I, T), tj = cdiv(J, T);
-  int n = 0;
-  for (int x = 0; x < ti; ++x)
-    for (int y = 0; y < tj; ++y)
-      if (!(sym_cols > 0 && y < x && (y + 1) * T <= sym_cols)) ++n;
-  return n;
-}
+// split-K reductions fill whole rounds of resident blocks (plan_rounds):
+// MI355X has 256 CUs; blocks per CU follow from each config's LDS image
+constexpr int kCUs = 256;
 
 struct WgradPlan {
   int I, J, kp, cout_pad, nc, ch;
@@ -371,9 +350,11 @@ static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows) {
   p.I = K;
   p.J = p.kp + p.cout_pad + (with_stats ? 1 : 0);
   if (with_stats)
-    plan_chunks(rows, live_tiles(p.I, p.J, K, 128), &p.nc, &p.ch);
+    plan_rounds(rows, live_tiles<128, 128>(p.I, p.J, K),
+                kCUs * gemm_blocks_per_cu<128, 128, 32, false, false>(), &p.nc, &p.ch);
   else
-    plan_chunks(rows, cdiv(p.I, 128) * cdiv(p.J, 32), &p.nc, &p.ch);
+    plan_rounds(rows, live_tiles<128, 32>(p.I, p.J, 0),
+                kCUs * gemm_blocks_per_cu<128, 32, 32, false, false>(), &p.nc, &p.ch);
   p.floats = (long long)p.nc * (p.I + 1) * p.J;
   return p;
 }
@@ -386,7 +367,8 @@ struct GcovPlan {
 static GcovPlan gcov_plan(int n, long long rows) {
   GcovPlan p;
   p.np = roundup4(n);
-  plan_chunks(rows, live_tiles(p.np, p.np, p.np, 64), &p.nc, &p.ch, 512);
+  plan_rounds(rows, live_tiles<64, 64>(p.np, p.np, p.np),
+              kCUs * gemm_blocks_per_cu<64, 64, 32, false, false>(), &p.nc, &p.ch);
   p.floats = (long long)p.nc * (p.np + 1) * p.np;
   return p;
 }

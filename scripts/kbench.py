@@ -3,6 +3,7 @@ backward (wgrad + A-factor reductions) at the bench workload size.
 
   python scripts/kbench.py gemm 4096
   python scripts/kbench.py backward 10240
+  python scripts/kbench.py backward1 10240   # two timed reps (profiling)
 """
 import ctypes
 import os
@@ -39,7 +40,7 @@ def gemm(n):
     print('gemm {}^3: {:.3f} ms  {:.1f} TFLOP/s'.format(n, ms, 2 * n ** 3 / ms / 1e9))
 
 
-def backward(M, with_stats=True, site=1):
+def backward(M, with_stats=True, site=1, reps=10):
     from actorcritic._engine import NetEngine, OBS_BYTES
     eng = NetEngine(4, 32)
     obs = torch.randint(0, 256, (M, 84, 84, 4), dtype=torch.uint8, device='cuda')
@@ -54,7 +55,7 @@ def backward(M, with_stats=True, site=1):
     f = F()
     f.obs, f.M, f.acts = obs, M, acts
     _lib.call('acmi_prof_enable', site, 64)
-    ms = timeit(lambda: eng.backward(f, st, with_stats))
+    ms = timeit(lambda: eng.backward(f, st, with_stats), reps=reps, warm=min(3, reps))
     tot, cnt = ctypes.c_double(), ctypes.c_int()
     _lib.call('acmi_prof_collect', ctypes.byref(tot), ctypes.byref(cnt))
     _lib.call('acmi_prof_enable', 0, 0)
@@ -66,6 +67,8 @@ if __name__ == '__main__':
     what = sys.argv[1]
     if what == 'gemm':
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 4096)
+    elif what == 'backward1':  # a short run for PMC passes
+        backward(int(sys.argv[2]) if len(sys.argv) > 2 else 10240, True, 2, reps=2)
     elif what == 'backward':
         M = int(sys.argv[2]) if len(sys.argv) > 2 else 10240
         for site in (1, 2, 4):

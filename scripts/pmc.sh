@@ -1,0 +1,28 @@
+#!/bin/bash
+# PMC passes over one command (each pass its own rocprofv3 run; counters only
+# with --kernel-trace, never with runtime/sys traces).
+# usage: scripts/pmc.sh <outname> <script.py | executable> [args...]
+set -o pipefail
+root="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+out="$root/gpurun_out/$1"; shift
+mkdir -p "$out"
+cd /tmp && export TMPDIR=/tmp
+pass() {
+  local name=$1; shift
+  echo "=== pmc pass $name: $*"
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" -d "$out/$name" -o "$name" --output-format csv \
+    -- "${CMD[@]}" > "$out/$name.log" 2>&1
+  local rc=$?
+  echo "=== pass $name rc=$rc"
+  return $rc
+}
+ARGS=("$@")
+# a .py script runs under python3; anything else is an executable in the repo
+if [[ "${ARGS[0]}" == *.py ]]; then CMD=(python3 "$root/${ARGS[0]}" "${ARGS[@]:1}")
+else CMD=("$root/${ARGS[0]}" "${ARGS[@]:1}"); fi
+pass sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES &&
+pass lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM &&
+pass tcc TCC_HIT_sum TCC_MISS_sum &&
+pass fetch FETCH_SIZE &&
+pass write WRITE_SIZE &&
+pass ta TA_TA_BUSY_sum TA_BUSY_avr
