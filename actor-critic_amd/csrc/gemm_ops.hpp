@@ -35,8 +35,11 @@ __device__ __forceinline__ float u8norm(uint32_t u) {
   return __builtin_fmaf(r, inv, q);
 }
 
+// Element offsets are 32-bit unsigned: every operand the engine reads holds
+// < 2^31 elements (checked on the host, acmi_*), so address arithmetic is
+// one 32-bit decode plus one 64-bit scaled add per load.
 struct OffOk {
-  long long off;
+  uint32_t off;
   bool ok;
 };
 
@@ -93,32 +96,33 @@ struct ConvRows {
   using Cp = OffOk;
   using elem_t = T;
   const T* x;
-  long long img_stride;  // elements of T between images
-  int rows;              // images * L
+  uint32_t img_stride;  // elements of T between images
+  int rows;             // images * L
 
-  // row/col decode clamped indices instead of branching (see StF4)
+  // row/col decode clamped indices instead of branching (see StF4); unsigned
+  // division by the constant extents is a multiply-high and a shift
   __device__ __forceinline__ R row(int r0) const {
     const bool ok = r0 < rows;
-    const int r = ok ? r0 : 0;
-    const int img = r / L;
-    const int p = r - img * L;
-    const int oh = p / OW;
-    const int ow = p - oh * OW;
-    return R{(long long)img * img_stride + (oh * S * W + ow * S) * C, ok};
+    const uint32_t r = ok ? (uint32_t)r0 : 0u;
+    const uint32_t img = r / L;
+    const uint32_t p = r - img * L;
+    const uint32_t oh = p / OW;
+    const uint32_t ow = p - oh * OW;
+    return R{img * img_stride + (oh * (S * W) + ow * S) * C, ok};
   }
   __device__ __forceinline__ Cp col(int c0) const {
     const bool ok = c0 < COLS;
-    const int c = ok ? c0 : 0;
-    const int kh = c / (KW * C);
-    const int rem = c - kh * (KW * C);
-    const int kw = rem / C;
-    const int ch = rem - kw * C;
+    const uint32_t c = ok ? (uint32_t)c0 : 0u;
+    const uint32_t kh = c / (KW * C);
+    const uint32_t rem = c - kh * (KW * C);
+    const uint32_t kw = rem / C;
+    const uint32_t ch = rem - kw * C;
     return Cp{(kh * W + kw) * C + ch, ok};
   }
   using St = typename std::conditional<sizeof(T) == 1, StU8, StF4>::type;
   __device__ __forceinline__ St stage(const R& r, const Cp& c, bool in) const {
     const bool ok = in && r.ok && c.ok;
-    const T* src = x + r.off + c.off;
+    const T* src = x + (r.off + c.off);
     if constexpr (sizeof(T) == 1)
       return StU8{*reinterpret_cast<const uint32_t*>(
           ok ? static_cast<const void*>(src) : static_cast<const void*>(zero_run()))};
@@ -136,12 +140,14 @@ struct DenseRows {
   int ld;
   int rows;
   int cols;  // multiple of 4, or rows zero-padded to ld
-  __device__ __forceinline__ R row(int r) const { return R{(long long)r * ld, r < rows}; }
-  __device__ __forceinline__ Cp col(int c) const { return Cp{c, c < cols}; }
+  __device__ __forceinline__ R row(int r) const {
+    return R{(uint32_t)r * (uint32_t)ld, r < rows};
+  }
+  __device__ __forceinline__ Cp col(int c) const { return Cp{(uint32_t)c, c < cols}; }
   using St = StF4;
   __device__ __forceinline__ St stage(const R& r, const Cp& c, bool in) const {
     const bool ok = in && r.ok && c.ok;
-    return stage_f4(x + r.off + c.off, ok);
+    return stage_f4(x + (r.off + c.off), ok);
   }
 };
 
@@ -164,7 +170,7 @@ struct ConvTRows {
   static constexpr int L = PH * PW;  // rows per image per phase
   static_assert(COUT % 4 == 0, "");
   struct R {
-    long long off;
+    uint32_t off;
     int ihp, iwp;
     bool ok;
   };
@@ -178,12 +184,12 @@ struct ConvTRows {
 
   __device__ __forceinline__ R row(int r0) const {
     const bool ok = r0 < rows;
-    const int r = ok ? r0 : 0;
-    const int img = r / L;
-    const int p = r - img * L;
-    const int ihp = p / PW;
-    const int iwp = p - ihp * PW;
-    return R{((long long)img * OH * OW + ihp * OW + iwp) * COUT, ihp, iwp, ok};
+    const uint32_t r = ok ? (uint32_t)r0 : 0u;
+    const uint32_t img = r / L;
+    const uint32_t p = r - img * L;
+    const uint32_t ihp = p / PW;
+    const uint32_t iwp = p - ihp * PW;
+    return R{(img * (OH * OW) + ihp * OW + iwp) * COUT, (int)ihp, (int)iwp, ok};
   }
   __device__ __forceinline__ Cp col(int c0) const {
     const bool ok = c0 < COLS;
@@ -199,7 +205,7 @@ struct ConvTRows {
     const int oh = r.ihp - c.khp;
     const int ow = r.iwp - c.kwp;
     const bool ok = in & r.ok & c.ok & (oh >= 0) & (ow >= 0) & (oh < OH) & (ow < OW);
-    return stage_f4(dy + r.off + c.off, ok);
+    return stage_f4(dy + (uint32_t)(r.off + c.off), ok);
   }
 };
 
@@ -237,7 +243,7 @@ struct CatRowsI {
   static constexpr bool KCONTIG = false;
   struct R {
     typename Src::R p;
-    long long dyoff;
+    uint32_t dyoff;
     bool ok;
   };
   struct C {
@@ -254,7 +260,7 @@ struct CatRowsI {
   int rows;
   __device__ __forceinline__ R row(int r) const {
     const bool ok = r < rows;
-    return R{src.row(ok ? r : 0), ok ? (long long)r * ldy : 0, ok};
+    return R{src.row(ok ? r : 0), ok ? (uint32_t)r * (uint32_t)ldy : 0u, ok};
   }
   __device__ __forceinline__ C col(int j) const {
     C c;
@@ -271,8 +277,8 @@ struct CatRowsI {
     constexpr bool FP = std::is_same<typename Src::elem_t, float>::value;
     const bool rin = in && r.ok;
     const float* a = (c.seg == 2 && rin) ? homog_run() : zero_run();
-    a = (c.seg == 1 && rin) ? dy + r.dyoff + c.jj : a;
-    if constexpr (FP) a = (c.seg == 0 && rin && r.p.ok && c.p.ok) ? src.x + r.p.off + c.p.off : a;
+    a = (c.seg == 1 && rin) ? dy + (r.dyoff + (uint32_t)c.jj) : a;
+    if constexpr (FP) a = (c.seg == 0 && rin && r.p.ok && c.p.ok) ? src.x + (r.p.off + c.p.off) : a;
     return *reinterpret_cast<const float4*>(a);
   }
 };
@@ -287,12 +293,12 @@ struct MatI {
   int ld;
   int K;
   int N;
-  __device__ __forceinline__ R row(int k) const { return R{(long long)k * ld, k < K}; }
+  __device__ __forceinline__ R row(int k) const { return R{(uint32_t)k * (uint32_t)ld, k < K}; }
   __device__ __forceinline__ C col(int j) const { return j; }
   using St = StF4;
   __device__ __forceinline__ St stage(const R& r, const C& j, bool in) const {
     const bool ok = in && r.ok && j < N;
-    const float* p = m + r.off + j;
+    const float* p = m + (r.off + (uint32_t)j);
     if constexpr (ALIGNED) {  // N % 4 == 0
       return stage_f4(p, ok);
     } else {
@@ -312,12 +318,12 @@ struct MatTK {
   int ld;
   int K;
   int N;
-  __device__ __forceinline__ R row(int j) const { return R{(long long)j * ld, j < N}; }
+  __device__ __forceinline__ R row(int j) const { return R{(uint32_t)j * (uint32_t)ld, j < N}; }
   __device__ __forceinline__ C col(int k) const { return k; }
   using St = StF4;
   __device__ __forceinline__ St stage(const R& r, const C& k, bool in) const {
     const bool ok = in && r.ok && k < K;
-    const float* p = m + r.off + k;
+    const float* p = m + (r.off + (uint32_t)k);
     if constexpr (ALIGNED) {  // K % 4 == 0
       return stage_f4(p, ok);
     } else {
@@ -338,7 +344,7 @@ struct ConvTWeights {
   using R = OffOk;
   using C = OffOk;
   const float* w;  // HWIO
-  __device__ __forceinline__ R row(int j) const { return R{(long long)j * COUT, j < CIN}; }
+  __device__ __forceinline__ R row(int j) const { return R{(uint32_t)j * COUT, j < CIN}; }
   __device__ __forceinline__ C col(int k) const {
     if (k >= K) return C{0, false};
     const int ph = blockIdx.z / S;
@@ -349,12 +355,12 @@ struct ConvTWeights {
     const int co = rem - kwp * COUT;
     const int kh = ph + S * khp;
     const int kw = pw + S * kwp;
-    return C{(long long)(kh * KW + kw) * CIN * COUT + co, true};
+    return C{(uint32_t)((kh * KW + kw) * CIN * COUT + co), true};
   }
   using St = StF4;
   __device__ __forceinline__ St stage(const R& r, const C& c, bool in) const {
     const bool ok = in && r.ok && c.ok;
-    return stage_f4(w + r.off + c.off, ok);
+    return stage_f4(w + (r.off + c.off), ok);
   }
 };
 

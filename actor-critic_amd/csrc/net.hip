@@ -199,7 +199,7 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   const long long st = act_img_stride;
   {  // conv1: [B,84,84,4]u8 -> [B,20,20,32]
     using Src = ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>;
-    RowsAsK<Src> opA{Src{obs, img_stride, B * 400}};
+    RowsAsK<Src> opA{Src{obs, (uint32_t)img_stride, B * 400}};
     MatI<true> opB{P + L.off[0], 32, 256, 32};
     EpiAct epi{a->a1, P + L.off[1], 32, 400, st * 400 * 32};
     prof_begin(ACMI_PROF_CONV1_FWD, s);
@@ -208,14 +208,14 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   }
   {  // conv2: -> [B,9,9,64]
     using Src = ConvRows<float, 20, 20, 32, 4, 4, 2>;
-    RowsAsK<Src> opA{Src{a->a1, st * 400 * 32, B * 81}};
+    RowsAsK<Src> opA{Src{a->a1, (uint32_t)(st * 400 * 32), B * 81}};
     MatI<true> opB{P + L.off[2], 64, 512, 64};
     EpiAct epi{a->a2, P + L.off[3], 64, 81, st * 81 * 64};
     launch_gemm<128, 64, 32, 2, 1, false, false>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
   }
   {  // conv3: -> [B,7,7,C3]
     using Src = ConvRows<float, 9, 9, 64, 3, 3, 1>;
-    RowsAsK<Src> opA{Src{a->a2, st * 81 * 64, B * 49}};
+    RowsAsK<Src> opA{Src{a->a2, (uint32_t)(st * 81 * 64), B * 49}};
     MatI<true> opB{P + L.off[4], C3, 576, C3};
     EpiAct epi{a->a3, P + L.off[5], C3, 49, st * 49 * C3};
     if constexpr (C3 == 32)
@@ -351,7 +351,7 @@ static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows) {
   p.J = p.kp + p.cout_pad + (with_stats ? 1 : 0);
   if (with_stats)
     plan_rounds(rows, live_tiles<128, 128>(p.I, p.J, K),
-                kCUs * gemm_blocks_per_cu<128, 128, 32, false, false>(), &p.nc, &p.ch);
+                kCUs * gemm_blocks_per_cu<128, 128, 16, false, false>(), &p.nc, &p.ch);
   else
     plan_rounds(rows, live_tiles<128, 32>(p.I, p.J, 0),
                 kCUs * gemm_blocks_per_cu<128, 32, 32, false, false>(), &p.nc, &p.ch);
@@ -390,7 +390,7 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
   EpiPartial epi{part, I, J};
   prof_begin(site, s);
   if (with_stats)  // only the upper triangle of the symmetric [P]^T[P] block
-    launch_gemm<128, 128, 32, 2, 2, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s, K);
+    launch_gemm<128, 128, 16, 2, 2, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s, K);
   else
     launch_gemm<128, 32, 32, 1, 1, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s);
   prof_end(site, s);
@@ -469,7 +469,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     RowsAsK<Src> opA{Src{bw->d2, B * Src::L}};
     ConvTWeights<4, 4, 2, 32, 64> opB{P + L.off[2]};
     EpiConvTPhase<20, 20, 2, 32> epi{bw->d1, a->a1};
-    launch_gemm<256, 32, 32, 2, 1, false, false>(opA, opB, epi, B * Src::L, 32, Src::COLS, 4, 0, s);
+    launch_gemm<128, 32, 32, 1, 1, false, false>(opA, opB, epi, B * Src::L, 32, Src::COLS, 4, 0, s);
   }
   ACMI_LAUNCH_CHECK("dx_chain");
   return ACMI_OK;
@@ -507,7 +507,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // conv1: patches of the u8 observations
   // conv1: weight gradient on the f32 engine; its A factor from the u8 frames on
   // the i8 matrix cores (exact integer sums, afactor_u8.hip)
-  rc = wgrad_layer(ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>{obs, img_stride, B * 400}, 256,
+  rc = wgrad_layer(ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>{obs, (uint32_t)img_stride, B * 400}, 256,
                    400LL * B, bw->d1, 32, 32, false, part, ws_cap, grads + L.off[0], 32, nullptr,
                    nullptr, s, ACMI_PROF_CONV1_WGRAD);
   if (rc || !st) return rc;
@@ -613,6 +613,12 @@ int acmi_kfac_layout(int A, int C3, int64_t* din, int64_t* dout, int64_t* so, in
   return ACMI_OK;
 }
 
+// The GEMM operand loaders address with 32-bit element offsets (gemm_ops.hpp):
+// every buffer a launch reads must span < 2^31 elements.
+static bool spans32(long long rows, long long stride, long long per_row) {
+  return rows <= 0 || (rows - 1) * stride + per_row < (1LL << 31);
+}
+
 static int forward_dispatch(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride,
                             int B, const acmi_acts_t* acts, int want_value,
                             long long act_stride, acmi_stream_t stream) {
@@ -626,6 +632,8 @@ static int forward_dispatch(const acmi_net_t* net, const uint8_t* obs, int64_t i
                    acts->ld_logits >= net->num_actions && (!want_value || acts->value),
                ACMI_ERR_ARG, "acmi_forward: bad activation buffers");
   ACMI_REQUIRE(act_stride >= 1, ACMI_ERR_ARG, "bad activation stride");
+  ACMI_REQUIRE(spans32(B, img_stride, 84 * 84 * 4) && spans32(B, act_stride * 400 * 32, 400 * 32),
+               ACMI_ERR_ARG, "acmi_forward: batch spans >= 2^31 elements (B=%d)", B);
   if (B == 0) return ACMI_OK;
   hipStream_t s = (hipStream_t)stream;
   if (L.C3 == 32)
@@ -674,6 +682,8 @@ int acmi_backward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride,
                "acmi_backward: bad B / img_stride");
   ACMI_REQUIRE(bwd->ldh >= net->num_actions + 1 && bwd->ldh % 4 == 0, ACMI_ERR_ARG,
                "acmi_backward: ldh must be >= A+1 and a multiple of 4 (zero padded)");
+  ACMI_REQUIRE(spans32(B, img_stride, 84 * 84 * 4) && spans32(B, 400 * 32, 400 * 32), ACMI_ERR_ARG,
+               "acmi_backward: batch spans >= 2^31 elements (B=%d)", B);
   const long long cap = acmi_backward_ws_floats(B, net->num_actions, net->conv3_filters);
   hipStream_t s = (hipStream_t)stream;
   if (L.C3 == 32)
@@ -690,7 +700,7 @@ int acmi_kfac_output_stats(const acmi_net_t* net, int B, const acmi_acts_t* acts
   ACMI_REQUIRE(net && acts && bwd && g_stats && ws, ACMI_ERR_ARG,
                "acmi_kfac_output_stats: null argument");
   ACMI_REQUIRE(make_layout(net->num_actions, net->conv3_filters, &L), ACMI_ERR_ARG, "bad net");
-  ACMI_REQUIRE(B > 0, ACMI_ERR_ARG, "bad B");
+  ACMI_REQUIRE(B > 0 && spans32(B, 400 * 32, 400 * 32), ACMI_ERR_ARG, "bad B");
   const long long cap = acmi_backward_ws_floats(B, net->num_actions, net->conv3_filters);
   hipStream_t s = (hipStream_t)stream;
   if (L.C3 == 32)

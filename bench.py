@@ -100,7 +100,7 @@ def main():
         torch.cuda.synchronize()
         parallel.barrier()
         torch.cuda.synchronize()
-        site = _lib.PROF_CONV1_WGRAD
+        site = _lib.PROF_CONV2_WGRAD
         _lib.call('acmi_prof_enable', site, max(1, args.steps))
         marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
         inv_flags = []
@@ -125,17 +125,29 @@ def main():
     upd_plain = [u for u, f in zip(upd_ms, inv_flags) if not f]
     mean = lambda xs: (sum(xs) / len(xs)) if xs else None
 
-    # dominant kernel: conv1 weight gradient fused with the K-FAC A factor,
-    # [P;1]^T [P | dY | 1] over M*400 patch rows: algorithmic 2*400*257*(257+32)
-    # FLOP per sample (A factor 257^2 + dW 257x32 per conv1 location)
+    # dominant kernel: conv2 weight gradient fused with the K-FAC A factor,
+    # [P;1]^T [P | dY | 1] over the M*81 conv2 output pixels, P = 4x4x32 patches.
+    # Algorithmic FLOP per pixel = 2 * (unique outputs): the symmetric 513x513
+    # A factor counted once (513*514/2) plus the 513x64 [dW;db] block
+    # (DESIGN.md "Roofline").  The kernel executes 14 128x128 tiles per pixel
+    # (2*14*128*128 FLOP), reported as executed_tflops.
     M = N * T
-    kern_flops = 2.0 * 400 * 257 * (257 + 32) * M if acktr else 2.0 * 400 * 257 * 32 * M
+    rows = 81 * M
+    if acktr:
+        kern_flops = 2.0 * (513 * 514 / 2 + 513 * 64) * rows
+        exec_flops = 2.0 * 14 * 128 * 128 * rows
+        kern_name = 'conv2 wgrad + K-FAC A-factor reduction GEMM (f32 MFMA)'
+    else:
+        kern_flops = 2.0 * 513 * 64 * rows
+        exec_flops = 2.0 * 8 * 128 * 32 * rows
+        kern_name = 'conv2 wgrad reduction GEMM (f32 MFMA)'
     kern_ms = tot_ms.value / max(1, cnt.value)
     achieved = kern_flops / (kern_ms * 1e-3) / 1e12 if cnt.value else None
-    roofline = {'bound': 'mfma', 'kernel': 'conv1 wgrad+A-factor reduction GEMM (f32 MFMA)',
+    roofline = {'bound': 'mfma', 'kernel': kern_name,
                 'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                 'frac': (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None, 'traffic': None,
-                'launches': cnt.value, 'avg_ms': kern_ms, 'flops_per_launch': kern_flops}
+                'launches': cnt.value, 'avg_ms': kern_ms, 'flops_per_launch': kern_flops,
+                'executed_tflops': exec_flops / (kern_ms * 1e-3) / 1e12 if cnt.value else None}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
