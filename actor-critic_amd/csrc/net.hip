@@ -137,7 +137,10 @@ inline int roundup4(int x) { return (x + 3) & ~3; }
 
 // policy/value heads, one wave per row: the 512-long dot products of a4 with
 // the A+1 head columns, lane-strided partial sums + a butterfly (fixed order).
-__global__ __launch_bounds__(256) void heads_kernel(const float* a4, long long a4_stride, int B,
+// With part != nullptr the row of a4 is first finalised from fc4's split-K
+// partial slabs [nz][B+1][512] (relu(sum_z + b4), fixed z order) and stored.
+__global__ __launch_bounds__(256) void heads_kernel(const float* part, int nz, const float* b4,
+                                                    float* a4, long long a4_stride, int B,
                                                     const float* wpi, const float* bpi,
                                                     const float* wv, const float* bv, int A,
                                                     float* logits, long long l_stride,
@@ -145,10 +148,22 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* a4, long long a
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= B) return;
-  const float* x = a4 + (long long)row * a4_stride;
+  float* x = a4 + (long long)row * a4_stride;
   float xv[8];
+  if (part) {
+    const long long zs = (long long)(B + 1) * 512;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) xv[e] = x[lane + 64 * e];
+    for (int e = 0; e < 8; ++e) {
+      const int j = lane + 64 * e;
+      float acc = 0.f;
+      for (int z = 0; z < nz; ++z) acc += part[z * zs + (long long)row * 512 + j];
+      xv[e] = fmaxf(acc + b4[j], 0.f);
+      x[j] = xv[e];
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xv[e] = x[lane + 64 * e];
+  }
   for (int a = 0; a < A; ++a) {
     float s = 0.f;
 #pragma unroll
@@ -163,18 +178,6 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* a4, long long a
     s = wave_sum(s);
     if (lane == 0) value[(long long)row * v_stride] = s + bv[0];
   }
-}
-
-// fc4 split-K: partial slabs [z][B+1][512] -> relu(sum_z + bias) (fixed z order)
-__global__ void fc_splitk_finalize(const float* part, int nz, int B, const float* bias,
-                                   float* out, long long row_stride) {
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long long)B * 512) return;
-  const int i = (int)(idx / 512), j = (int)(idx - (long long)i * 512);
-  const long long zs = (long long)(B + 1) * 512;
-  float s = 0.f;
-  for (int z = 0; z < nz; ++z) s += part[z * zs + idx];
-  out[(long long)i * row_stride + j] = fmaxf(s + bias[j], 0.f);
 }
 
 // split factor for fc4 at small batch (64 x 128 tiles over 512 columns)
@@ -203,7 +206,11 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     MatI<true> opB{P + L.off[0], 32, 256, 32};
     EpiAct epi{a->a1, P + L.off[1], 32, 400, st * 400 * 32};
     prof_begin(ACMI_PROF_CONV1_FWD, s);
-    launch_gemm<256, 32, 32, 2, 1, false, false>(opA, opB, epi, B * 400, 32, 256, 1, 0, s);
+    // rollout-size batches fill the chip better with 128-row tiles
+    if (B <= 2048)
+      launch_gemm<128, 32, 32, 1, 1, false, false>(opA, opB, epi, B * 400, 32, 256, 1, 0, s);
+    else
+      launch_gemm<256, 32, 32, 2, 1, false, false>(opA, opB, epi, B * 400, 32, 256, 1, 0, s);
     prof_end(ACMI_PROF_CONV1_FWD, s);
   }
   {  // conv2: -> [B,9,9,64]
@@ -211,7 +218,10 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     RowsAsK<Src> opA{Src{a->a1, (uint32_t)(st * 400 * 32), B * 81}};
     MatI<true> opB{P + L.off[2], 64, 512, 64};
     EpiAct epi{a->a2, P + L.off[3], 64, 81, st * 81 * 64};
-    launch_gemm<128, 64, 32, 2, 1, false, false>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
+    if (B <= 2048)
+      launch_gemm<64, 64, 32, 1, 1, false, false>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
+    else
+      launch_gemm<128, 64, 32, 2, 1, false, false>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
   }
   {  // conv3: -> [B,7,7,C3]
     using Src = ConvRows<float, 9, 9, 64, 3, 3, 1>;
@@ -223,28 +233,28 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     else
       launch_gemm<128, 64, 32, 2, 1, false, false>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
   }
-  {  // fc4: [B,49*C3] -> [B,512]
-    const int K = 49 * C3;
-    // rows are images; with an image stride the dense row stride is st*K
-    RowsAsK<DenseRows> opA{DenseRows{a->a3, (int)(st * K), B, K}};
-    MatI<true> opB{P + L.off[6], 512, K, 512};
-    int nz, chunk;
-    fc4_plan(B, K, &nz, &chunk);
-    if (nz > 1 && a->ws && a->ws_floats >= (long long)nz * (B + 1) * 512) {
-      // small (rollout) batches: split K over blockIdx.z, fixed-order reduce
-      EpiPartial epi{a->ws, B, 512};
-      launch_gemm<64, 128, 32, 1, 2, true, false>(opA, opB, epi, B, 512, K, nz, chunk, s);
-      hipLaunchKernelGGL(fc_splitk_finalize, dim3(cdiv((long long)B * 512, 256)), dim3(256), 0, s,
-                         a->ws, nz, B, P + L.off[7], a->a4, st * 512);
-    } else {
-      EpiAct epi{a->a4, P + L.off[7], 512, 1, st * 512};
-      launch_gemm<64, 128, 32, 1, 2, false, false>(opA, opB, epi, B, 512, K, 1, 0, s);
-    }
+  // fc4: [B,49*C3] -> [B,512]
+  const int K4 = 49 * C3;
+  // rows are images; with an image stride the dense row stride is st*K4
+  RowsAsK<DenseRows> opA4{DenseRows{a->a3, (int)(st * K4), B, K4}};
+  MatI<true> opB4{P + L.off[6], 512, K4, 512};
+  int nz, chunk;
+  fc4_plan(B, K4, &nz, &chunk);
+  const bool split = nz > 1 && a->ws && a->ws_floats >= (long long)nz * (B + 1) * 512;
+  if (split) {
+    // small (rollout) batches: split K over chunks; the heads kernel reduces
+    // the slabs in fixed order and applies bias + relu
+    EpiPartial epi{a->ws, B, 512};
+    launch_gemm<64, 128, 32, 1, 2, true, false>(opA4, opB4, epi, B, 512, K4, nz, chunk, s);
+  } else {
+    EpiAct epi{a->a4, P + L.off[7], 512, 1, st * 512};
+    launch_gemm<64, 128, 32, 1, 2, false, false>(opA4, opB4, epi, B, 512, K4, 1, 0, s);
   }
   // heads: [B,512] -> logits [B,A], value [B]
-  hipLaunchKernelGGL(heads_kernel, dim3(cdiv(B, 4)), dim3(256), 0, s, a->a4, st * 512, B,
-                     P + L.off[8], P + L.off[9], P + L.off[10], P + L.off[11], L.A, a->logits,
-                     st * a->ld_logits, want_value ? a->value : nullptr, st);
+  hipLaunchKernelGGL(heads_kernel, dim3(cdiv(B, 4)), dim3(256), 0, s, split ? a->ws : nullptr, nz,
+                     P + L.off[7], a->a4, st * 512, B, P + L.off[8], P + L.off[9], P + L.off[10],
+                     P + L.off[11], L.A, a->logits, st * a->ld_logits,
+                     want_value ? a->value : nullptr, st);
   ACMI_LAUNCH_CHECK("acmi_forward");
   return ACMI_OK;
 }
