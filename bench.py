@@ -32,6 +32,22 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32-input MFMA peak
 HBM_PEAK_GBS = 8000.0
 
 
+def measured_traffic(kernel, workload):
+    """HBM bytes per launch of the roofline kernel from the newest committed PMC
+    summary (profiles/*/pmc_traffic.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE,
+    separate passes) when it was measured on this kernel and workload; else None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*', 'pmc_traffic.json')), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get('kernel') == kernel and d.get('workload') == workload:
+            return d.get('hbm_bytes_per_launch')
+    return None
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
@@ -143,9 +159,10 @@ def main():
         kern_name = 'conv2 wgrad reduction GEMM (f32 MFMA)'
     kern_ms = tot_ms.value / max(1, cnt.value)
     achieved = kern_flops / (kern_ms * 1e-3) / 1e12 if cnt.value else None
+    traffic = measured_traffic(kern_name, 'Breakout {} {} envs/GPU x {} steps'.format(args.algo.upper(), N, T))
     roofline = {'bound': 'mfma', 'kernel': kern_name,
                 'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                'frac': (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None, 'traffic': None,
+                'frac': (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None, 'traffic': traffic,
                 'launches': cnt.value, 'avg_ms': kern_ms, 'flops_per_launch': kern_flops,
                 'executed_tflops': exec_flops / (kern_ms * 1e-3) / 1e12 if cnt.value else None}
 
