@@ -49,9 +49,20 @@ class Layout(object):
         _lib.call('acmi_kfac_layout', A, C3, din, dout, so, ctypes.byref(tot))
         self.din, self.dout, self.stat_off, self.stat_total = list(din), list(dout), list(so), tot.value
         self.inv_total = int(lib.acmi_kfac_inverse_floats(A, C3))
+        ioff = (ctypes.c_int64 * 12)()
+        ild = (ctypes.c_int64 * 12)()
+        _lib.call('acmi_kfac_inverse_layout', A, C3, ioff, ild)
+        self.inv_off, self.inv_ld = list(ioff), list(ild)
         self.shapes = [(8, 8, 4, 32), (32,), (4, 4, 32, 64), (64,), (3, 3, 64, C3), (C3,), (49 * C3, 512), (512,),
                        (512, A), (A,), (512, 1), (1,)]
         self.names = ['conv1', 'conv2', 'conv3', 'fc4', 'fc_policy', 'fc_baseline']
+
+    def inverse_block(self, inv, m):
+        """[n, n] view of inverse block m (2l: Ainv_l, 2l+1: Ginv_l) of a flat
+        inverse buffer (rows padded to inv_ld[m], acmi_kfac_inverse_layout)."""
+        n = self.dout[m // 2] if m % 2 else self.din[m // 2]
+        o, ld = self.inv_off[m], self.inv_ld[m]
+        return inv[o:o + n * ld].view(n, ld)[:, :n]
 
     def init_params(self, seed=0):
         """Orthogonal init with gains sqrt(2) / 0.01 / 1.0 and zero biases."""

@@ -67,6 +67,7 @@ _SIGS = {
     'acmi_kfac_output_stats': (c_int, [ctypes.POINTER(Net), c_int, ctypes.POINTER(Acts), ctypes.POINTER(Bwd),
                                        c_u32, c_u32, c_u32, c_vp, c_vp, c_vp]),
     'acmi_kfac_ema': (c_int, [c_vp, c_vp, c_vp, c_i64, c_float, c_float, c_float, c_vp]),
+    'acmi_kfac_inverse_layout': (c_int, [c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     'acmi_kfac_inverse_floats': (c_i64, [c_int, c_int]),
     'acmi_kfac_inverse_ws_doubles': (c_i64, [c_int, c_int]),
     'acmi_kfac_inverse': (c_int, [c_int, c_int, c_vp, c_float, c_int, c_vp, c_vp, c_vp]),

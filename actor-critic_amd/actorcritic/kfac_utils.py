@@ -100,12 +100,8 @@ class KfacOptimizer(Optimizer):
             coeff=z(1))
         # kfac initialises the inverse variables to the identity (used until the first
         # inverse update, i.e. between the cold start and gs = cold + invert_every)
-        inv = s['inv']
-        o = 0
-        for l in range(6):
-            for d in (L.din[l], L.dout[l]):
-                inv[o:o + d * d].view(d, d).fill_diagonal_(1.0)
-                o += d * d
+        for m in range(12):
+            L.inverse_block(s['inv'], m).fill_diagonal_(1.0)
         self._state = s
         return s
 

@@ -24,6 +24,7 @@ struct KLayout {
   long long poff[12];  // param offsets
   long long nparams;
   long long inv_off[12];  // Ainv_l at [2l], Ginv_l at [2l+1]
+  long long inv_ld[12];   // row stride of each inverse block (n rounded up to 4)
   long long inv_total;
 };
 
@@ -39,12 +40,14 @@ static bool klayout(int A, int C3, KLayout* K) {
   K->stat_total = tot;
   for (int i = 0; i < 12; ++i) K->poff[i] = off[i];
   K->nparams = acmi_param_count(A, C3);
+  // inverse blocks are n x ld, ld = n rounded up to 4 (zero padding columns):
+  // the preconditioning GEMMs then read every row as aligned float4 runs
   long long o = 0;
-  for (int l = 0; l < 6; ++l) {
-    K->inv_off[2 * l] = o;
-    o += K->din[l] * K->din[l];
-    K->inv_off[2 * l + 1] = o;
-    o += K->dout[l] * K->dout[l];
+  for (int m = 0; m < 12; ++m) {
+    const long long n = (m & 1) ? K->dout[m / 2] : K->din[m / 2];
+    K->inv_off[m] = o;
+    K->inv_ld[m] = (n + 3) / 4 * 4;
+    o += n * K->inv_ld[m];
   }
   K->inv_total = o;
   return true;
@@ -251,18 +254,19 @@ struct OutSet {
   long long m_off[12];
   int n[12];
   int np[12];
+  int ld[12];
   long long dst_off[12];
 };
 __global__ void gj_store_kernel(OutSet o, float* inv) {
   const int m = blockIdx.y;
-  const int n = o.n[m], np = o.np[m];
+  const int n = o.n[m], np = o.np[m], ld = o.ld[m];
   const double* M = o.ws + o.m_off[m];
   float* dst = inv + o.dst_off[m];
-  const long long tot = (long long)n * n;
+  const long long tot = (long long)n * ld;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
        e += (long long)gridDim.x * blockDim.x) {
-    const int r = (int)(e / n), c = (int)(e - (long long)r * n);
-    dst[e] = (float)(0.5 * (M[(long long)r * np + c] + M[(long long)c * np + r]));
+    const int r = (int)(e / ld), c = (int)(e - (long long)r * ld);
+    dst[e] = c < n ? (float)(0.5 * (M[(long long)r * np + c] + M[(long long)c * np + r])) : 0.f;
   }
 }
 
@@ -422,6 +426,17 @@ int acmi_kfac_ema(float* biased, float* factors, const float* stats, int64_t n, 
   return ACMI_OK;
 }
 
+int acmi_kfac_inverse_layout(int A, int C3, int64_t* offsets, int64_t* lds) {
+  KLayout K;
+  ACMI_REQUIRE(offsets && lds && klayout(A, C3, &K), ACMI_ERR_ARG,
+               "acmi_kfac_inverse_layout: bad arguments");
+  for (int m = 0; m < 12; ++m) {
+    offsets[m] = K.inv_off[m];
+    lds[m] = K.inv_ld[m];
+  }
+  return ACMI_OK;
+}
+
 int64_t acmi_kfac_inverse_floats(int A, int C3) {
   KLayout K;
   if (!klayout(A, C3, &K)) return -1;
@@ -522,6 +537,7 @@ int acmi_kfac_inverse(int A, int C3, const float* factors, float damping, int co
     o.m_off[m] = s.m_off[m];
     o.n[m] = s.n[m];
     o.np[m] = s.np[m];
+    o.ld[m] = (int)K.inv_ld[m];
     o.dst_off[m] = K.inv_off[m];
   }
   hipLaunchKernelGGL(gj_store_kernel, dim3(256, 12), dim3(256), 0, st, o, inv);
@@ -618,7 +634,7 @@ int64_t acmi_kfac_step_ws_floats(int A, int C3) {
   KLayout K;
   if (!klayout(A, C3, &K)) return -1;
   long long m = 0;
-  for (int l = 0; l < 6; ++l) m = std::max(m, K.din[l] * K.dout[l]);
+  for (int l = 0; l < 6; ++l) m = std::max(m, K.din[l] * K.inv_ld[2 * l + 1]);
   return m + KRED + 16;
 }
 
@@ -630,34 +646,42 @@ int acmi_kfac_step(int A, int C3, float* params, float* velocity, const float* g
                ACMI_ERR_ARG, "acmi_kfac_step: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   long long tmax = 0;
-  for (int l = 0; l < 6; ++l) tmax = std::max(tmax, K.din[l] * K.dout[l]);
+  for (int l = 0; l < 6; ++l) tmax = std::max(tmax, K.din[l] * K.inv_ld[2 * l + 1]);
   float* t1 = ws;
   float* part = ws + tmax;
   float* coeff = part + KRED;
   for (int l = 0; l < 6; ++l) {
     const int din = (int)K.din[l], dout = (int)K.dout[l];
+    const int lda = (int)K.inv_ld[2 * l], ldg = (int)K.inv_ld[2 * l + 1];
     const float* ainv = inv + K.inv_off[2 * l];
     const float* ginv = inv + K.inv_off[2 * l + 1];
     const float* g = grads + K.poff[2 * l];  // [W; b] contiguous, din x dout
     float* out = precon + K.poff[2 * l];
-    // t1 = Ainv g  (Ainv symmetric: A(k,i) = Ainv[k][i])
-    MatI<false> a1{ainv, din, din, din};
-    MatI<false> b1{g, dout, din, dout};
-    EpiStore e1{t1, dout};
+    // t1 = Ainv g  (Ainv symmetric: A(k,i) = Ainv[k][i]); t1 rows padded to ldg
+    MatI<true> a1{ainv, lda, din, din};
+    EpiStore e1{t1, ldg};
     // out = t1 Ginv
-    MatTKu a2{t1, dout, dout, din};
-    MatI<false> b2{ginv, dout, dout, dout};
+    MatTK<true> a2{t1, ldg, dout, din};
+    MatI<true> b2{ginv, ldg, dout, dout};
     EpiStore e2{out, dout};
-    if (dout >= 128) {
-      launch_gemm<128, 128, 32, 2, 2, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
-      launch_gemm<128, 128, 32, 2, 2, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
-    } else if (dout > 32) {
-      launch_gemm<128, 64, 32, 2, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
-      launch_gemm<128, 64, 32, 2, 1, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
-    } else {
+    if (dout % 4 == 0) {
+      MatI<true> b1{g, dout, din, dout};
+      if (dout >= 128)
+        launch_gemm<128, 128, 32, 2, 2, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
+      else if (dout > 32)
+        launch_gemm<128, 64, 32, 2, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
+      else
+        launch_gemm<128, 32, 32, 1, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
+    } else {  // the value head (dout = 1): unaligned rows of g
+      MatI<false> b1{g, dout, din, dout};
       launch_gemm<128, 32, 32, 1, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
-      launch_gemm<128, 32, 32, 1, 1, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
     }
+    if (dout >= 128)
+      launch_gemm<128, 128, 32, 2, 2, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
+    else if (dout > 32)
+      launch_gemm<128, 64, 32, 2, 1, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
+    else
+      launch_gemm<128, 32, 32, 1, 1, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
   }
   const long long n = K.nparams;
   hipLaunchKernelGGL(kdot_partial_kernel, dim3(KRED), dim3(256), 0, s, grads, precon, n, part);

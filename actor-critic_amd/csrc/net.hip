@@ -92,29 +92,19 @@ bool get_layout(int A, int C3, Layout* L) { return make_layout(A, C3, L); }
 // ---------------------------------------------------------------------------
 // small helpers
 // ---------------------------------------------------------------------------
-// transposed heads weights: B(k = a, j) = a<A ? pi.W[j][a] : a==A ? v.W[j] : 0
-struct HeadsWT {
-  static constexpr bool KCONTIG = true;
-  using R = int;  // j
-  using C = int;  // a
-  const float* wpi;
-  const float* wv;
-  int A;
-  // branch-free: both candidate loads come from clamped addresses
-  __device__ __forceinline__ float el(int a, int j) const {
-    const bool okj = j < 512;
-    const float p = wpi[okj && a < A ? j * A + a : 0];
-    const float v = wv[okj ? j : 0];
-    return (okj && a < A) ? p : ((okj && a == A) ? v : 0.f);
-  }
-  __device__ __forceinline__ R row(int j) const { return j; }
-  __device__ __forceinline__ C col(int a) const { return a; }
-  using St = float4;  // tiny operand (K = ldh): masked at load time
-  __device__ __forceinline__ St stage(const R& j, const C& k, bool in) const {
-    const float4 v = make_float4(el(k, j), el(k + 1, j), el(k + 2, j), el(k + 3, j));
-    return in ? v : f4zero();
-  }
-};
+// d4 = (dhead [W_pi | w_v]^T) * relu'(a4): A+1 MACs per output, elementwise
+// over [B][512] (memory-bound); the k-ordered fmaf chain is the f32 MFMA's.
+__global__ void heads_dx_kernel(const float* dhead, int ldh, int B, const float* wpi,
+                                const float* wv, int A, const float* a4, float* d4) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)B * 512) return;
+  const int m = (int)(idx >> 9), j = (int)(idx & 511);
+  const float* g = dhead + (long long)m * ldh;
+  float acc = 0.f;
+  for (int a = 0; a < A; ++a) acc = __builtin_fmaf(g[a], wpi[j * A + a], acc);
+  acc = __builtin_fmaf(g[A], wv[j], acc);
+  d4[idx] = a4[idx] > 0.f ? acc : 0.f;
+}
 
 // conv/fc epilogue with an image remap so the rollout can write step t of an
 // env-major [N][T][rows] activation buffer in place.
@@ -139,6 +129,7 @@ inline int roundup4(int x) { return (x + 3) & ~3; }
 // the A+1 head columns, lane-strided partial sums + a butterfly (fixed order).
 // With part != nullptr the row of a4 is first finalised from fc4's split-K
 // partial slabs [nz][B+1][512] (relu(sum_z + b4), fixed z order) and stored.
+template <int NZ>
 __global__ __launch_bounds__(256) void heads_kernel(const float* part, int nz, const float* b4,
                                                     float* a4, long long a4_stride, int B,
                                                     const float* wpi, const float* bpi,
@@ -150,13 +141,20 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* part, int nz, c
   if (row >= B) return;
   float* x = a4 + (long long)row * a4_stride;
   float xv[8];
-  if (part) {
+  if (NZ > 0) {
+    // all NZ x 8 slab loads are issued before the (fixed-order) sums
     const long long zs = (long long)(B + 1) * 512;
+    float v[NZ > 0 ? NZ : 1][8];
+#pragma unroll
+    for (int z = 0; z < NZ; ++z)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[z][e] = part[z * zs + (long long)row * 512 + lane + 64 * e];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int j = lane + 64 * e;
       float acc = 0.f;
-      for (int z = 0; z < nz; ++z) acc += part[z * zs + (long long)row * 512 + j];
+#pragma unroll
+      for (int z = 0; z < NZ; ++z) acc += v[z][e];
       xv[e] = fmaxf(acc + b4[j], 0.f);
       x[j] = xv[e];
     }
@@ -251,10 +249,25 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     launch_gemm<64, 128, 32, 1, 2, false, false>(opA4, opB4, epi, B, 512, K4, 1, 0, s);
   }
   // heads: [B,512] -> logits [B,A], value [B]
-  hipLaunchKernelGGL(heads_kernel, dim3(cdiv(B, 4)), dim3(256), 0, s, split ? a->ws : nullptr, nz,
-                     P + L.off[7], a->a4, st * 512, B, P + L.off[8], P + L.off[9], P + L.off[10],
-                     P + L.off[11], L.A, a->logits, st * a->ld_logits,
-                     want_value ? a->value : nullptr, st);
+  const dim3 hg(cdiv(B, 4)), hb(256);
+  const float* hp = split ? a->ws : nullptr;
+  float* hv = want_value ? a->value : nullptr;
+#define ACMI_HEADS(NZ)                                                                        \
+  hipLaunchKernelGGL(heads_kernel<NZ>, hg, hb, 0, s, hp, nz, P + L.off[7], a->a4, st * 512, B, \
+                     P + L.off[8], P + L.off[9], P + L.off[10], P + L.off[11], L.A, a->logits, \
+                     st * a->ld_logits, hv, st)
+  switch (split ? nz : 0) {
+    case 0: ACMI_HEADS(0); break;
+    case 2: ACMI_HEADS(2); break;
+    case 3: ACMI_HEADS(3); break;
+    case 4: ACMI_HEADS(4); break;
+    case 5: ACMI_HEADS(5); break;
+    case 6: ACMI_HEADS(6); break;
+    case 7: ACMI_HEADS(7); break;
+    case 8: ACMI_HEADS(8); break;
+    default: ACMI_REQUIRE(false, ACMI_ERR_ARG, "fc4 split factor %d out of range", nz);
+  }
+#undef ACMI_HEADS
   ACMI_LAUNCH_CHECK("acmi_forward");
   return ACMI_OK;
 }
@@ -336,13 +349,82 @@ __global__ void finalize_cov_kernel(const float* part, int nchunk, int n,
 // G of the value head: element (A, A) of the heads product
 __global__ void finalize_cov_elem_kernel(const float* part, int nchunk, int n,
                                          int a, float* out, int rows) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  // one wave: lane-strided partial sums + a butterfly (fixed order)
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x >= 64 || blockIdx.x != 0) return;
   const long long cs = (long long)(n + 1) * n;
   const float* p = part + (long long)a * n + a;
   float s = 0.f;
-  for (int c = 0; c < nchunk; ++c) s += p[c * cs];
-  out[0] = s * (1.0f / (float)rows);
+  for (int c = lane; c < nchunk; c += 64) s += p[c * cs];
+  s = wave_sum(s);
+  if (lane == 0) out[0] = s * (1.0f / (float)rows);
 }
+
+// G = D^T D for narrow D (n <= NP, NP in {32, 64}) straight from global memory:
+// each wave streams row pairs (lane l: row 2q + (l>>5), column l&31 [+32]) as
+// the A and B fragments of v_mfma_f32_32x32x2_f32 (the Gram tile is D^T D of
+// the same registers), UNR k-steps of loads in flight; the block's 4 waves are
+// summed in LDS in a fixed order into part[chunk][NP+1][NP] (finalize_cov_*).
+template <int NP>
+__global__ __launch_bounds__(256) void gram_small_kernel(const float* D, int ld, int n,
+                                                        long long rows, long long chunk,
+                                                        float* part) {
+  constexpr int T = NP / 32;         // column tiles
+  constexpr int NT = T * (T + 1) / 2;  // upper-triangle tile pairs
+  constexpr int UNR = 8;
+  __shared__ float red[4][NP * NP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, c = lane & 31;
+  const long long r0 = (long long)blockIdx.x * chunk;
+  const long long r1 = min(rows, r0 + chunk);
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  const float* zero = zero_run();
+  for (long long base = r0 + 2 * wave; base < r1; base += 8 * UNR) {
+    float v[UNR][T];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const long long row = base + 8 * u + h;
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int col = c + 32 * t;
+        const bool ok = row < r1 && col < n;
+        v[u][t] = *(ok ? D + row * ld + col : zero);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      int t = 0;
+#pragma unroll
+      for (int x = 0; x < T; ++x)
+#pragma unroll
+        for (int y = x; y < T; ++y, ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u][x], v[u][y], acc[t], 0, 0, 0);
+    }
+  }
+  // acc[t][r]: tile (x, y), row 32x + (r&3) + 8(r>>2) + 4h, column 32y + c
+  {
+    int t = 0;
+#pragma unroll
+    for (int x = 0; x < T; ++x)
+#pragma unroll
+      for (int y = x; y < T; ++y, ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = 32 * x + (r & 3) + 8 * (r >> 2) + 4 * h, j = 32 * y + c;
+          red[wave][i * NP + j] = acc[t][r];
+          if (x != y) red[wave][j * NP + i] = acc[t][r];
+        }
+  }
+  __syncthreads();
+  float* out = part + (long long)blockIdx.x * (NP + 1) * NP;
+  for (int e = threadIdx.x; e < NP * NP; e += 256)
+    out[e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+}
+
 
 // split-K reductions fill whole rounds of resident blocks (plan_rounds):
 // MI355X has 256 CUs; blocks per CU follow from each config's LDS image
@@ -373,6 +455,15 @@ struct GcovPlan {
   int np, nc, ch;
   long long floats;
 };
+
+// narrow Gram: chunks of >= 512 rows, at most 2048 blocks (8 per CU)
+static void gram_plan(long long rows, int* nc, long long* chunk) {
+  long long n = std::min<long long>(2048, std::max<long long>(1, rows / 512));
+  long long ch = (rows + n - 1) / n;
+  ch = (ch + 63) / 64 * 64;
+  *chunk = ch;
+  *nc = (int)((rows + ch - 1) / ch);
+}
 
 static GcovPlan gcov_plan(int n, long long rows) {
   GcovPlan p;
@@ -415,13 +506,26 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
 static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
                       float* part, long long part_cap, float* out,
                       hipStream_t s, float* out_v = nullptr, int v_index = -1) {
-  const GcovPlan pl = gcov_plan(n, rows);
-  const int np = pl.np, nc = pl.nc, ch = pl.ch;
-  DenseRows src{g, ld, (int)rows, np};
-  RowsAsI<DenseRows> op{src};
-  ACMI_REQUIRE(pl.floats <= part_cap, ACMI_ERR_WS, "gcov workspace too small");
-  EpiPartial epi{part, np, np};
-  launch_gemm<64, 64, 32, 1, 1, true, false>(op, op, epi, np, np, (int)rows, nc, ch, s, np);
+  int np, nc;
+  if (n <= 64) {  // narrow: streaming Gram kernel
+    np = n <= 32 ? 32 : 64;
+    long long ch;
+    gram_plan(rows, &nc, &ch);
+    ACMI_REQUIRE((long long)nc * (np + 1) * np <= part_cap, ACMI_ERR_WS, "gcov workspace too small");
+    if (np == 32)
+      hipLaunchKernelGGL(gram_small_kernel<32>, dim3(nc), dim3(256), 0, s, g, ld, n, rows, ch, part);
+    else
+      hipLaunchKernelGGL(gram_small_kernel<64>, dim3(nc), dim3(256), 0, s, g, ld, n, rows, ch, part);
+  } else {
+    const GcovPlan pl = gcov_plan(n, rows);
+    np = pl.np;
+    nc = pl.nc;
+    DenseRows src{g, ld, (int)rows, np};
+    RowsAsI<DenseRows> op{src};
+    ACMI_REQUIRE(pl.floats <= part_cap, ACMI_ERR_WS, "gcov workspace too small");
+    EpiPartial epi{part, np, np};
+    launch_gemm<64, 64, 32, 1, 1, true, false>(op, op, epi, np, np, (int)rows, nc, pl.ch, s, np);
+  }
   hipLaunchKernelGGL(finalize_cov_kernel, dim3(cdiv((long long)sub * sub, 4)), dim3(256), 0,
                      s, part, nc, np, sub, out, (int)rows);
   if (out_v)
@@ -441,7 +545,15 @@ static long long bwd_partial_cap(int B, int A, int C3) {
     m = std::max(m, wgrad_plan(Ks[l], co[l], true, rowsL[l]).floats);
     m = std::max(m, wgrad_plan(Ks[l], co[l], false, rowsL[l]).floats);
     // G factors of the same layer's output
-    m = std::max(m, gcov_plan(co[l], rowsL[l]).floats);
+    if (co[l] <= 64) {
+      int nc;
+      long long ch;
+      gram_plan(rowsL[l], &nc, &ch);
+      const long long np = co[l] <= 32 ? 32 : 64;
+      m = std::max(m, nc * (np + 1) * np);
+    } else {
+      m = std::max(m, gcov_plan(co[l], rowsL[l]).floats);
+    }
   }
   m = std::max(m, conv1_afactor_ws_ints(rowsL[0]));
   return m;
@@ -454,12 +566,9 @@ template <int C3>
 static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a,
                     const acmi_bwd_t* bw, const float* dhead, int ldh,
                     hipStream_t s) {
-  {  // heads -> d4 = (dhead W_h^T) * relu'(a4)
-    RowsAsK<DenseRows> opA{DenseRows{dhead, ldh, B, ldh}};
-    HeadsWT opB{P + L.off[8], P + L.off[10], L.A};
-    EpiReluGrad epi{bw->d4, a->a4, 512};
-    launch_gemm<128, 128, 8, 2, 2, false, false>(opA, opB, epi, B, 512, ldh, 1, 0, s);
-  }
+  // heads -> d4 = (dhead W_h^T) * relu'(a4)
+  hipLaunchKernelGGL(heads_dx_kernel, dim3(cdiv((long long)B * 512, 256)), dim3(256), 0, s, dhead,
+                     ldh, B, P + L.off[8], P + L.off[10], L.A, a->a4, bw->d4);
   {  // fc4 -> d3 = (d4 W4^T) * relu'(a3)
     const int K3 = 49 * C3;
     RowsAsK<DenseRows> opA{DenseRows{bw->d4, 512, B, 512}};

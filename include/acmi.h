@@ -202,9 +202,14 @@ int acmi_kfac_ema(float* biased, float* factors, const float* stats,
  *   pi_l = sqrt((tr A_l / din_l) / (tr G_l / dout_l))
  *   Ainv_l = (A_l + pi_l*sqrt(lambda_l) I)^-1,  Ginv_l = (G_l + sqrt(lambda_l)/pi_l I)^-1
  * computed in fp64 (block Gauss-Jordan, SPD, no pivoting) and stored f32.
- * inv layout: for l = 0..5: Ainv_l (din^2) then Ginv_l (dout^2).
+ * inv layout: 12 blocks, m = 2l (Ainv_l, n = din_l) and 2l+1 (Ginv_l,
+ * n = dout_l); block m is n rows of stride ld_m = n rounded up to 4 at
+ * offsets[m] (acmi_kfac_inverse_layout), padding columns zero, so the
+ * preconditioning GEMMs read aligned float4 runs.
  * ws: >= acmi_kfac_inverse_ws_doubles(...) doubles.
  * ---------------------------------------------------------------------- */
+int acmi_kfac_inverse_layout(int num_actions, int conv3_filters, int64_t* offsets,
+                             int64_t* lds);
 int64_t acmi_kfac_inverse_floats(int num_actions, int conv3_filters);
 int64_t acmi_kfac_inverse_ws_doubles(int num_actions, int conv3_filters);
 int acmi_kfac_inverse(int num_actions, int conv3_filters,

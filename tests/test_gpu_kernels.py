@@ -191,7 +191,16 @@ def test_kfac_inverse_matches_numpy(lib, cuda):
               _lib.stream_handle())
     torch.cuda.synchronize()
     inv_h = inv.cpu().numpy().astype(np.float64)
-    o = 0
+    ioff = (ctypes.c_int64 * 12)()
+    ild = (ctypes.c_int64 * 12)()
+    _lib.call('acmi_kfac_inverse_layout', A, C3, ioff, ild)
+
+    def block(m, n):
+        o, ld = ioff[m], ild[m]
+        b = inv_h[o:o + n * ld].reshape(n, ld)
+        assert ld % 4 == 0 and ld >= n and not b[:, n:].any(), 'padding columns must be zero'
+        return b[:, :n]
+
     for l in range(6):
         af = min(l, 4)
         Am, Gm = mats[af], mats[5 + l]
@@ -199,10 +208,8 @@ def test_kfac_inverse_matches_numpy(lib, cuda):
         pi = np.sqrt((np.trace(Am) / da) / (np.trace(Gm) / dg))
         ref_a = np.linalg.inv(Am + pi * np.sqrt(damping) * np.eye(da))
         ref_g = np.linalg.inv(Gm + np.sqrt(damping) / pi * np.eye(dg))
-        got_a = inv_h[o:o + da * da].reshape(da, da)
-        o += da * da
-        got_g = inv_h[o:o + dg * dg].reshape(dg, dg)
-        o += dg * dg
+        got_a = block(2 * l, da)
+        got_g = block(2 * l + 1, dg)
         for got, ref in ((got_a, ref_a), (got_g, ref_g)):
             rel = np.abs(got - ref).max() / np.abs(ref).max()
             assert rel < 1e-5, (l, rel)
