@@ -183,15 +183,32 @@ __global__ void conv1_afactor_finalize(const int* part, const int* colsum, int n
   if (hi == 256 && lo == 256) {
     v = 1.0;
   } else {
+    // int32 partials are exact; summed in int64 (the order is immaterial)
     long long sx_lo = 0;
-    for (int c = 0; c < nchunk; ++c) sx_lo += colsum[(long long)c * 256 + lo];
+    for (int c0 = 0; c0 < nchunk; c0 += 8) {
+      int v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = colsum[(long long)(c0 + u < nchunk ? c0 + u : 0) * 256 + lo];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sx_lo += (c0 + u < nchunk) ? v[u] : 0;
+    }
     if (hi == 256) {
       v = (double)(sx_lo + 128 * R) / (255.0 * (double)R);
     } else {
       long long sx_hi = 0, cx = 0;
-      for (int c = 0; c < nchunk; ++c) {
-        sx_hi += colsum[(long long)c * 256 + hi];
-        cx += part[(long long)c * 65536 + lo * 256 + hi];
+      for (int c0 = 0; c0 < nchunk; c0 += 8) {
+        int vh[8], vc[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const long long c = c0 + u < nchunk ? c0 + u : 0;
+          vh[u] = colsum[c * 256 + hi];
+          vc[u] = part[c * 65536 + lo * 256 + hi];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          sx_hi += (c0 + u < nchunk) ? vh[u] : 0;
+          cx += (c0 + u < nchunk) ? vc[u] : 0;
+        }
       }
       const long long uu = cx + 128 * (sx_lo + sx_hi) + 16384 * R;
       v = (double)uu / (65025.0 * (double)R);

@@ -36,6 +36,25 @@ void set_error(const char* fmt, ...);
   } while (0)
 
 // ---------------------------------------------------------------------------
+// fixed-order sum of p[c * stride], c = 0..n-1, with 8 loads in flight: the
+// loads of a group are issued before its (sequential, in-order) adds; a
+// missing tail element reads p[0] and is multiplied by 0 (no branch, no
+// select on a loaded value)
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T chunk_sum(const T* p, int n, long long stride) {
+  T s = 0;
+  for (int c0 = 0; c0 < n; c0 += 8) {
+    T v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(c0 + u < n ? (long long)(c0 + u) : 0LL) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += (c0 + u < n) ? v[u] : T(0);
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------------------
 // counter-based hashing (bit-identical restatement in oracle/oracle.py:mix32)
 // lowbias32 finaliser (C. Wellons); all arithmetic mod 2^32.
 // ---------------------------------------------------------------------------

@@ -96,14 +96,25 @@ bool get_layout(int A, int C3, Layout* L) { return make_layout(A, C3, L); }
 // over [B][512] (memory-bound); the k-ordered fmaf chain is the f32 MFMA's.
 __global__ void heads_dx_kernel(const float* dhead, int ldh, int B, const float* wpi,
                                 const float* wv, int A, const float* a4, float* d4) {
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long long)B * 512) return;
-  const int m = (int)(idx >> 9), j = (int)(idx & 511);
+  // 4 consecutive outputs per thread (float4 a4 / d4)
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long long)B * 128) return;
+  const int m = (int)(q >> 7), j0 = (int)(q & 127) * 4;
   const float* g = dhead + (long long)m * ldh;
-  float acc = 0.f;
-  for (int a = 0; a < A; ++a) acc = __builtin_fmaf(g[a], wpi[j * A + a], acc);
-  acc = __builtin_fmaf(g[A], wv[j], acc);
-  d4[idx] = a4[idx] > 0.f ? acc : 0.f;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int a = 0; a < A; ++a) {
+    const float ga = g[a];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(ga, wpi[(j0 + e) * A + a], acc[e]);
+  }
+  const float gv = g[A];  // (wv is not 16-byte aligned for every A: scalar loads)
+  const float4 x = *reinterpret_cast<const float4*>(a4 + q * 4);
+  float4 o;
+  o.x = x.x > 0.f ? __builtin_fmaf(gv, wv[j0 + 0], acc[0]) : 0.f;
+  o.y = x.y > 0.f ? __builtin_fmaf(gv, wv[j0 + 1], acc[1]) : 0.f;
+  o.z = x.z > 0.f ? __builtin_fmaf(gv, wv[j0 + 2], acc[2]) : 0.f;
+  o.w = x.w > 0.f ? __builtin_fmaf(gv, wv[j0 + 3], acc[3]) : 0.f;
+  *reinterpret_cast<float4*>(d4 + q * 4) = o;
 }
 
 // conv/fc epilogue with an image remap so the rollout can write step t of an
@@ -304,8 +315,7 @@ __global__ void finalize_wgrad_kernel(WgradDesc d) {
     const int n = (int)(idx - (long long)a * d.cout);
     const int row = a < K ? a : d.I;
     const float* p = d.part + (long long)row * d.J + d.kp + n;
-    float s = 0.f;
-    for (int c = 0; c < d.nchunk; ++c) s += p[c * cs];
+    const float s = chunk_sum(p, d.nchunk, cs);
     if (n < d.nsplit) d.gradA[(long long)a * d.nsplit + n] = s;
     else d.gradB[(long long)a * (d.cout - d.nsplit) + (n - d.nsplit)] = s;
   } else {
@@ -320,8 +330,7 @@ __global__ void finalize_wgrad_kernel(WgradDesc d) {
     } else {
       const int col = hi < K ? hi : d.J - 1;
       const float* p = d.part + (long long)lo * d.J + col;
-      s = 0.f;
-      for (int c = 0; c < d.nchunk; ++c) s += p[c * cs];
+      s = chunk_sum(p, d.nchunk, cs);
     }
     d.astat[e] = s * (1.0f / (float)d.rows);
   }
@@ -363,16 +372,18 @@ __global__ void finalize_cov_elem_kernel(const float* part, int nchunk, int n,
 // G = D^T D for narrow D (n <= NP, NP in {32, 64}) straight from global memory:
 // each wave streams row pairs (lane l: row 2q + (l>>5), column l&31 [+32]) as
 // the A and B fragments of v_mfma_f32_32x32x2_f32 (the Gram tile is D^T D of
-// the same registers), UNR k-steps of loads in flight; the block's 4 waves are
-// summed in LDS in a fixed order into part[chunk][NP+1][NP] (finalize_cov_*).
+// the same registers).  Two register sets of UNR k-steps: the next group's
+// loads are issued before this group's MFMAs.  The block's 4 waves are summed
+// into one LDS image in wave order (deterministic) and stored as
+// part[chunk][NP+1][NP] (finalize_cov_*).
 template <int NP>
 __global__ __launch_bounds__(256) void gram_small_kernel(const float* D, int ld, int n,
                                                         long long rows, long long chunk,
                                                         float* part) {
-  constexpr int T = NP / 32;         // column tiles
+  constexpr int T = NP / 32;           // column tiles
   constexpr int NT = T * (T + 1) / 2;  // upper-triangle tile pairs
   constexpr int UNR = 8;
-  __shared__ float red[4][NP * NP];
+  __shared__ float red[NP * NP];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5, c = lane & 31;
   const long long r0 = (long long)blockIdx.x * chunk;
@@ -383,8 +394,7 @@ __global__ __launch_bounds__(256) void gram_small_kernel(const float* D, int ld,
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   const float* zero = zero_run();
-  for (long long base = r0 + 2 * wave; base < r1; base += 8 * UNR) {
-    float v[UNR][T];
+  auto load = [&](long long base, float (&v)[UNR][T]) {
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const long long row = base + 8 * u + h;
@@ -395,6 +405,8 @@ __global__ __launch_bounds__(256) void gram_small_kernel(const float* D, int ld,
         v[u][t] = *(ok ? D + row * ld + col : zero);
       }
     }
+  };
+  auto mma = [&](const float (&v)[UNR][T]) {
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       int t = 0;
@@ -404,27 +416,41 @@ __global__ __launch_bounds__(256) void gram_small_kernel(const float* D, int ld,
         for (int y = x; y < T; ++y, ++t)
           acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u][x], v[u][y], acc[t], 0, 0, 0);
     }
+  };
+  float va[UNR][T], vb[UNR][T];
+  long long base = r0 + 2 * wave;
+  load(base, va);
+  for (; base < r1; base += 16 * UNR) {
+    load(base + 8 * UNR, vb);
+    mma(va);
+    if (base + 8 * UNR >= r1) break;
+    load(base + 16 * UNR, va);
+    mma(vb);
   }
   // acc[t][r]: tile (x, y), row 32x + (r&3) + 8(r>>2) + 4h, column 32y + c
-  {
-    int t = 0;
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+      int t = 0;
 #pragma unroll
-    for (int x = 0; x < T; ++x)
+      for (int x = 0; x < T; ++x)
 #pragma unroll
-      for (int y = x; y < T; ++y, ++t)
+        for (int y = x; y < T; ++y, ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int i = 32 * x + (r & 3) + 8 * (r >> 2) + 4 * h, j = 32 * y + c;
-          red[wave][i * NP + j] = acc[t][r];
-          if (x != y) red[wave][j * NP + i] = acc[t][r];
-        }
+          for (int r = 0; r < 16; ++r) {
+            const int i = 32 * x + (r & 3) + 8 * (r >> 2) + 4 * h, j = 32 * y + c;
+            const float prev_ij = w ? red[i * NP + j] : 0.f;
+            red[i * NP + j] = prev_ij + acc[t][r];
+            if (x != y) {
+              const float prev_ji = w ? red[j * NP + i] : 0.f;
+              red[j * NP + i] = prev_ji + acc[t][r];
+            }
+          }
+    }
+    __syncthreads();
   }
-  __syncthreads();
   float* out = part + (long long)blockIdx.x * (NP + 1) * NP;
-  for (int e = threadIdx.x; e < NP * NP; e += 256)
-    out[e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+  for (int e = threadIdx.x; e < NP * NP; e += 256) out[e] = red[e];
 }
-
 
 // split-K reductions fill whole rounds of resident blocks (plan_rounds):
 // MI355X has 256 CUs; blocks per CU follow from each config's LDS image
@@ -567,7 +593,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
                     const acmi_bwd_t* bw, const float* dhead, int ldh,
                     hipStream_t s) {
   // heads -> d4 = (dhead W_h^T) * relu'(a4)
-  hipLaunchKernelGGL(heads_dx_kernel, dim3(cdiv((long long)B * 512, 256)), dim3(256), 0, s, dhead,
+  hipLaunchKernelGGL(heads_dx_kernel, dim3(cdiv((long long)B * 128, 256)), dim3(256), 0, s, dhead,
                      ldh, B, P + L.off[8], P + L.off[10], L.A, a->a4, bw->d4);
   {  // fc4 -> d3 = (d4 W4^T) * relu'(a3)
     const int K3 = 49 * C3;

@@ -76,22 +76,22 @@ __global__ void categorical_kernel(const float* logits, int ld, int B, int A, co
 __global__ void returns_kernel(const float* r, const uint8_t* d, const float* v,
                                const float* vb, int N, int T, const float* gp,
                                const float* bp, float* tgt, float* adv) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+  // one thread per (env, step): the first terminal at or after t ends the sum
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)N * T) return;
+  const int n = (int)(idx / T), t = (int)(idx - (long long)n * T);
   const float* rn = r + (long long)n * T;
   const uint8_t* dn = d + (long long)n * T;
-  // first terminal at or after t, scanning from the back
   int next_term = T;  // index of the first terminal >= t (T = none)
-  for (int t = T - 1; t >= 0; --t) {
-    if (dn[t]) next_term = t;
-    const int stop = next_term < T ? next_term : T - 1;
-    float acc = 0.f;
-    for (int i = t; i <= stop; ++i) acc = __fadd_rn(acc, __fmul_rn(rn[i], gp[i - t]));
-    const float boot = next_term < T ? 0.f : __fmul_rn(bp[T - t], vb[n]);
-    const float target = __fadd_rn(acc, boot);
-    tgt[(long long)n * T + t] = target;
-    adv[(long long)n * T + t] = __fsub_rn(target, v[(long long)n * T + t]);
-  }
+  for (int i = T - 1; i >= t; --i)
+    if (dn[i]) next_term = i;
+  const int stop = next_term < T ? next_term : T - 1;
+  float acc = 0.f;
+  for (int i = t; i <= stop; ++i) acc = __fadd_rn(acc, __fmul_rn(rn[i], gp[i - t]));
+  const float boot = next_term < T ? 0.f : __fmul_rn(bp[T - t], vb[n]);
+  const float target = __fadd_rn(acc, boot);
+  tgt[idx] = target;
+  adv[idx] = __fsub_rn(target, v[idx]);
 }
 
 // ---------------------------------------------------------------------------
@@ -394,7 +394,7 @@ int acmi_returns(const float* rewards, const uint8_t* terminals, const float* va
                    adv && N >= 0 && T >= 1,
                ACMI_ERR_ARG, "acmi_returns: bad arguments");
   if (N == 0) return ACMI_OK;
-  hipLaunchKernelGGL(returns_kernel, dim3(cdiv(N, 64)), dim3(64), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(returns_kernel, dim3(cdiv((long long)N * T, 256)), dim3(256), 0, (hipStream_t)stream,
                      rewards, terminals, values, v_boot, N, T, gamma_pow, boot_pow, targets,
                      adv);
   ACMI_LAUNCH_CHECK("acmi_returns");
