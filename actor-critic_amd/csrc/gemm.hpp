@@ -28,14 +28,10 @@
 #pragma once
 
 #include <algorithm>
+#include <type_traits>
 
 #include "gemm_ops.hpp"
 
-// K-loop schedule: 0 = fetch the next tile before the MFMA block; 1 = spread
-// the fetch over the k-steps; 2 = as 1 with the order pinned per k-step
-#ifndef ACMI_GEMM_SCHED
-#define ACMI_GEMM_SCHED 0
-#endif
 
 namespace acmi {
 
@@ -59,15 +55,51 @@ struct Tile {
 // 1-D and XCD-aware (cdna_hip_programming.md §5.5 T1): hardware block b runs
 // on XCD b % 8, and each XCD gets a contiguous run of logical blocks, i.e. all
 // tiles of a few chunks, so the tiles that read the same rows share one L2.
-// Otherwise the grid is (tiles_i, tiles_j, zdim) and operands/epilogues may
-// use blockIdx.z for their own purposes (stride phases).
+// Otherwise the grid is (tiles_i, tiles_j, zdim) and the z coordinate (a
+// stride phase) is handed to operands/epilogues that have a member z.
 // COLSUM: blocks with blockIdx.x == 0 also return sum_k B(k, j) through
 // epi.colsum(j, v) (the homogeneous row of [P;1]^T [..]).
 // sym_cols > 0: the product's top-left sym_cols x sym_cols block is symmetric
 // and only its upper triangle is consumed, so blocks lying strictly below the
 // diagonal (every column < every row) inside it exit at once.
+// Epilogue of a wave's (32*WTM) x (32*WTN) sub-tile at (ib, jb):
+// acc[tm][tn][r] -> (ib + 32tm + (r&3) + 8(r>>2) + 4(lane>>5), jb + 32tn + (lane&31))
+// (gfx950 32x32 C/D map).  All aux loads first (clamped indices), then the
+// bounded stores.
+template <int WTM, int WTN, class Epi, class Acc>
+__device__ __forceinline__ void store_tile(const Epi& epi, const Acc& acc, int ib, int jb, int lane,
+                                           int I, int J) {
+  const int khalf = lane >> 5;
+  float x[WTM][WTN][16];
+#pragma unroll
+  for (int tm = 0; tm < WTM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < WTN; ++tn) {
+      const int j = min(jb + tn * 32 + (lane & 31), J - 1);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = min(ib + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf, I - 1);
+        x[tm][tn][r] = epi.aux(i, j);
+      }
+    }
+#pragma unroll
+  for (int tm = 0; tm < WTM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < WTN; ++tn) {
+      const int j = jb + tn * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int i = ib + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+        if (i < I && j < J) epi.store(i, j, acc[tm][tn][r], x[tm][tn][r]);
+      }
+    }
+}
+
+// DEPTH: K-tiles of staging loads in flight (register sets): 1 = the next
+// tile's loads overlap the current tile's MFMAs; 2 = two tiles ahead, for
+// latency-bound shapes (short per-tile MFMA work, L2-missing gathers).
 template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM,
-          class OpA, class OpB, class Epi>
+          class OpA, class OpB, class Epi, int DEPTH = 1>
 __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
                                                    int I, int J, int K,
                                                    int k_chunk, int sym_cols) {
@@ -101,10 +133,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
       }
     }
     by = min(bx * BM / BN, ssym) + t;
-    epi.z = bz;
   } else if (sym_cols > 0 && (by + 1) * BN <= bx * BM && (by + 1) * BN <= sym_cols) {
     return;
   }
+  set_z(opA, bz);
+  set_z(opB, bz);
+  set_z(epi, bz);
   constexpr int SA = OpA::KCONTIG ? BM + 1 : BM + 4;
   constexpr int SB = OpB::KCONTIG ? BN + 1 : BN + 4;
   constexpr int NA = BM * BK / 4 / 256;
@@ -127,8 +161,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
   }
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-  typename OpA::St ra[NA];
-  typename OpB::St rb[NB];
+  static_assert(DEPTH == 1 || DEPTH == 2, "prefetch depth 1 or 2");
+  typename OpA::St ra[DEPTH][NA];
+  typename OpB::St rb[DEPTH][NB];
 
   // per-thread element coordinates: KCONTIG operands keep their row (i) fixed
   // across K-tiles, the others their columns (i) -> hoist that address part.
@@ -165,38 +200,48 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
   // loads are unconditional (operands clamp out-of-range addresses); the K
   // bound and the operand masks are applied at commit (finish).  One element
   // (float4 run) at a time, so the K loop can spread them over its k-steps.
-  auto fetch_a = [&](int k0, int v) {
+  // register set S is a compile-time index (std::integral_constant): a runtime
+  // index into ra/rb would put the staging registers in scratch
+  auto fetch = [&](int k0, auto S) {
+    constexpr int set = decltype(S)::value;
     if constexpr (OpA::KCONTIG) {
       const int k = k0 + (tid % AK) * 4;  // same k for every v (256 % AK == 0)
-      ra[v] = opA.stage(rowA[v], opA.col(k), k < kend);
+      const auto c = opA.col(k);
+#pragma unroll
+      for (int v = 0; v < NA; ++v) ra[set][v] = opA.stage(rowA[v], c, k < kend);
     } else {
-      const int k = k0 + tid / TPRA + RSA * (v / RPRA);
-      ra[v] = opA.stage(opA.row(k), colA[v % RPRA], k < kend);
+#pragma unroll
+      for (int rr = 0; rr < NROWA; ++rr) {
+        const int k = k0 + tid / TPRA + RSA * rr;
+        const auto r = opA.row(k);
+#pragma unroll
+        for (int u = 0; u < RPRA; ++u) ra[set][rr * RPRA + u] = opA.stage(r, colA[u], k < kend);
+      }
     }
-  };
-  auto fetch_b = [&](int k0, int v) {
     if constexpr (OpB::KCONTIG) {
       const int k = k0 + (tid % BKs) * 4;
-      rb[v] = opB.stage(rowB[v], opB.col(k), k < kend);
+      const auto c = opB.col(k);
+#pragma unroll
+      for (int v = 0; v < NB; ++v) rb[set][v] = opB.stage(rowB[v], c, k < kend);
     } else {
-      const int k = k0 + tid / TPRB + RSB * (v / RPRB);
-      rb[v] = opB.stage(opB.row(k), colB[v % RPRB], k < kend);
+#pragma unroll
+      for (int rr = 0; rr < NROWB; ++rr) {
+        const int k = k0 + tid / TPRB + RSB * rr;
+        const auto r = opB.row(k);
+#pragma unroll
+        for (int u = 0; u < RPRB; ++u) rb[set][rr * RPRB + u] = opB.stage(r, colB[u], k < kend);
+      }
     }
   };
-  auto fetch = [&](int k0) {
-#pragma unroll
-    for (int v = 0; v < NA; ++v) fetch_a(k0, v);
-#pragma unroll
-    for (int v = 0; v < NB; ++v) fetch_b(k0, v);
-  };
 
-  auto commit = [&](int buf) {
+  auto commit = [&](int buf, auto S) {
+    constexpr int set = decltype(S)::value;
     float* As = lds + buf * ABUF;
     float* Bs = lds + 2 * ABUF + buf * BBUF;
 #pragma unroll
     for (int v = 0; v < NA; ++v) {
       const int idx = tid + 256 * v;
-      const float4 x = finish(ra[v]);
+      const float4 x = finish(ra[set][v]);
       if constexpr (OpA::KCONTIG) {
         const int i = idx / (BK / 4);
         const int k = (idx - i * (BK / 4)) * 4;
@@ -213,7 +258,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
 #pragma unroll
     for (int v = 0; v < NB; ++v) {
       const int idx = tid + 256 * v;
-      const float4 x = finish(rb[v]);
+      const float4 x = finish(rb[set][v]);
       if constexpr (OpB::KCONTIG) {
         const int j = idx / (BK / 4);
         const int k = (idx - j * (BK / 4)) * 4;
@@ -243,9 +288,12 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
 #pragma unroll
   for (int tn = 0; tn < WTN; ++tn) csum[tn] = 0.f;
 
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, DEPTH == 2 ? 1 : 0>;
   if (nk > 0) {
-    fetch(kbeg);
-    commit(0);
+    fetch(kbeg, S0{});
+    commit(0, S0{});
+    if constexpr (DEPTH == 2) fetch(kbeg + BK, S1{});
   }
   __syncthreads();
 
@@ -253,20 +301,16 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
   const int brow = wn * WTN * 32 + (lane & 31);
   const int khalf = lane >> 5;
 
-  // The loop body is one basic block: the next tile's fetch is unconditional
-  // (past kend it reads clamped addresses and is zeroed), so its loads stay in
-  // flight across the MFMAs and are only waited for at the LDS commit.
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const int knext = kbeg + (kt + 1) * BK;
+  // One K-tile: issue the staging loads DEPTH tiles ahead (unconditional:
+  // past kend they read clamped addresses and are zeroed), run the MFMAs on
+  // LDS buffer `cur`, then write the tile kt+1 held in register set SC to the
+  // other buffer.  The body is one basic block and sched_barriers keep the
+  // commit (which waits for its loads) behind the MFMA block.
+  auto step = [&](int kt, int cur, auto SC, auto SF) {
+    fetch(kbeg + (kt + DEPTH) * BK, SF);
+    __builtin_amdgcn_sched_barrier(0);
     const float* As = lds + cur * ABUF;
     const float* Bs = lds + 2 * ABUF + cur * BBUF;
-#if ACMI_GEMM_SCHED == 0
-    fetch(knext);
-    // keep the scheduler from hoisting the commit's finish() (which waits for
-    // the loads) into the MFMA block
-    __builtin_amdgcn_sched_barrier(0);
-#endif
     float a[WTM], b[WTN];
 #pragma unroll
     for (int tm = 0; tm < WTM; ++tm) a[tm] = As[khalf * SA + arow + tm * 32];
@@ -282,18 +326,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
 #pragma unroll
         for (int tn = 0; tn < WTN; ++tn) bn[tn] = Bs[(kk + 2 + khalf) * SB + brow + tn * 32];
       }
-#if ACMI_GEMM_SCHED != 0
-      // the next tile's staging loads, one element per operand per k-step,
-      // between the MFMAs (a wave's address arithmetic then overlaps its own
-      // matrix work instead of preceding it)
-      {
-        constexpr int NSTEP = BK / 2;
-        const int st = kk / 2;
-        (void)NSTEP;
-        if (st < NA) fetch_a(knext, st);
-        if (st < NB) fetch_b(knext, st);
-      }
-#endif
       if constexpr (COLSUM) {
 #pragma unroll
         for (int tn = 0; tn < WTN; ++tn) csum[tn] += b[tn];
@@ -303,9 +335,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
 #pragma unroll
         for (int tn = 0; tn < WTN; ++tn)
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[tm], b[tn], acc[tm][tn], 0, 0, 0);
-#if ACMI_GEMM_SCHED == 2
-      __builtin_amdgcn_sched_barrier(0);
-#endif
       if (kk + 2 < BK) {
 #pragma unroll
         for (int tm = 0; tm < WTM; ++tm) a[tm] = an[tm];
@@ -314,23 +343,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    commit(cur ^ 1);
+    commit(cur ^ 1, SC);
     __syncthreads();
+  };
+  // two K-tiles per iteration so the register sets are compile-time indices:
+  // with DEPTH 2, tile t lives in set t & 1
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, 0, S1{}, S0{});
+    if (kt + 1 < nk) step(kt + 1, 1, S0{}, S1{});
   }
 
   // epilogue: acc[tm][tn][r] -> C[i][j],  j = lane&31 (+tile),
   // i = (r&3) + 8*(r>>2) + 4*(lane>>5) (+tile)   (gfx950 32x32 C/D map)
-#pragma unroll
-  for (int tm = 0; tm < WTM; ++tm)
-#pragma unroll
-    for (int tn = 0; tn < WTN; ++tn) {
-      const int j = j0 + wn * WTN * 32 + tn * 32 + (lane & 31);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = i0 + wm * WTM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
-        if (i < I && j < J) epi(i, j, acc[tm][tn][r]);
-      }
-    }
+  store_tile<WTM, WTN>(epi, acc, i0 + wm * WTM * 32, j0 + wn * WTN * 32, lane, I, J);
   if constexpr (COLSUM) {
     if (bx == 0 && wm == 0) {
 #pragma unroll
@@ -344,12 +369,17 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
 }
 
 // ---------------------------------------------------------------------------
-// Epilogues
+// Epilogues.  Two phases per element so no load sits under the tile-edge
+// branch (the .s trap (c) again: a load under `if (i < I && j < J)` waits
+// vmcnt(0) per element): aux(i, j) loads what the store needs from a clamped,
+// always valid (i, j) for every element first; store(i, j, v, aux) then runs
+// under the bounds check.
 // ---------------------------------------------------------------------------
 struct EpiStore {
   float* out;
   long long ld;
-  __device__ __forceinline__ void operator()(int i, int j, float v) const {
+  __device__ __forceinline__ float aux(int, int) const { return 0.f; }
+  __device__ __forceinline__ void store(int i, int j, float v, float) const {
     out[(long long)i * ld + j] = v;
   }
 };
@@ -360,24 +390,11 @@ struct EpiBiasAct {
   long long ld;
   const float* bias;
   int relu;
-  __device__ __forceinline__ void operator()(int i, int j, float v) const {
-    v += bias[j];
+  __device__ __forceinline__ float aux(int, int j) const { return bias[j]; }
+  __device__ __forceinline__ void store(int i, int j, float v, float b) const {
+    v += b;
     if (relu) v = fmaxf(v, 0.f);
     out[(long long)i * ld + j] = v;
-  }
-};
-
-// fc heads: j < A -> logits[i][j] = v + bpi[j]; j == A -> value[i] = v + bv
-struct EpiHeads {
-  float* logits;
-  int ld;
-  float* value;
-  const float* bpi;
-  const float* bv;
-  int A;
-  __device__ __forceinline__ void operator()(int i, int j, float v) const {
-    if (j < A) logits[(long long)i * ld + j] = v + bpi[j];
-    else if (value) value[i] = v + bv[0];
   }
 };
 
@@ -386,29 +403,32 @@ struct EpiReluGrad {
   float* out;
   const float* act;
   long long ld;
-  __device__ __forceinline__ void operator()(int i, int j, float v) const {
-    const long long o = (long long)i * ld + j;
-    out[o] = act[o] > 0.f ? v : 0.f;
+  __device__ __forceinline__ float aux(int i, int j) const { return act[(long long)i * ld + j]; }
+  __device__ __forceinline__ void store(int i, int j, float v, float x) const {
+    out[(long long)i * ld + j] = x > 0.f ? v : 0.f;
   }
 };
 
-// input-gradient of a strided conv, one phase per blockIdx.z: row i =
+// input-gradient of a strided conv, one phase per grid z (member z): row i =
 // (img, ih', iw') -> NHWC pixel (S*ih'+ph, S*iw'+pw); masked by ReLU'.
 template <int IH, int IW, int S, int CIN>
 struct EpiConvTPhase {
   float* out;
   const float* act;
-  __device__ __forceinline__ void operator()(int i, int j, float v) const {
+  int z = 0;  // stride phase, set by the kernel
+  __device__ __forceinline__ long long offset(int i, int j) const {
     constexpr int PH = IH / S, PW = IW / S, L = PH * PW;
-    const int ph = blockIdx.z / S;
-    const int pw = blockIdx.z - ph * S;
-    const int img = i / L;
-    const int p = i - img * L;
-    const int ihp = p / PW;
-    const int iwp = p - ihp * PW;
-    const long long o =
-        (((long long)img * IH + (S * ihp + ph)) * IW + (S * iwp + pw)) * CIN + j;
-    out[o] = act[o] > 0.f ? v : 0.f;
+    const int ph = z / S;
+    const int pw = z - ph * S;
+    const uint32_t img = (uint32_t)i / L;
+    const uint32_t p = (uint32_t)i - img * L;
+    const uint32_t ihp = p / PW;
+    const uint32_t iwp = p - ihp * PW;
+    return (((long long)img * IH + (S * ihp + ph)) * IW + (S * iwp + pw)) * CIN + j;
+  }
+  __device__ __forceinline__ float aux(int i, int j) const { return act[offset(i, j)]; }
+  __device__ __forceinline__ void store(int i, int j, float v, float x) const {
+    out[offset(i, j)] = x > 0.f ? v : 0.f;
   }
 };
 
@@ -418,7 +438,8 @@ struct EpiPartial {
   int I;
   int J;
   int z = 0;  // chunk, set by gemm_kernel
-  __device__ __forceinline__ void operator()(int i, int j, float v) const {
+  __device__ __forceinline__ float aux(int, int) const { return 0.f; }
+  __device__ __forceinline__ void store(int i, int j, float v, float) const {
     part[((long long)z * (I + 1) + i) * J + j] = v;
   }
   __device__ __forceinline__ void colsum(int j, float v) const {
@@ -476,13 +497,13 @@ inline int live_tiles(int I, int J, int sym_cols) {
   return live;
 }
 
-template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM,
+template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM, int DEPTH = 1,
           class OpA, class OpB, class Epi>
 inline void launch_gemm(const OpA& a, const OpB& b, const Epi& e, int I, int J,
                         int K, int zdim, int k_chunk, hipStream_t s, int sym_cols = 0) {
   dim3 grid(cdiv(I, BM), cdiv(J, BN), zdim);
   if (SPLITK) grid = dim3(live_tiles<BM, BN>(I, J, sym_cols) * zdim);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WTM, WTN, SPLITK, COLSUM, OpA, OpB, Epi>),
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WTM, WTN, SPLITK, COLSUM, OpA, OpB, Epi, DEPTH>),
                      grid, dim3(256), 0, s, a, b, e, I, J, K, k_chunk, sym_cols);
 }
 

@@ -43,6 +43,18 @@ struct OffOk {
   bool ok;
 };
 
+// Operands and epilogues that depend on the block's third grid coordinate (a
+// stride phase, a split-K chunk) hold it in a member `z`, which the GEMM kernels
+// set per tile (set_z); they never read blockIdx.z themselves.
+template <class T, class = void>
+struct has_z : std::false_type {};
+template <class T>
+struct has_z<T, std::void_t<decltype(std::declval<T&>().z)>> : std::true_type {};
+template <class T>
+__device__ __forceinline__ void set_z(T& t, int z) {
+  if constexpr (has_z<T>::value) t.z = z;
+}
+
 // Loads are never guarded by branches and their results never pass through
 // a mask: an element outside the operand loads from a 16-byte zero run (or the
 // homogeneous run (1,0,0,0)) instead, selected on the ADDRESS.  A load under a
@@ -334,7 +346,7 @@ struct MatTK {
 using MatTKu = MatTK<false>;
 
 // Conv weight as the B operand of the input gradient, one stride phase per
-// blockIdx.z:  B(k = (kh',kw',co), j = ci) = W[ph+S*kh'][pw+S*kw'][ci][co].
+// block (member z):  B(k = (kh',kw',co), j = ci) = W[ph+S*kh'][pw+S*kw'][ci][co].
 template <int KH, int KW, int S, int CIN, int COUT>
 struct ConvTWeights {
   static constexpr bool KCONTIG = true;
@@ -344,11 +356,12 @@ struct ConvTWeights {
   using R = OffOk;
   using C = OffOk;
   const float* w;  // HWIO
+  int z = 0;       // stride phase (ph, pw) = (z / S, z % S), set by the kernel
   __device__ __forceinline__ R row(int j) const { return R{(uint32_t)j * COUT, j < CIN}; }
   __device__ __forceinline__ C col(int k) const {
     if (k >= K) return C{0, false};
-    const int ph = blockIdx.z / S;
-    const int pw = blockIdx.z - ph * S;
+    const int ph = z / S;
+    const int pw = z - ph * S;
     const int khp = k / (KWP * COUT);
     const int rem = k - khp * (KWP * COUT);
     const int kwp = rem / COUT;

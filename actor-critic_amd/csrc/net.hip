@@ -125,11 +125,11 @@ struct EpiAct {
   int cols;         // output channels (row length)
   int L;            // output rows per image
   long long img_stride;  // floats between consecutive images in `out`
-  __device__ __forceinline__ void operator()(int i, int j, float v) const {
-    const int img = i / L;
-    const int p = i - img * L;
-    v = fmaxf(v + bias[j], 0.f);
-    out[(long long)img * img_stride + (long long)p * cols + j] = v;
+  __device__ __forceinline__ float aux(int, int j) const { return bias[j]; }
+  __device__ __forceinline__ void store(int i, int j, float v, float b) const {
+    const uint32_t img = (uint32_t)i / (uint32_t)L;
+    const uint32_t p = (uint32_t)i - img * (uint32_t)L;
+    out[(long long)img * img_stride + (long long)p * cols + j] = fmaxf(v + b, 0.f);
   }
 };
 

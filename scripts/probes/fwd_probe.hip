@@ -4,7 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 
-#include "../../actor-critic_amd/csrc/gemm.hpp"
+#include "../../actor-critic_amd/csrc/gemm_stream.hpp"
 
 namespace acmi {
 void set_error(const char*, ...) {}
@@ -85,6 +85,14 @@ int main(int argc, char** argv) {
   printf("M=%d\n", M);
   RUN("conv1 256x32x32", f1, (launch_gemm<256, 32, 32, 2, 1, false, false>(A1, B1, E1, M * 400, 32, 256, 1, 0, 0)));
   RUN("conv1 128x32x32", f1, (launch_gemm<128, 32, 32, 1, 1, false, false>(A1, B1, E1, M * 400, 32, 256, 1, 0, 0)));
+  RUN("conv1 128x32x32 depth2", f1, (launch_gemm<128, 32, 32, 1, 1, false, false, 2>(A1, B1, E1, M * 400, 32, 256, 1, 0, 0)));
+  RUN("conv2 64x64x32 depth2", f2, (launch_gemm<64, 64, 32, 1, 1, false, false, 2>(A2, B2, E2, M * 81, 64, 512, 1, 0, 0)));
+  RUN("conv3 128x32x32 depth2", f3, (launch_gemm<128, 32, 32, 1, 1, false, false, 2>(A3, B3, E3, M * 49, 32, 576, 1, 0, 0)));
+  RUN("conv1 128x32x32 stream", f1, (launch_gemm_stream<128, 32, 32, 1, 1>(A1, B1, E1, M * 400, 32, 256, 1, 0)));
+  RUN("conv1 256x32x32 stream", f1, (launch_gemm_stream<256, 32, 32, 2, 1>(A1, B1, E1, M * 400, 32, 256, 1, 0)));
+  RUN("conv2 64x64x32 stream", f2, (launch_gemm_stream<64, 64, 32, 1, 1>(A2, B2, E2, M * 81, 64, 512, 1, 0)));
+  RUN("conv2 128x64x32 stream", f2, (launch_gemm_stream<128, 64, 32, 2, 1>(A2, B2, E2, M * 81, 64, 512, 1, 0)));
+  RUN("conv3 128x32x32 stream", f3, (launch_gemm_stream<128, 32, 32, 1, 1>(A3, B3, E3, M * 49, 32, 576, 1, 0)));
   RUN("conv2 128x64x32", f2, (launch_gemm<128, 64, 32, 2, 1, false, false>(A2, B2, E2, M * 81, 64, 512, 1, 0, 0)));
   RUN("conv2 64x64x32", f2, (launch_gemm<64, 64, 32, 1, 1, false, false>(A2, B2, E2, M * 81, 64, 512, 1, 0, 0)));
   RUN("conv2 128x32x32", f2, (launch_gemm<128, 32, 32, 1, 1, false, false>(A2, B2, E2, M * 81, 64, 512, 1, 0, 0)));

@@ -7,7 +7,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "../../actor-critic_amd/csrc/gemm.hpp"
+#include "../../actor-critic_amd/csrc/gemm_stream.hpp"
 
 namespace acmi {
 void set_error(const char*, ...) {}
@@ -98,6 +98,15 @@ int main(int argc, char** argv) {
       launch_gemm<128, 128, 16, 2, 2, true, true>(opA, opB, epi, I, J, (int)R, nc, ch, 0, K);
     });
     printf("conv2 implicit  128x128x16: %.3f ms  %.1f TF (computed tiles)\n", ms2, flops / ms2 / 1e9);
+    {
+      int ncq, chq;
+      plan_rounds(R, live, 1024, &ncq, &chq);
+      check_nc(ncq);
+      float msq = timeit([&] {
+        launch_gemm<128, 128, 16, 2, 2, true, true, 2>(opA, opB, epi, I, J, (int)R, ncq, chq, 0, K);
+      });
+      printf("conv2 implicit  128x128x16 depth2 (1024 slots): %.3f ms  %.1f TF\n", msq, flops / msq / 1e9);
+    }
     int nc3, ch3;
     plan_rounds(R, 8, 256, &nc3, &ch3); check_nc(nc3);
     float ms3 = timeit([&] {
@@ -221,6 +230,22 @@ int main(int argc, char** argv) {
       launch_gemm<128, 32, 32, 1, 1, false, false>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0, 0);
     });
     printf("conv2 dX 128x32x32: %.3f ms  %.1f TF\n", m3, fl / m3 / 1e9);
+    float m5 = timeit([&] {
+      launch_gemm<128, 32, 32, 1, 1, false, false, 2>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0, 0);
+    });
+    printf("conv2 dX 128x32x32 depth2: %.3f ms  %.1f TF\n", m5, fl / m5 / 1e9);
+    float m7 = timeit([&] {
+      launch_gemm_stream<128, 32, 32, 1, 1>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0);
+    });
+    printf("conv2 dX 128x32x32 stream: %.3f ms  %.1f TF\n", m7, fl / m7 / 1e9);
+    float m8 = timeit([&] {
+      launch_gemm_stream<256, 32, 32, 2, 1>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0);
+    });
+    printf("conv2 dX 256x32x32 stream: %.3f ms  %.1f TF\n", m8, fl / m8 / 1e9);
+    float m6 = timeit([&] {
+      launch_gemm<256, 32, 32, 2, 1, false, false, 2>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0, 0);
+    });
+    printf("conv2 dX 256x32x32 depth2: %.3f ms  %.1f TF\n", m6, fl / m6 / 1e9);
     float m4 = timeit([&] {
       launch_gemm<128, 32, 64, 1, 1, false, false>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0, 0);
     });
