@@ -306,40 +306,43 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
   // LDS buffer `cur`, then write the tile kt+1 held in register set SC to the
   // other buffer.  The body is one basic block and sched_barriers keep the
   // commit (which waits for its loads) behind the MFMA block.
-  auto step = [&](int kt, int cur, auto SC, auto SF) {
+  auto step = [&](int kt, int cur, auto SC, auto SF, auto MF) {
+    constexpr bool mf = decltype(MF)::value;
     fetch(kbeg + (kt + DEPTH) * BK, SF);
     __builtin_amdgcn_sched_barrier(0);
-    const float* As = lds + cur * ABUF;
-    const float* Bs = lds + 2 * ABUF + cur * BBUF;
-    float a[WTM], b[WTN];
+    if constexpr (mf) {
+      const float* As = lds + cur * ABUF;
+      const float* Bs = lds + 2 * ABUF + cur * BBUF;
+      float a[WTM], b[WTN];
 #pragma unroll
-    for (int tm = 0; tm < WTM; ++tm) a[tm] = As[khalf * SA + arow + tm * 32];
+      for (int tm = 0; tm < WTM; ++tm) a[tm] = As[khalf * SA + arow + tm * 32];
 #pragma unroll
-    for (int tn = 0; tn < WTN; ++tn) b[tn] = Bs[khalf * SB + brow + tn * 32];
+      for (int tn = 0; tn < WTN; ++tn) b[tn] = Bs[khalf * SB + brow + tn * 32];
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      // fragments of the next k-step are read before this step's MFMAs
-      float an[WTM], bn[WTN];
-      if (kk + 2 < BK) {
+      for (int kk = 0; kk < BK; kk += 2) {
+        // fragments of the next k-step are read before this step's MFMAs
+        float an[WTM], bn[WTN];
+        if (kk + 2 < BK) {
 #pragma unroll
-        for (int tm = 0; tm < WTM; ++tm) an[tm] = As[(kk + 2 + khalf) * SA + arow + tm * 32];
+          for (int tm = 0; tm < WTM; ++tm) an[tm] = As[(kk + 2 + khalf) * SA + arow + tm * 32];
 #pragma unroll
-        for (int tn = 0; tn < WTN; ++tn) bn[tn] = Bs[(kk + 2 + khalf) * SB + brow + tn * 32];
-      }
-      if constexpr (COLSUM) {
+          for (int tn = 0; tn < WTN; ++tn) bn[tn] = Bs[(kk + 2 + khalf) * SB + brow + tn * 32];
+        }
+        if constexpr (COLSUM) {
 #pragma unroll
-        for (int tn = 0; tn < WTN; ++tn) csum[tn] += b[tn];
-      }
+          for (int tn = 0; tn < WTN; ++tn) csum[tn] += b[tn];
+        }
 #pragma unroll
-      for (int tm = 0; tm < WTM; ++tm)
+        for (int tm = 0; tm < WTM; ++tm)
 #pragma unroll
-        for (int tn = 0; tn < WTN; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[tm], b[tn], acc[tm][tn], 0, 0, 0);
-      if (kk + 2 < BK) {
+          for (int tn = 0; tn < WTN; ++tn)
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[tm], b[tn], acc[tm][tn], 0, 0, 0);
+        if (kk + 2 < BK) {
 #pragma unroll
-        for (int tm = 0; tm < WTM; ++tm) a[tm] = an[tm];
+          for (int tm = 0; tm < WTM; ++tm) a[tm] = an[tm];
 #pragma unroll
-        for (int tn = 0; tn < WTN; ++tn) b[tn] = bn[tn];
+          for (int tn = 0; tn < WTN; ++tn) b[tn] = bn[tn];
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -348,9 +351,23 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
   };
   // two K-tiles per iteration so the register sets are compile-time indices:
   // with DEPTH 2, tile t lives in set t & 1
-  for (int kt = 0; kt < nk; kt += 2) {
-    step(kt, 0, S1{}, S0{});
-    if (kt + 1 < nk) step(kt + 1, 1, S0{}, S1{});
+  // A wave whose whole sub-tile lies strictly below the diagonal of the
+  // symmetric block (diagonal blocks, sym_cols) computes nothing anyone reads:
+  // it only stages and syncs (its SIMD serves the co-resident blocks' MFMAs).
+  const int wrow0 = i0 + wm * WTM * 32, wcol1 = j0 + (wn + 1) * WTN * 32;
+  const bool wave_idle = sym_cols > 0 && wcol1 <= wrow0 && wcol1 <= sym_cols;
+  using MFon = std::integral_constant<bool, true>;
+  using MFoff = std::integral_constant<bool, false>;
+  if (!wave_idle) {
+    for (int kt = 0; kt < nk; kt += 2) {
+      step(kt, 0, S1{}, S0{}, MFon{});
+      if (kt + 1 < nk) step(kt + 1, 1, S0{}, S1{}, MFon{});
+    }
+  } else {
+    for (int kt = 0; kt < nk; kt += 2) {
+      step(kt, 0, S1{}, S0{}, MFoff{});
+      if (kt + 1 < nk) step(kt + 1, 1, S0{}, S1{}, MFoff{});
+    }
   }
 
   // epilogue: acc[tm][tn][r] -> C[i][j],  j = lane&31 (+tile),
