@@ -71,7 +71,7 @@ __device__ __forceinline__ const float* zero_run() { return kMaskRuns; }
 __device__ __forceinline__ const float* homog_run() { return kMaskRuns + 4; }
 
 using StF4 = float4;
-struct StU8 {  // four u8 pixels, normalised by 1/255 at finish
+struct StU8 {  // four u8 pixels
   uint32_t u;
 };
 __device__ __forceinline__ StF4 stage_f4(const float* p, bool ok) {
@@ -84,10 +84,14 @@ __device__ __forceinline__ StF4 stage_tail(const float* p, bool ok, int n) {
   return make_float4(*(ok ? p : z), *(ok && n > 1 ? p + 1 : z), *(ok && n > 2 ? p + 2 : z),
                      *(ok && n > 3 ? p + 3 : z));
 }
+// u8 pixels enter the MFMAs as their integer values 0..255 (exact in f32,
+// v_cvt_f32_ubyte0..3); the 1/255 of the reference's normalisation is applied
+// once per output by the consumer (EpiAct::scale for conv1, the conv1 weight
+// gradient's wscale in finalize_wgrad_kernel).
 __device__ __forceinline__ float4 finish(const StU8& s) {
   const uint32_t u = s.u;
-  return make_float4(u8norm(u & 255u), u8norm((u >> 8) & 255u), u8norm((u >> 16) & 255u),
-                     u8norm(u >> 24));
+  return make_float4((float)(u & 255u), (float)((u >> 8) & 255u), (float)((u >> 16) & 255u),
+                     (float)(u >> 24));
 }
 
 // ---------------------------------------------------------------------------
@@ -96,7 +100,7 @@ __device__ __forceinline__ float4 finish(const StU8& s) {
 
 // Patches of NHWC images for a VALID conv; row r = (img, oh, ow), column
 // c = (kh, kw, ch) with ch fastest (== HWIO flatten == TF extract_image_patches
-// order).  T = uint8_t normalises by 1/255.
+// order).  T = uint8_t yields raw 0..255 values (see finish(StU8)).
 template <typename T, int H, int W, int C, int KH, int KW, int S>
 struct ConvRows {
   static constexpr int OH = (H - KH) / S + 1;

@@ -125,11 +125,12 @@ struct EpiAct {
   int cols;         // output channels (row length)
   int L;            // output rows per image
   long long img_stride;  // floats between consecutive images in `out`
+  float scale = 1.f;     // conv1: 1/255 (its A operand is the raw u8 pixels)
   __device__ __forceinline__ float aux(int, int j) const { return bias[j]; }
   __device__ __forceinline__ void store(int i, int j, float v, float b) const {
     const uint32_t img = (uint32_t)i / (uint32_t)L;
     const uint32_t p = (uint32_t)i - img * (uint32_t)L;
-    out[(long long)img * img_stride + (long long)p * cols + j] = fmaxf(v + b, 0.f);
+    out[(long long)img * img_stride + (long long)p * cols + j] = fmaxf(__builtin_fmaf(v, scale, b), 0.f);
   }
 };
 
@@ -213,7 +214,7 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     using Src = ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>;
     RowsAsK<Src> opA{Src{obs, (uint32_t)img_stride, B * 400}};
     MatI<true> opB{P + L.off[0], 32, 256, 32};
-    EpiAct epi{a->a1, P + L.off[1], 32, 400, st * 400 * 32};
+    EpiAct epi{a->a1, P + L.off[1], 32, 400, st * 400 * 32, 1.0f / 255.0f};
     prof_begin(ACMI_PROF_CONV1_FWD, s);
     // rollout-size batches fill the chip better with 128-row tiles
     if (B <= 2048)
@@ -301,6 +302,7 @@ struct WgradDesc {
   float* gradB;  // columns [nsplit, cout)
   float* astat;  // nullable
   int rows;
+  float wscale;  // applied to the weight rows (a < K) of the gradient
 };
 
 __global__ void finalize_wgrad_kernel(WgradDesc d) {
@@ -315,7 +317,7 @@ __global__ void finalize_wgrad_kernel(WgradDesc d) {
     const int n = (int)(idx - (long long)a * d.cout);
     const int row = a < K ? a : d.I;
     const float* p = d.part + (long long)row * d.J + d.kp + n;
-    const float s = chunk_sum(p, d.nchunk, cs);
+    const float s = a < K ? chunk_sum(p, d.nchunk, cs) * d.wscale : chunk_sum(p, d.nchunk, cs);
     if (n < d.nsplit) d.gradA[(long long)a * d.nsplit + n] = s;
     else d.gradB[(long long)a * (d.cout - d.nsplit) + (n - d.nsplit)] = s;
   } else {
@@ -505,7 +507,8 @@ template <class Src>
 static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
                        int ldy, int cout, bool with_stats, float* part,
                        long long part_cap, float* gradA, int nsplit,
-                       float* gradB, float* astat, hipStream_t s, int site = 0) {
+                       float* gradB, float* astat, hipStream_t s, int site = 0,
+                       float wscale = 1.f) {
   const WgradPlan pl = wgrad_plan(K, cout, with_stats, rows);
   const int I = pl.I, J = pl.J, kp = pl.kp, nc = pl.nc, ch = pl.ch;
   RowsAsI<Src> opA{src};
@@ -521,7 +524,7 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
   else
     launch_gemm<128, 32, 32, 1, 1, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s);
   prof_end(site, s);
-  WgradDesc d{part, nc, I, J, kp, cout, gradA, nsplit, gradB, astat, (int)rows};
+  WgradDesc d{part, nc, I, J, kp, cout, gradA, nsplit, gradB, astat, (int)rows, wscale};
   const long long total = (long long)(K + 1) * cout + (astat ? (long long)(K + 1) * (K + 1) : 0);
   hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, d);
   ACMI_LAUNCH_CHECK("wgrad_layer");
@@ -654,7 +657,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // the i8 matrix cores (exact integer sums, afactor_u8.hip)
   rc = wgrad_layer(ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>{obs, (uint32_t)img_stride, B * 400}, 256,
                    400LL * B, bw->d1, 32, 32, false, part, ws_cap, grads + L.off[0], 32, nullptr,
-                   nullptr, s, ACMI_PROF_CONV1_WGRAD);
+                   nullptr, s, ACMI_PROF_CONV1_WGRAD, 1.0f / 255.0f);  // raw u8 patches
   if (rc || !st) return rc;
   prof_begin(ACMI_PROF_CONV1_AFACTOR, s);
   rc = conv1_afactor_u8(obs, img_stride, B, astat + L.stat_off[0], reinterpret_cast<int*>(ws),
