@@ -40,7 +40,9 @@ def init_from_env(backend=None):
     if ws > 1 and not is_initialized():
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         if backend is None:
-            backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+            # ACMI_DIST_BACKEND=gloo rehearses N ranks on one GPU (RCCL refuses
+            # two ranks on one device); the default on GPUs is nccl (= RCCL)
+            backend = os.environ.get('ACMI_DIST_BACKEND') or ('nccl' if torch.cuda.is_available() else 'gloo')
         dist.init_process_group(backend=backend, init_method='env://')
     return world_size(), rank()
 
