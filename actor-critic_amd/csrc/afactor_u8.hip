@@ -16,6 +16,8 @@
 // Operand lane map (verified on gfx950, scripts/probes/mfma_i8_probe.hip):
 // lane l holds A[row l&31][k = 16(l>>5) + j] and B[k = 16(l>>5) + j][col l&31],
 // j = 0..15; D uses the standard 32x32 map.
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace acmi {
@@ -26,20 +28,44 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr int AF_BK = 64;          // rows per stage (two 32-deep MFMA steps)
 constexpr int AF_LINE = 80;        // bytes per LDS column line: 64 rows + 16 pad
 constexpr int AF_TILE = 128 * AF_LINE;
-constexpr int AF_CHUNK = 16384;    // rows per block: |partial| < 2^31
+constexpr int AF_CHUNK = 16384;    // max rows per block: |partial| < 2^31
+constexpr int AF_SLOTS = 256 * 4;  // resident blocks (4 per CU by LDS)
+
+// rows < r_end load their patch bytes; the others load this run of 0x80
+// bytes, i.e. x = 0 after the XOR (selected on the address, see gemm_ops.hpp)
+__device__ __attribute__((weak, aligned(16))) uint32_t kX0Run[4] = {0x80808080u, 0x80808080u,
+                                                                    0x80808080u, 0x80808080u};
+
+// chunks: at least ceil(rows / AF_CHUNK), grown so 3 tile pairs x chunks fill
+// whole rounds of AF_SLOTS blocks; chunk length a multiple of AF_BK
+static void af_plan(long long rows, int* nchunk, int* chunk) {
+  const long long nc0 = std::max<long long>(1, (rows + AF_CHUNK - 1) / AF_CHUNK);
+  const long long rounds = (3 * nc0 + AF_SLOTS - 1) / AF_SLOTS;
+  const long long nc = std::max<long long>(nc0, rounds * AF_SLOTS / 3);
+  long long ch = (rows + nc - 1) / nc;
+  ch = (ch + AF_BK - 1) / AF_BK * AF_BK;
+  *chunk = (int)std::max<long long>(ch, AF_BK);
+  *nchunk = (int)((rows + *chunk - 1) / *chunk);
+}
 constexpr int AF_OBS_W = 84;
 
 __global__ __launch_bounds__(256) void conv1_afactor_i8_kernel(const uint8_t* obs,
                                                                long long img_stride,
-                                                               int rows, int* part,
-                                                               int* colsum) {
-  const int pair = blockIdx.x;  // tile pairs (0,0) (0,1) (1,1)
+                                                               int rows, int chunk_rows,
+                                                               int* part, int* colsum) {
+  // 1-D grid, XCD-contiguous (gemm.hpp): logical block l = (chunk, pair), the
+  // 3 tile pairs of a chunk adjacent, so they read the chunk's frames through
+  // one L2
+  const int total = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, base_l = total >> 3, rem = total & 7;
+  const int l = xcd * base_l + min(xcd, rem) + (b >> 3);
+  const int chunk = l / 3;
+  const int pair = l - 3 * chunk;  // tile pairs (0,0) (0,1) (1,1)
   const int ta = pair == 2 ? 1 : 0;
   const int tb = pair == 0 ? 0 : 1;
   const bool diag = ta == tb;
-  const int chunk = blockIdx.y;
-  const int r_begin = chunk * AF_CHUNK;
-  const int r_end = min(rows, r_begin + AF_CHUNK);
+  const int r_begin = chunk * chunk_rows;
+  const int r_end = min(rows, r_begin + chunk_rows);
   __shared__ __attribute__((aligned(16))) uint8_t lds[2][2][AF_TILE];
 
   const int tid = threadIdx.x;
@@ -59,27 +85,23 @@ __global__ __launch_bounds__(256) void conv1_afactor_i8_kernel(const uint8_t* ob
   const int coffA = col_off(ta);
   const int coffB = col_off(tb);
 
+  // raw patch bytes; the XOR (x = u ^ 0x80) is applied at commit, after the
+  // MFMAs, so nothing waits on the loads at fetch time
   uint2 ra[4], rb[4];
+  const uint8_t* x0 = reinterpret_cast<const uint8_t*>(kX0Run);
   auto fetch = [&](int r0) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = r0 + 4 * q4 + q;
-      if (r < r_end) {
-        const int img = r / 400;
-        const int p = r - img * 400;
-        const int oh = p / 20;
-        const int ow = p - oh * 20;
-        const uint8_t* base = obs + (long long)img * img_stride + (oh * 4 * AF_OBS_W + ow * 4) * 4;
-        uint2 a = *reinterpret_cast<const uint2*>(base + coffA);
-        ra[q] = make_uint2(a.x ^ 0x80808080u, a.y ^ 0x80808080u);
-        if (!diag) {
-          uint2 b = *reinterpret_cast<const uint2*>(base + coffB);
-          rb[q] = make_uint2(b.x ^ 0x80808080u, b.y ^ 0x80808080u);
-        }
-      } else {
-        ra[q] = make_uint2(0u, 0u);  // x = 0: contributes nothing
-        rb[q] = make_uint2(0u, 0u);
-      }
+      const bool ok = r < r_end;
+      const uint32_t rr = ok ? (uint32_t)r : (uint32_t)r_begin;
+      const uint32_t img = rr / 400u;
+      const uint32_t p = rr - img * 400u;
+      const uint32_t oh = p / 20u;
+      const uint32_t ow = p - oh * 20u;
+      const uint8_t* base = obs + (long long)img * img_stride + (oh * 4 * AF_OBS_W + ow * 4) * 4;
+      ra[q] = *reinterpret_cast<const uint2*>(ok ? base + coffA : x0);
+      if (!diag) rb[q] = *reinterpret_cast<const uint2*>(ok ? base + coffB : x0);
     }
   };
   // 4 rows x 4 bytes -> 4 column words of 4 consecutive rows (v_perm_b32)
@@ -94,16 +116,17 @@ __global__ __launch_bounds__(256) void conv1_afactor_i8_kernel(const uint8_t* ob
     out[3] = __builtin_amdgcn_perm(p23h, p01h, 0x07060302u);
   };
   auto commit = [&](int buf) {
+    constexpr uint32_t F = 0x80808080u;
     uint32_t cols[8];
-    transpose4(ra[0].x, ra[1].x, ra[2].x, ra[3].x, cols);
-    transpose4(ra[0].y, ra[1].y, ra[2].y, ra[3].y, cols + 4);
+    transpose4(ra[0].x ^ F, ra[1].x ^ F, ra[2].x ^ F, ra[3].x ^ F, cols);
+    transpose4(ra[0].y ^ F, ra[1].y ^ F, ra[2].y ^ F, ra[3].y ^ F, cols + 4);
     uint8_t* dst = lds[buf][0];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       *reinterpret_cast<uint32_t*>(dst + (8 * cg + j) * AF_LINE + 4 * q4) = cols[j];
     if (!diag) {
-      transpose4(rb[0].x, rb[1].x, rb[2].x, rb[3].x, cols);
-      transpose4(rb[0].y, rb[1].y, rb[2].y, rb[3].y, cols + 4);
+      transpose4(rb[0].x ^ F, rb[1].x ^ F, rb[2].x ^ F, rb[3].x ^ F, cols);
+      transpose4(rb[0].y ^ F, rb[1].y ^ F, rb[2].y ^ F, rb[3].y ^ F, cols + 4);
       uint8_t* dstb = lds[buf][1];
 #pragma unroll
       for (int j = 0; j < 8; ++j)
@@ -129,7 +152,8 @@ __global__ __launch_bounds__(256) void conv1_afactor_i8_kernel(const uint8_t* ob
   const int half = lane >> 5;
   for (int st = 0; st < nst; ++st) {
     const int cur = st & 1;
-    if (st + 1 < nst) fetch(r_begin + (st + 1) * AF_BK);
+    fetch(r_begin + (st + 1) * AF_BK);  // past the chunk: the x = 0 run
+    __builtin_amdgcn_sched_barrier(0);
     const uint8_t* As = lds[cur][0];
     const uint8_t* Bs = lds[cur][diag ? 0 : 1];
 #pragma unroll
@@ -152,7 +176,8 @@ __global__ __launch_bounds__(256) void conv1_afactor_i8_kernel(const uint8_t* ob
 #pragma unroll
       for (int w = 0; w < AF_BK / 4; ++w) csum = __builtin_amdgcn_sdot4((int)line[w], 0x01010101, csum, false);
     }
-    if (st + 1 < nst) commit(cur ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    commit(cur ^ 1);
     __syncthreads();
   }
 
@@ -218,21 +243,23 @@ __global__ void conv1_afactor_finalize(const int* part, const int* colsum, int n
 }
 
 long long conv1_afactor_ws_ints(long long rows) {
-  const long long nchunk = (rows + AF_CHUNK - 1) / AF_CHUNK;
-  return nchunk * (65536 + 256);
+  int nchunk, chunk;
+  af_plan(rows, &nchunk, &chunk);
+  return (long long)nchunk * (65536 + 256);
 }
 
 int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* astat, int* ws,
                      long long ws_ints, hipStream_t s) {
   const long long rows = 400LL * B;
-  const int nchunk = (int)((rows + AF_CHUNK - 1) / AF_CHUNK);
+  int nchunk, chunk;
+  af_plan(rows, &nchunk, &chunk);
   ACMI_REQUIRE(conv1_afactor_ws_ints(rows) <= ws_ints, ACMI_ERR_WS,
                "conv1 A-factor workspace too small");
   ACMI_REQUIRE(img_stride % 8 == 0, ACMI_ERR_ARG, "conv1 A factor needs 8-byte aligned images");
   int* part = ws;
   int* colsum = ws + (long long)nchunk * 65536;
-  hipLaunchKernelGGL(conv1_afactor_i8_kernel, dim3(3, nchunk), dim3(256), 0, s, obs, img_stride,
-                     (int)rows, part, colsum);
+  hipLaunchKernelGGL(conv1_afactor_i8_kernel, dim3(3 * nchunk), dim3(256), 0, s, obs, img_stride,
+                     (int)rows, chunk, part, colsum);
   hipLaunchKernelGGL(conv1_afactor_finalize, dim3(cdiv(257 * 257, 256)), dim3(256), 0, s, part,
                      colsum, nchunk, (int)rows, astat);
   ACMI_LAUNCH_CHECK("conv1_afactor_u8");
