@@ -11,6 +11,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), 'libacmi.so')
+if os.environ.get('ACMI_LIB'):  # A/B timing of another build (scripts/kbench.py)
+    LIB_PATH = os.environ['ACMI_LIB']
 
 c_int = ctypes.c_int
 c_i64 = ctypes.c_int64

@@ -63,9 +63,30 @@ def backward(M, with_stats=True, site=1, reps=10):
         M, with_stats, ms, site, tot.value / max(1, cnt.value), cnt.value))
 
 
+def inverse(A=4, C3=32, reps=10):
+    lib = _lib.load()
+    din = (ctypes.c_int64 * 6)()
+    dout = (ctypes.c_int64 * 6)()
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, din, dout, so, ctypes.byref(tot))
+    fac = torch.zeros(tot.value, device='cuda')
+    for f in range(11):
+        n = din[f] if f < 5 else dout[f - 5]
+        x = torch.randn(2 * n, n, device='cuda')
+        fac[so[f]:so[f] + n * n] = (x.t() @ x / (2 * n)).reshape(-1)
+    inv = torch.zeros(lib.acmi_kfac_inverse_floats(A, C3), device='cuda')
+    ws = torch.zeros(lib.acmi_kfac_inverse_ws_doubles(A, C3), dtype=torch.float64, device='cuda')
+    ms = timeit(lambda: _lib.call('acmi_kfac_inverse', A, C3, _lib.ptr(fac), ctypes.c_float(0.01), 0,
+                                  _lib.ptr(inv), _lib.ptr(ws), _lib.stream_handle()), reps=reps)
+    print('kfac inverse (all 12 damped inverses): {:.3f} ms'.format(ms))
+
+
 if __name__ == '__main__':
     what = sys.argv[1]
-    if what == 'gemm':
+    if what == 'inverse':
+        inverse()
+    elif what == 'gemm':
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 4096)
     elif what == 'backward1':  # a short run for PMC passes
         backward(int(sys.argv[2]) if len(sys.argv) > 2 else 10240, True, 2, reps=2)
