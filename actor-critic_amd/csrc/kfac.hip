@@ -139,31 +139,46 @@ __global__ void damp_kernel(DampSet d, const double* tr, double* ws) {
   }
 }
 
-// in-LDS Gauss-Jordan (sweep) inverse of the GJB x GJB pivot block
+// Gauss-Jordan (sweep) inverse of the GJB x GJB pivot block in the registers
+// of wave 0: lane c (< 32) holds column c; the pivot column t is broadcast
+// from lane t with readlane (t is a compile-time index after unrolling), so
+// the 32 sequential sweeps need no LDS round trips and no block barriers.
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 __device__ void pivot_inverse(double (*P)[GJB + 1]) {
-  const int tid = threadIdx.x;  // 256 threads, 4 elements each
-  for (int t = 0; t < GJB; ++t) {
-    const double piv = P[t][t];
-    const double ipiv = 1.0 / piv;
-    double nv[4];
+  static_assert(GJB == 32, "one lane per pivot-block column");
+  if (threadIdx.x < 64) {
+    const int c = threadIdx.x & 31;  // lanes 32..63 mirror 0..31
+    double col[GJB];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = tid + 256 * q;
-      const int r = e / GJB, c = e - r * GJB;
-      const double v = P[r][c];
-      if (r == t && c == t) nv[q] = ipiv;
-      else if (r == t) nv[q] = v * ipiv;
-      else if (c == t) nv[q] = -v * ipiv;
-      else nv[q] = v - P[r][t] * P[t][c] * ipiv;
-    }
-    __syncthreads();
+    for (int r = 0; r < GJB; ++r) col[r] = P[r][c];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int e = tid + 256 * q;
-      P[e / GJB][e % GJB] = nv[q];
+    for (int t = 0; t < GJB; ++t) {
+      double pt[GJB];  // column t (uniform across lanes)
+#pragma unroll
+      for (int r = 0; r < GJB; ++r) pt[r] = readlane_d(col[r], t);
+      const double ipiv = 1.0 / pt[t];
+      const double ptc = col[t];  // row t, this lane's column
+      const bool is_t = c == t;
+#pragma unroll
+      for (int r = 0; r < GJB; ++r) {
+        double nv;
+        if (r == t) nv = is_t ? ipiv : col[r] * ipiv;
+        else nv = is_t ? -pt[r] * ipiv : col[r] - pt[r] * ptc * ipiv;
+        col[r] = nv;
+      }
     }
-    __syncthreads();
+    if (threadIdx.x < 32) {
+#pragma unroll
+      for (int r = 0; r < GJB; ++r) P[r][c] = col[r];
+    }
   }
+  __syncthreads();
 }
 
 constexpr int PANEL_COLS = 256;
@@ -198,10 +213,13 @@ __global__ __launch_bounds__(256) void gj_panel_kernel(MatSet s, double* ws, int
         R[(long long)t * np + j] = acc;
       }
     }
-    // Ccol[i][t] = M[i][kb + t] for rows i in this chunk (old values)
-    const int i = j;
-#pragma unroll
-    for (int t = 0; t < GJB; ++t) C[(long long)i * GJB + t] = M[(long long)i * np + kb + t];
+  }
+  // Ccol[i][t] = M[i][kb + t] for the rows i of this chunk (old values): t
+  // fastest over consecutive threads, so reads and writes are coalesced
+  const int rows = min(PANEL_COLS, np - c0);
+  for (int e = threadIdx.x; e < rows * GJB; e += 256) {
+    const int i = c0 + e / GJB, t = e % GJB;
+    C[(long long)i * GJB + t] = M[(long long)i * np + kb + t];
   }
 }
 
@@ -224,7 +242,26 @@ __global__ __launch_bounds__(256) void gj_update_kernel(MatSet s, double* ws, in
     Rs[tt][c] = (j0 + c < np) ? R[(long long)tt * np + j0 + c] : 0.0;
   }
   __syncthreads();
+  // 4x4 outputs per thread, register-blocked: per pivot column t, 4 values of
+  // Ccol and 4 of Rrow' feed 16 FMAs
   const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
+  double acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+#pragma unroll 8
+  for (int t = 0; t < GJB; ++t) {
+    double cv[4], rv[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) cv[a] = Cs[ty + 16 * a][t];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) rv[b] = Rs[t][tx + 16 * b];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] += cv[a] * rv[b];
+  }
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
     const int i = i0 + ty + 16 * a;
@@ -239,10 +276,7 @@ __global__ __launch_bounds__(256) void gj_update_kernel(MatSet s, double* ws, in
       if (ipiv) {
         v = R[(long long)(i - kb) * np + j];  // pivot rows: Pinv M_kj (Pinv itself in-block)
       } else {
-        double acc = 0.0;
-#pragma unroll 8
-        for (int t = 0; t < GJB; ++t) acc += Cs[ty + 16 * a][t] * Rs[t][tx + 16 * b];
-        v = (jpiv ? 0.0 : M[(long long)i * np + j]) - acc;
+        v = (jpiv ? 0.0 : M[(long long)i * np + j]) - acc[a][b];
       }
       M[(long long)i * np + j] = v;
     }
