@@ -199,10 +199,13 @@ __global__ __launch_bounds__(256) void conv1_afactor_i8_kernel(const uint8_t* ob
 // A (257 x 257, f32) from the exact integer sums; element (a, b), a,b <= 256
 __global__ void conv1_afactor_finalize(const int* part, const int* colsum, int nchunk, int rows,
                                        float* astat) {
+  // upper triangle only (consecutive threads read consecutive partials),
+  // written to both halves
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= 257 * 257) return;
   const int a = idx / 257, b = idx - a * 257;
-  const int lo = a < b ? a : b, hi = a < b ? b : a;
+  if (a > b) return;
+  const int lo = a, hi = b;
   const long long R = rows;
   double v;
   if (hi == 256 && lo == 256) {
@@ -239,7 +242,8 @@ __global__ void conv1_afactor_finalize(const int* part, const int* colsum, int n
       v = (double)uu / (65025.0 * (double)R);
     }
   }
-  astat[idx] = (float)v;
+  astat[lo * 257 + hi] = (float)v;
+  astat[hi * 257 + lo] = (float)v;
 }
 
 long long conv1_afactor_ws_ints(long long rows) {

@@ -700,8 +700,9 @@ int acmi_kfac_step(int A, int C3, float* params, float* velocity, const float* g
     EpiStore e2{out, dout};
     if (dout % 4 == 0) {
       MatI<true> b1{g, dout, din, dout};
+      // 64x64 tiles: fc4 (1569 x 512) gives 200 blocks instead of 52
       if (dout >= 128)
-        launch_gemm<128, 128, 32, 2, 2, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
+        launch_gemm<64, 64, 32, 1, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
       else if (dout > 32)
         launch_gemm<128, 64, 32, 2, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
       else
@@ -711,7 +712,7 @@ int acmi_kfac_step(int A, int C3, float* params, float* velocity, const float* g
       launch_gemm<128, 32, 32, 1, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
     }
     if (dout >= 128)
-      launch_gemm<128, 128, 32, 2, 2, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
+      launch_gemm<64, 64, 32, 1, 1, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
     else if (dout > 32)
       launch_gemm<128, 64, 32, 2, 1, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
     else

@@ -108,12 +108,16 @@ __global__ void heads_dx_kernel(const float* dhead, int ldh, int B, const float*
     for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(ga, wpi[(j0 + e) * A + a], acc[e]);
   }
   const float gv = g[A];  // (wv is not 16-byte aligned for every A: scalar loads)
+#pragma unroll
+  for (int e = 0; e < 4; ++e) acc[e] = __builtin_fmaf(gv, wv[j0 + e], acc[e]);
   const float4 x = *reinterpret_cast<const float4*>(a4 + q * 4);
+  // masks as multiplies by 0/1 of the computed sums (a select with a load
+  // operand would be turned into a branch around the load)
   float4 o;
-  o.x = x.x > 0.f ? __builtin_fmaf(gv, wv[j0 + 0], acc[0]) : 0.f;
-  o.y = x.y > 0.f ? __builtin_fmaf(gv, wv[j0 + 1], acc[1]) : 0.f;
-  o.z = x.z > 0.f ? __builtin_fmaf(gv, wv[j0 + 2], acc[2]) : 0.f;
-  o.w = x.w > 0.f ? __builtin_fmaf(gv, wv[j0 + 3], acc[3]) : 0.f;
+  o.x = acc[0] * (float)(x.x > 0.f);
+  o.y = acc[1] * (float)(x.y > 0.f);
+  o.z = acc[2] * (float)(x.z > 0.f);
+  o.w = acc[3] * (float)(x.w > 0.f);
   *reinterpret_cast<float4*>(d4 + q * 4) = o;
 }
 
@@ -321,20 +325,23 @@ __global__ void finalize_wgrad_kernel(WgradDesc d) {
     if (n < d.nsplit) d.gradA[(long long)a * d.nsplit + n] = s;
     else d.gradB[(long long)a * (d.cout - d.nsplit) + (n - d.nsplit)] = s;
   } else {
+    // upper triangle only (a <= b: consecutive b read consecutive partials),
+    // written to both halves
     const long long e = idx - ngrad;
     const int a = (int)(e / (K + 1));
     const int b = (int)(e - (long long)a * (K + 1));
-    const int lo = a < b ? a : b;
-    const int hi = a < b ? b : a;
+    if (a > b) return;
     float s;
-    if (hi == K && lo == K) {
+    if (a == K) {
       s = (float)d.rows;
     } else {
-      const int col = hi < K ? hi : d.J - 1;
-      const float* p = d.part + (long long)lo * d.J + col;
+      const int col = b < K ? b : d.J - 1;
+      const float* p = d.part + (long long)a * d.J + col;
       s = chunk_sum(p, d.nchunk, cs);
     }
-    d.astat[e] = s * (1.0f / (float)d.rows);
+    s *= 1.0f / (float)d.rows;
+    d.astat[(long long)a * (K + 1) + b] = s;
+    d.astat[(long long)b * (K + 1) + a] = s;
   }
 }
 
