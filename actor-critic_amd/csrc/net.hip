@@ -348,6 +348,21 @@ __global__ void finalize_wgrad_kernel(WgradDesc d) {
 // G factor: part [nchunk][I+1][J] (I == J == n, no colsum row used); one
 // wave per output element sums the chunks in a fixed (lane-strided, then
 // butterfly) order, so the result is deterministic.
+// thread per upper-triangle element (few chunks): consecutive threads read
+// consecutive partials, the value is written to both halves
+__global__ void finalize_cov_thread_kernel(const float* part, int nchunk, int n, int sub,
+                                           float* out, int rows) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= sub * sub) return;
+  const int a = idx / sub, b = idx - a * sub;
+  if (a > b) return;
+  const long long cs = (long long)(n + 1) * n;
+  const float v = chunk_sum(part + (long long)a * n + b, nchunk, cs) * (1.0f / (float)rows);
+  out[a * sub + b] = v;
+  out[b * sub + a] = v;
+}
+
+// wave per element (many chunks: the lanes split the chunks)
 __global__ void finalize_cov_kernel(const float* part, int nchunk, int n,
                                     int sub, float* out, int rows) {
   // out is sub x sub, taken from the top-left of the n x n product
@@ -562,8 +577,12 @@ static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
     EpiPartial epi{part, np, np};
     launch_gemm<64, 64, 32, 1, 1, true, false>(op, op, epi, np, np, (int)rows, nc, pl.ch, s, np);
   }
-  hipLaunchKernelGGL(finalize_cov_kernel, dim3(cdiv((long long)sub * sub, 4)), dim3(256), 0,
-                     s, part, nc, np, sub, out, (int)rows);
+  if (nc <= 64)
+    hipLaunchKernelGGL(finalize_cov_thread_kernel, dim3(cdiv((long long)sub * sub, 256)), dim3(256), 0,
+                       s, part, nc, np, sub, out, (int)rows);
+  else
+    hipLaunchKernelGGL(finalize_cov_kernel, dim3(cdiv((long long)sub * sub, 4)), dim3(256), 0,
+                       s, part, nc, np, sub, out, (int)rows);
   if (out_v)
     hipLaunchKernelGGL(finalize_cov_elem_kernel, dim3(1), dim3(64), 0, s, part, nc, np,
                        v_index, out_v, (int)rows);
