@@ -6,7 +6,7 @@
 //   * conv forward (implicit im2col, u8/255 fused for conv1)       RowsAsK
 //   * conv input-gradient (transposed conv as a per-stride-phase gather)
 //   * fc forward / input-gradient
-//   * weight gradient fused with the K-FAC A-factor: [P;1]^T [P | dY | 1]
+//   * weight gradient fused with the K-FAC A-factor: [P;1]^T [P | dY]
 //     over the huge row dimension, split over blockIdx.z into per-chunk
 //     partials reduced later in a fixed order (deterministic, no atomics)
 //   * K-FAC G-factors and the natural-gradient preconditioning products.
@@ -100,9 +100,11 @@ __device__ __forceinline__ void store_tile(const Epi& epi, const Acc& acc, int i
 // latency-bound shapes (short per-tile MFMA work, L2-missing gathers).
 template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM,
           class OpA, class OpB, class Epi, int DEPTH = 1>
-__global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
-                                                   int I, int J, int K,
-                                                   int k_chunk, int sym_cols) {
+// waves_per_eu(4): the 128x128x16 reduction tiles fit 4 blocks per CU in LDS;
+// without the hint the compiler parks the accumulators in AGPRs next to ~85
+// VGPRs and only 3 fit, so the planned rounds (plan_rounds) would not be resident
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+void gemm_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, int sym_cols) {
   using TL = Tile<BM, BN, BK, WTM, WTN>;
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if constexpr (SPLITK) {
@@ -354,8 +356,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(OpA opA, OpB opB, Epi epi,
   // A wave whose whole sub-tile lies strictly below the diagonal of the
   // symmetric block (diagonal blocks, sym_cols) computes nothing anyone reads:
   // it only stages and syncs (its SIMD serves the co-resident blocks' MFMAs).
-  const int wrow0 = i0 + wm * WTM * 32, wcol1 = j0 + (wn + 1) * WTN * 32;
-  const bool wave_idle = sym_cols > 0 && wcol1 <= wrow0 && wcol1 <= sym_cols;
+  // So does a wave whose sub-tile lies wholly outside I x J (edge tiles).
+  const int wrow0 = i0 + wm * WTM * 32, wcol0 = j0 + wn * WTN * 32, wcol1 = wcol0 + WTN * 32;
+  const bool wave_idle =
+      (sym_cols > 0 && wcol1 <= wrow0 && wcol1 <= sym_cols) || wrow0 >= I || wcol0 >= J;
   using MFon = std::integral_constant<bool, true>;
   using MFoff = std::integral_constant<bool, false>;
   if (!wave_idle) {

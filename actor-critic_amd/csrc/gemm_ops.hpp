@@ -249,9 +249,10 @@ using RowsAsK = RowsOp<Src, true>;
 template <class Src>
 using RowsAsI = RowsOp<Src, false>;
 
-// B(k, j) over row k of [P | dY | 1]:  j < kp -> P(k, j) (kp = 0 skips P),
-// kp <= j < kp + cout_pad -> dY(k, j-kp), j == kp+cout_pad -> 1 (homogeneous
-// column, only for rows k < rows).  dY rows must be zero-padded from cout up to
+// B(k, j) over row k of [P | dY]:  j < kp -> P(k, j) (kp = 0 skips P),
+// kp <= j < kp + cout_pad -> dY(k, j-kp), zero beyond.  The homogeneous
+// coordinate needs no column: its row is the kernel's column sums and its
+// column equals that row's P part by symmetry.  dY rows must be zero-padded from cout up to
 // cout_pad <= ldy (the loss kernel writes its padding; conv/fc couts are
 // multiples of 4), so every dY run is one unmasked float4.
 template <class Src>
@@ -264,7 +265,7 @@ struct CatRowsI {
   };
   struct C {
     typename Src::Cp p;
-    int seg;  // 0 patch, 1 dY, 2 homogeneous, 3 zero
+    int seg;  // 0 patch, 1 dY, 3 zero
     int jj;
   };
   Src src;
@@ -282,7 +283,7 @@ struct CatRowsI {
     C c;
     c.p = src.col(j < kp ? j : 0);
     c.jj = j - kp;
-    c.seg = j < kp ? 0 : (c.jj < cout_pad ? 1 : (c.jj == cout_pad ? 2 : 3));
+    c.seg = j < kp ? 0 : (c.jj < cout_pad ? 1 : 3);
     return c;
   }
   // One float4 load per element: P and dY are both float rows, so the
@@ -292,8 +293,7 @@ struct CatRowsI {
     // u8 patch sources only appear with kp == 0 (plain conv1 weight gradient)
     constexpr bool FP = std::is_same<typename Src::elem_t, float>::value;
     const bool rin = in && r.ok;
-    const float* a = (c.seg == 2 && rin) ? homog_run() : zero_run();
-    a = (c.seg == 1 && rin) ? dy + (r.dyoff + (uint32_t)c.jj) : a;
+    const float* a = (c.seg == 1 && rin) ? dy + (r.dyoff + (uint32_t)c.jj) : zero_run();
     if constexpr (FP) a = (c.seg == 0 && rin && r.p.ok && c.p.ok) ? src.x + (r.p.off + c.p.off) : a;
     return *reinterpret_cast<const float4*>(a);
   }

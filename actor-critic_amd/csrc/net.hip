@@ -335,8 +335,8 @@ __global__ void finalize_wgrad_kernel(WgradDesc d) {
     if (a == K) {
       s = (float)d.rows;
     } else {
-      const int col = b < K ? b : d.J - 1;
-      const float* p = d.part + (long long)a * d.J + col;
+      // column K (the homogeneous coordinate) = sum of P = column-sum row
+      const float* p = b < K ? d.part + (long long)a * d.J + b : d.part + (long long)d.I * d.J + a;
       s = chunk_sum(p, d.nchunk, cs);
     }
     s *= 1.0f / (float)d.rows;
@@ -490,7 +490,9 @@ static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows) {
   p.cout_pad = roundup4(cout);
   p.kp = with_stats ? K : 0;
   p.I = K;
-  p.J = p.kp + p.cout_pad + (with_stats ? 1 : 0);
+  // no homogeneous column: the A factor's last column (sum of P) is the
+  // column-sum row's P part, by symmetry
+  p.J = p.kp + p.cout_pad;
   if (with_stats)
     plan_rounds(rows, live_tiles<128, 128>(p.I, p.J, K),
                 kCUs * gemm_blocks_per_cu<128, 128, 16, false, false>(), &p.nc, &p.ch);
@@ -524,7 +526,8 @@ static GcovPlan gcov_plan(int n, long long rows) {
   return p;
 }
 
-// Launch [P;1]^T [P | dY | 1] (with_stats) or P^T [dY] (+colsum) over rows.
+// Launch [P;1]^T [P | dY] (with_stats; the 1 row is the column-sum row) or
+// [P;1]^T [dY] over rows.
 template <class Src>
 static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
                        int ldy, int cout, bool with_stats, float* part,

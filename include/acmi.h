@@ -303,7 +303,7 @@ int acmi_gemm_f32(const float* A, const float* B, float* C, int M, int N,
  * the launch stream around every launch of `site` (up to `capacity`);
  * acmi_prof_collect synchronises them and returns the summed milliseconds
  * and the count, then rearms.  site 0 disables.  Not graph-capture safe. */
-#define ACMI_PROF_CONV1_WGRAD 1 /* conv1 [P;1]^T [P | dY | 1] reduction GEMM */
+#define ACMI_PROF_CONV1_WGRAD 1 /* conv1 [P;1]^T [dY] reduction GEMM */
 #define ACMI_PROF_CONV2_WGRAD 2
 #define ACMI_PROF_CONV1_FWD 3
 #define ACMI_PROF_CONV1_AFACTOR 4 /* exact-integer i8-MFMA conv1 A factor */
