@@ -94,6 +94,7 @@ PROF_CONV1_WGRAD = 1
 PROF_CONV2_WGRAD = 2
 PROF_CONV1_FWD = 3
 PROF_CONV1_AFACTOR = 4
+PROF_CONV2_DX = 5
 
 EXPORTED = tuple(_SIGS)
 

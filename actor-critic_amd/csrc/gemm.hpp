@@ -65,34 +65,68 @@ struct Tile {
 // Epilogue of a wave's (32*WTM) x (32*WTN) sub-tile at (ib, jb):
 // acc[tm][tn][r] -> (ib + 32tm + (r&3) + 8(r>>2) + 4(lane>>5), jb + 32tn + (lane&31))
 // (gfx950 32x32 C/D map).  All aux loads first (clamped indices), then the
-// bounded stores.
+// bounded stores.  Epilogues with VEC4 take the four consecutive rows a lane
+// holds (r = 4g..4g+3) as one float4 (aux4/store4 at row i0 = 4-aligned; I % 4
+// == 0): one 16-byte access instead of four scalar ones when those rows are
+// contiguous in memory.
+template <class T, class = void>
+struct has_vec4 : std::false_type {};
+template <class T>
+struct has_vec4<T, std::void_t<decltype(T::VEC4)>> : std::integral_constant<bool, T::VEC4> {};
+
 template <int WTM, int WTN, class Epi, class Acc>
 __device__ __forceinline__ void store_tile(const Epi& epi, const Acc& acc, int ib, int jb, int lane,
                                            int I, int J) {
   const int khalf = lane >> 5;
-  float x[WTM][WTN][16];
+  if constexpr (has_vec4<Epi>::value) {
+    float4 x[WTM][WTN][4];
 #pragma unroll
-  for (int tm = 0; tm < WTM; ++tm)
+    for (int tm = 0; tm < WTM; ++tm)
 #pragma unroll
-    for (int tn = 0; tn < WTN; ++tn) {
-      const int j = min(jb + tn * 32 + (lane & 31), J - 1);
+      for (int tn = 0; tn < WTN; ++tn) {
+        const int j = min(jb + tn * 32 + (lane & 31), J - 1);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = min(ib + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf, I - 1);
-        x[tm][tn][r] = epi.aux(i, j);
+        for (int g = 0; g < 4; ++g)
+          x[tm][tn][g] = epi.aux4(min(ib + tm * 32 + 8 * g + 4 * khalf, I - 4), j);
       }
-    }
 #pragma unroll
-  for (int tm = 0; tm < WTM; ++tm)
+    for (int tm = 0; tm < WTM; ++tm)
 #pragma unroll
-    for (int tn = 0; tn < WTN; ++tn) {
-      const int j = jb + tn * 32 + (lane & 31);
+      for (int tn = 0; tn < WTN; ++tn) {
+        const int j = jb + tn * 32 + (lane & 31);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int i = ib + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
-        if (i < I && j < J) epi.store(i, j, acc[tm][tn][r], x[tm][tn][r]);
+        for (int g = 0; g < 4; ++g) {
+          const int i0 = ib + tm * 32 + 8 * g + 4 * khalf;
+          const float4 v = make_float4(acc[tm][tn][4 * g], acc[tm][tn][4 * g + 1],
+                                       acc[tm][tn][4 * g + 2], acc[tm][tn][4 * g + 3]);
+          if (i0 < I && j < J) epi.store4(i0, j, v, x[tm][tn][g]);
+        }
       }
-    }
+  } else {
+    float x[WTM][WTN][16];
+#pragma unroll
+    for (int tm = 0; tm < WTM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < WTN; ++tn) {
+        const int j = min(jb + tn * 32 + (lane & 31), J - 1);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = min(ib + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf, I - 1);
+          x[tm][tn][r] = epi.aux(i, j);
+        }
+      }
+#pragma unroll
+    for (int tm = 0; tm < WTM; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < WTN; ++tn) {
+        const int j = jb + tn * 32 + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = ib + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+          if (i < I && j < J) epi.store(i, j, acc[tm][tn][r], x[tm][tn][r]);
+        }
+      }
+  }
 }
 
 // DEPTH: K-tiles of staging loads in flight (register sets): 1 = the next
@@ -430,26 +464,38 @@ struct EpiReluGrad {
   }
 };
 
-// input-gradient of a strided conv, one phase per grid z (member z): row i =
-// (img, ih', iw') -> NHWC pixel (S*ih'+ph, S*iw'+pw); masked by ReLU'.
+// input-gradient of a strided conv as the TRANSPOSED product: row i =
+// (ph, pw, ci) (all stride phases), column j = super-pixel (img, ih', iw') ->
+// NHWC pixel (S*ih'+ph, S*iw'+pw), channel ci; masked by ReLU'.  A lane's four
+// consecutive rows are four consecutive channels of one pixel (VEC4).
 template <int IH, int IW, int S, int CIN>
-struct EpiConvTPhase {
+struct EpiConvT {
+  static constexpr bool VEC4 = true;
+  static_assert(CIN % 4 == 0, "channel runs of 4");
   float* out;
   const float* act;
-  int z = 0;  // stride phase, set by the kernel
   __device__ __forceinline__ long long offset(int i, int j) const {
     constexpr int PH = IH / S, PW = IW / S, L = PH * PW;
-    const int ph = z / S;
-    const int pw = z - ph * S;
-    const uint32_t img = (uint32_t)i / L;
-    const uint32_t p = (uint32_t)i - img * L;
+    const uint32_t img = (uint32_t)j / L;
+    const uint32_t p = (uint32_t)j - img * L;
     const uint32_t ihp = p / PW;
     const uint32_t iwp = p - ihp * PW;
-    return (((long long)img * IH + (S * ihp + ph)) * IW + (S * iwp + pw)) * CIN + j;
+    const int ph = i / (S * CIN);
+    const int rem = i - ph * (S * CIN);
+    const int pw = rem / CIN;
+    const int ci = rem - pw * CIN;
+    return (((long long)img * IH + (S * ihp + ph)) * IW + (S * iwp + pw)) * CIN + ci;
   }
-  __device__ __forceinline__ float aux(int i, int j) const { return act[offset(i, j)]; }
-  __device__ __forceinline__ void store(int i, int j, float v, float x) const {
-    out[offset(i, j)] = x > 0.f ? v : 0.f;
+  __device__ __forceinline__ float4 aux4(int i0, int j) const {
+    return *reinterpret_cast<const float4*>(act + offset(i0, j));
+  }
+  __device__ __forceinline__ void store4(int i0, int j, float4 v, float4 x) const {
+    float4 o;
+    o.x = x.x > 0.f ? v.x : 0.f;
+    o.y = x.y > 0.f ? v.y : 0.f;
+    o.z = x.z > 0.f ? v.z : 0.f;
+    o.w = x.w > 0.f ? v.w : 0.f;
+    *reinterpret_cast<float4*>(out + offset(i0, j)) = o;
   }
 };
 

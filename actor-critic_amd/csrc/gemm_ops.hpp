@@ -349,30 +349,36 @@ struct MatTK {
 };
 using MatTKu = MatTK<false>;
 
-// Conv weight as the B operand of the input gradient, one stride phase per
-// block (member z):  B(k = (kh',kw',co), j = ci) = W[ph+S*kh'][pw+S*kw'][ci][co].
+// Conv weight as the A operand of the (transposed) input gradient, all S*S
+// stride phases stacked: A(k = (kh',kw',co), i = (ph,pw,ci)) =
+// W[ph+S*kh'][pw+S*kw'][ci][co].  Every phase of an input super-pixel
+// (ih', iw') gathers the same dY neighbourhood (ConvTRows), so the phases are
+// just more rows of one GEMM: S*S*CIN of them (128 for conv2) instead of CIN.
+// The tap offset separates into an i part and a k part.
 template <int KH, int KW, int S, int CIN, int COUT>
 struct ConvTWeights {
   static constexpr bool KCONTIG = true;
   static constexpr int KHP = KH / S;
   static constexpr int KWP = KW / S;
   static constexpr int K = KHP * KWP * COUT;
+  static constexpr int N = S * S * CIN;
   using R = OffOk;
   using C = OffOk;
   const float* w;  // HWIO
-  int z = 0;       // stride phase (ph, pw) = (z / S, z % S), set by the kernel
-  __device__ __forceinline__ R row(int j) const { return R{(uint32_t)j * COUT, j < CIN}; }
+  __device__ __forceinline__ R row(int j) const {
+    const int ph = j / (S * CIN);
+    const int rem = j - ph * (S * CIN);
+    const int pw = rem / CIN;
+    const int ci = rem - pw * CIN;
+    return R{(uint32_t)(((ph * KW + pw) * CIN + ci) * COUT), j < N};
+  }
   __device__ __forceinline__ C col(int k) const {
     if (k >= K) return C{0, false};
-    const int ph = z / S;
-    const int pw = z - ph * S;
     const int khp = k / (KWP * COUT);
     const int rem = k - khp * (KWP * COUT);
     const int kwp = rem / COUT;
     const int co = rem - kwp * COUT;
-    const int kh = ph + S * khp;
-    const int kw = pw + S * kwp;
-    return C{(uint32_t)((kh * KW + kw) * CIN * COUT + co), true};
+    return C{(uint32_t)(S * (khp * KW + kwp) * CIN * COUT + co), true};
   }
   using St = StF4;
   __device__ __forceinline__ St stage(const R& r, const C& c, bool in) const {

@@ -634,19 +634,26 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     EpiReluGrad epi{bw->d3, a->a3, K3};
     launch_gemm<64, 128, 32, 1, 2, false, false>(opA, opB, epi, B, K3, 512, 1, 0, s);
   }
+  // conv input gradients as transposed products: rows = (phase, channel) of
+  // the weights, columns = (super-)pixels gathering dY (EpiConvT, float4 rows)
   {  // conv3 -> d2 (stride 1: one phase)
     using Src = ConvTRows<9, 9, 3, 3, 1, C3>;
-    RowsAsK<Src> opA{Src{bw->d3, B * Src::L}};
-    ConvTWeights<3, 3, 1, 64, C3> opB{P + L.off[4]};
-    EpiConvTPhase<9, 9, 1, 64> epi{bw->d2, a->a2};
-    launch_gemm<128, 64, 32, 2, 1, false, false>(opA, opB, epi, B * Src::L, 64, Src::COLS, 1, 0, s);
+    using W = ConvTWeights<3, 3, 1, 64, C3>;
+    W opA{P + L.off[4]};
+    RowsAsK<Src> opB{Src{bw->d3, B * Src::L}};
+    EpiConvT<9, 9, 1, 64> epi{bw->d2, a->a2};
+    launch_gemm<64, 128, 32, 1, 2, false, false>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
   }
-  {  // conv2 -> d1 (stride 2: four phases on blockIdx.z)
+  {  // conv2 -> d1 (stride 2: the four phases of a 2x2 super-pixel are the
+     // 4 x 32 rows of one product over the 10x10 super-pixels)
     using Src = ConvTRows<20, 20, 4, 4, 2, 64>;
-    RowsAsK<Src> opA{Src{bw->d2, B * Src::L}};
-    ConvTWeights<4, 4, 2, 32, 64> opB{P + L.off[2]};
-    EpiConvTPhase<20, 20, 2, 32> epi{bw->d1, a->a1};
-    launch_gemm<128, 32, 32, 1, 1, false, false>(opA, opB, epi, B * Src::L, 32, Src::COLS, 4, 0, s);
+    using W = ConvTWeights<4, 4, 2, 32, 64>;
+    W opA{P + L.off[2]};
+    RowsAsK<Src> opB{Src{bw->d2, B * Src::L}};
+    EpiConvT<20, 20, 2, 32> epi{bw->d1, a->a1};
+    prof_begin(ACMI_PROF_CONV2_DX, s);
+    launch_gemm<128, 128, 16, 2, 2, false, false>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
+    prof_end(ACMI_PROF_CONV2_DX, s);
   }
   ACMI_LAUNCH_CHECK("dx_chain");
   return ACMI_OK;

@@ -212,44 +212,37 @@ int main(int argc, char** argv) {
            2.0 * R * 256.0 * 128.0 * 10 / ms8 / 1e9);
     (void)live2;
   }
-  {  // conv2 input gradient: 4 stride phases, K = 4 taps x 64 per phase
+  {  // conv2 input gradient: the 4 stride phases as 4 x 32 columns, K = 4 taps x 64
     using Src = ConvTRows<20, 20, 4, 4, 2, 64>;
+    using W = ConvTWeights<4, 4, 2, 32, 64>;
     float *w2, *d1;
     CK(hipMalloc(&w2, 4 * 4 * 32 * 64 * 4));
     CK(hipMalloc(&d1, a1n * 4));
     fill<<<64, 256>>>(w2, 4 * 4 * 32 * 64, 9);
     RowsAsK<Src> opA{Src{dy, M * Src::L}};
-    ConvTWeights<4, 4, 2, 32, 64> opB{w2};
-    EpiConvTPhase<20, 20, 2, 32> epi{d1, a1};
-    const double fl = 2.0 * M * Src::L * 32 * Src::COLS * 4;
+    W opB{w2};
+    EpiConvT<20, 20, 2, 32> epi{d1, a1};
+    const double fl = 2.0 * M * Src::L * W::N * Src::COLS;
     float m1 = timeit([&] {
-      launch_gemm<256, 32, 32, 2, 1, false, false>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0, 0);
+      launch_gemm<128, 128, 16, 2, 2, false, false>(opA, opB, epi, M * Src::L, W::N, Src::COLS, 1, 0, 0);
     });
-    printf("conv2 dX 256x32x32: %.3f ms  %.1f TF\n", m1, fl / m1 / 1e9);
+    printf("conv2 dX 128x128x16: %.3f ms  %.1f TF\n", m1, fl / m1 / 1e9);
+    float m2 = timeit([&] {
+      launch_gemm<128, 128, 32, 2, 2, false, false>(opA, opB, epi, M * Src::L, W::N, Src::COLS, 1, 0, 0);
+    });
+    printf("conv2 dX 128x128x32: %.3f ms  %.1f TF\n", m2, fl / m2 / 1e9);
     float m3 = timeit([&] {
-      launch_gemm<128, 32, 32, 1, 1, false, false>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0, 0);
+      launch_gemm<128, 64, 32, 2, 1, false, false>(opA, opB, epi, M * Src::L, W::N, Src::COLS, 1, 0, 0);
     });
-    printf("conv2 dX 128x32x32: %.3f ms  %.1f TF\n", m3, fl / m3 / 1e9);
-    float m5 = timeit([&] {
-      launch_gemm<128, 32, 32, 1, 1, false, false, 2>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0, 0);
-    });
-    printf("conv2 dX 128x32x32 depth2: %.3f ms  %.1f TF\n", m5, fl / m5 / 1e9);
-    float m7 = timeit([&] {
-      launch_gemm_stream<128, 32, 32, 1, 1>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0);
-    });
-    printf("conv2 dX 128x32x32 stream: %.3f ms  %.1f TF\n", m7, fl / m7 / 1e9);
-    float m8 = timeit([&] {
-      launch_gemm_stream<256, 32, 32, 2, 1>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0);
-    });
-    printf("conv2 dX 256x32x32 stream: %.3f ms  %.1f TF\n", m8, fl / m8 / 1e9);
-    float m6 = timeit([&] {
-      launch_gemm<256, 32, 32, 2, 1, false, false, 2>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0, 0);
-    });
-    printf("conv2 dX 256x32x32 depth2: %.3f ms  %.1f TF\n", m6, fl / m6 / 1e9);
+    printf("conv2 dX 128x64x32: %.3f ms  %.1f TF\n", m3, fl / m3 / 1e9);
     float m4 = timeit([&] {
-      launch_gemm<128, 32, 64, 1, 1, false, false>(opA, opB, epi, M * Src::L, 32, Src::COLS, 4, 0, 0);
+      launch_gemm<64, 128, 32, 1, 2, false, false>(opA, opB, epi, M * Src::L, W::N, Src::COLS, 1, 0, 0);
     });
-    printf("conv2 dX 128x32x64: %.3f ms  %.1f TF\n", m4, fl / m4 / 1e9);
+    printf("conv2 dX 64x128x32: %.3f ms  %.1f TF\n", m4, fl / m4 / 1e9);
+    float m5 = timeit([&] {
+      launch_gemm<256, 128, 16, 4, 2, false, false>(opA, opB, epi, M * Src::L, W::N, Src::COLS, 1, 0, 0);
+    });
+    printf("conv2 dX 256x128x16: %.3f ms  %.1f TF\n", m5, fl / m5 / 1e9);
     CK(hipFree(w2));
     CK(hipFree(d1));
   }
