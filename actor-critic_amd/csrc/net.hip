@@ -642,7 +642,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     W opA{P + L.off[4]};
     RowsAsK<Src> opB{Src{bw->d3, B * Src::L}};
     EpiConvT<9, 9, 1, 64> epi{bw->d2, a->a2};
-    launch_gemm<64, 128, 32, 1, 2, false, false>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
+    launch_gemm<64, 128, 16, 1, 2, false, false>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
   }
   {  // conv2 -> d1 (stride 2: the four phases of a 2x2 super-pixel are the
      // 4 x 32 rows of one product over the 10x10 super-pixels)

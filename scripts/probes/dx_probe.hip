@@ -101,5 +101,35 @@ int main(int argc, char** argv) {
   ALL("mask", em)
   ALL("nomask", en)
   ALL("none", e0)
+  {  // conv3 (stride 1): I = 64 channels, J = 81 pixels per image, K = 9 taps x 32
+    using Src3 = ConvTRows<9, 9, 3, 3, 1, 32>;
+    using W3 = ConvTWeights<3, 3, 1, 64, 32>;
+    float *a2, *d2, *dy3, *w3;
+    CK(hipMalloc(&a2, (long long)M * 81 * 64 * 4));
+    CK(hipMalloc(&d2, (long long)M * 81 * 64 * 4));
+    CK(hipMalloc(&dy3, (long long)M * 49 * 32 * 4));
+    CK(hipMalloc(&w3, 9 * 64 * 32 * 4));
+    fill<<<4096, 256>>>(a2, (long long)M * 81 * 64, 4);
+    fill<<<4096, 256>>>(dy3, (long long)M * 49 * 32, 5);
+    fill<<<64, 256>>>(w3, 9 * 64 * 32, 6);
+    W3 oA{w3};
+    RowsAsK<Src3> oB{Src3{dy3, M * Src3::L}};
+    EpiConvT<9, 9, 1, 64> e3{d2, a2};
+    const int I3 = W3::N, J3 = M * Src3::L;
+    const double fl3 = 2.0 * I3 * J3 * Src3::COLS;
+#define RUN3(...)                                                                                \
+  {                                                                                               \
+    float ms = timeit([&] { launch_gemm<__VA_ARGS__, false, false>(oA, oB, e3, I3, J3, Src3::COLS, \
+                                                                   1, 0, 0); });                  \
+    printf("conv3 dX %-14s %.3f ms  %.1f TF\n", #__VA_ARGS__, ms, fl3 / ms / 1e9);                \
+  }
+    RUN3(64, 128, 32, 1, 2)
+    RUN3(64, 128, 32, 1, 2)
+    RUN3(64, 128, 16, 1, 2)
+    RUN3(64, 256, 16, 1, 4)
+    RUN3(64, 256, 32, 1, 4)
+    RUN3(64, 64, 32, 1, 1)
+    RUN3(64, 64, 16, 1, 1)
+  }
   return 0;
 }
