@@ -129,15 +129,28 @@ __device__ __forceinline__ void store_tile(const Epi& epi, const Acc& acc, int i
   }
 }
 
+// LDS bytes of one gemm_kernel block and the blocks one CU holds (160 KiB LDS,
+// 2048 threads)
+template <int BM, int BN, int BK, bool KA, bool KB>
+constexpr int gemm_lds_bytes() {
+  return 2 * BK * ((KA ? BM + 1 : BM + 4) + (KB ? BN + 1 : BN + 4)) * 4;
+}
+template <int BM, int BN, int BK, bool KA, bool KB>
+constexpr int gemm_blocks_per_cu() {
+  return std::min(8, 160 * 1024 / gemm_lds_bytes<BM, BN, BK, KA, KB>());
+}
+
 // DEPTH: K-tiles of staging loads in flight (register sets): 1 = the next
 // tile's loads overlap the current tile's MFMAs; 2 = two tiles ahead, for
 // latency-bound shapes (short per-tile MFMA work, L2-missing gathers).
 template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM,
           class OpA, class OpB, class Epi, int DEPTH = 1>
-// waves_per_eu(4): the 128x128x16 reduction tiles fit 4 blocks per CU in LDS;
-// without the hint the compiler parks the accumulators in AGPRs next to ~85
-// VGPRs and only 3 fit, so the planned rounds (plan_rounds) would not be resident
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+// split-K reductions: waves_per_eu = the blocks per CU the LDS allows (one wave
+// per SIMD each), which plan_rounds counts on: for the 128x128x16 tiles that
+// is 4, and without the hint the compiler parks the accumulators in AGPRs next
+// to ~85 VGPRs so only 3 fit.  Other launches keep the compiler's choice.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    SPLITK ? gemm_blocks_per_cu<BM, BN, BK, OpA::KCONTIG, OpB::KCONTIG>() : 1)))
 void gemm_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, int sym_cols) {
   using TL = Tile<BM, BN, BK, WTM, WTN>;
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
@@ -513,17 +526,6 @@ struct EpiPartial {
     part[((long long)z * (I + 1) + I) * J + j] = v;
   }
 };
-
-// LDS bytes of one gemm_kernel block and the blocks one CU holds (160 KiB LDS,
-// 2048 threads)
-template <int BM, int BN, int BK, bool KA, bool KB>
-constexpr int gemm_lds_bytes() {
-  return 2 * BK * ((KA ? BM + 1 : BM + 4) + (KB ? BN + 1 : BN + 4)) * 4;
-}
-template <int BM, int BN, int BK, bool KA, bool KB>
-constexpr int gemm_blocks_per_cu() {
-  return std::min(8, 160 * 1024 / gemm_lds_bytes<BM, BN, BK, KA, KB>());
-}
 
 // Split a reduction over `rows` into chunks for `live` tiles so the grid fills
 // whole rounds of `slots` resident blocks (a partly filled last round idles

@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include "gemm.hpp"
+#include "symred.hpp"
 
 namespace acmi {
 
@@ -482,6 +483,8 @@ constexpr int kCUs = 256;
 
 struct WgradPlan {
   int I, J, kp, cout_pad, nc, ch;
+  bool slabs;  // symred_kernel (slab groups) instead of 128x128 live tiles
+  SymPlan sp;
   long long floats;
 };
 
@@ -493,7 +496,11 @@ static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows) {
   // no homogeneous column: the A factor's last column (sum of P) is the
   // column-sum row's P part, by symmetry
   p.J = p.kp + p.cout_pad;
-  if (with_stats)
+  p.slabs = with_stats && sym_plan(K, p.cout_pad, &p.sp);  // (f32 patch sources only)
+  if (p.slabs)
+    plan_rounds(rows, p.sp.ngroups, kCUs * std::min(8, 160 * 1024 / symred_lds_bytes<16>()), &p.nc,
+                &p.ch);
+  else if (with_stats)
     plan_rounds(rows, live_tiles<128, 128>(p.I, p.J, K),
                 kCUs * gemm_blocks_per_cu<128, 128, 16, false, false>(), &p.nc, &p.ch);
   else
@@ -544,10 +551,16 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
                pl.floats, part_cap);
   EpiPartial epi{part, I, J};
   prof_begin(site, s);
-  if (with_stats)  // only the upper triangle of the symmetric [P]^T[P] block
-    launch_gemm<128, 128, 16, 2, 2, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s, K);
-  else
+  if constexpr (std::is_same<typename Src::elem_t, float>::value) {
+    if (pl.slabs)  // slab groups over the upper triangle of P^T P and the dY columns
+      launch_symred<16>(opB, epi, pl.sp, I, J, (int)rows, nc, ch, s);
+    else if (with_stats)  // 128x128 live tiles (fc4: K not a multiple of 64)
+      launch_gemm<128, 128, 16, 2, 2, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s, K);
+    else
+      launch_gemm<128, 32, 32, 1, 1, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s);
+  } else {  // u8 patches: weight gradient only
     launch_gemm<128, 32, 32, 1, 1, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s);
+  }
   prof_end(site, s);
   WgradDesc d{part, nc, I, J, kp, cout, gradA, nsplit, gradB, astat, (int)rows, wscale};
   const long long total = (long long)(K + 1) * cout + (astat ? (long long)(K + 1) * (K + 1) : 0);
