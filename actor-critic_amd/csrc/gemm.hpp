@@ -145,12 +145,14 @@ constexpr int gemm_blocks_per_cu() {
 // latency-bound shapes (short per-tile MFMA work, L2-missing gathers).
 template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM,
           class OpA, class OpB, class Epi, int DEPTH = 1>
-// split-K reductions: waves_per_eu = the blocks per CU the LDS allows (one wave
-// per SIMD each), which plan_rounds counts on: for the 128x128x16 tiles that
-// is 4, and without the hint the compiler parks the accumulators in AGPRs next
-// to ~85 VGPRs so only 3 fit.  Other launches keep the compiler's choice.
+// waves_per_eu = the blocks per CU the LDS allows (one wave per SIMD each),
+// which plan_rounds counts on for the split-K reductions: for the 128x128x16
+// tiles that is 4, and without the hint the compiler parks the accumulators in
+// AGPRs next to ~85 VGPRs so only 3 fit.  (The conv2 input gradient spills a
+// little at 4 and is still faster than at 3; shapes whose registers cannot
+// reach the LDS bound get the compiler's best, -Wno-pass-failed.)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    SPLITK ? gemm_blocks_per_cu<BM, BN, BK, OpA::KCONTIG, OpB::KCONTIG>() : 1)))
+    gemm_blocks_per_cu<BM, BN, BK, OpA::KCONTIG, OpB::KCONTIG>())))
 void gemm_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, int sym_cols) {
   using TL = Tile<BM, BN, BK, WTM, WTN>;
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;

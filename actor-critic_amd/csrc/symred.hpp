@@ -30,17 +30,20 @@ struct SymGroup {
   int8_t wa[4];     // per wave: staged slab of its rows (-1: idle)
   int8_t wb[4];     // per wave: staged slab of its columns
 };
-constexpr int kSymMaxGroups = 24;
+constexpr int kSymMaxGroups = 96;
 struct SymPlan {
   int ngroups;
   SymGroup g[kSymMaxGroups];
 };
 
-// K % 64 == 0 P columns (slabs 0..nb-1) and one dY slab (cout_pad <= 64) at
-// column K.  Returns false when the shape does not fit the scheme.
+// P columns 0..K-1 in slabs 0..nb-1 and one dY slab (cout_pad <= 64) at column
+// K.  When K % 64 != 0 (fc4: 1568) the last P slab runs into the first dY
+// columns: those products are also made by the (a, dY) sub-tiles from the same
+// inputs in the same order, so both write identical values, and its rows >= K
+// are never stored.  Returns false when the shape does not fit the scheme.
 inline bool sym_plan(int K, int cout_pad, SymPlan* p) {
-  if (K % 64 != 0 || cout_pad > 64 || cout_pad <= 0) return false;
-  const int nb = K / 64, np = nb / 2, dy = K;
+  if (cout_pad > 64 || cout_pad <= 0 || K <= 0) return false;
+  const int nb = (K + 63) / 64, np = nb / 2, dy = K;
   const bool odd = nb & 1;
   const int last = 64 * (nb - 1);
   int n = 0;

@@ -142,16 +142,16 @@ def main():
     mean = lambda xs: (sum(xs) / len(xs)) if xs else None
 
     # dominant kernel: conv2 weight gradient fused with the K-FAC A factor,
-    # [P;1]^T [P | dY | 1] over the M*81 conv2 output pixels, P = 4x4x32 patches.
+    # [P;1]^T [P | dY] over the M*81 conv2 output pixels, P = 4x4x32 patches.
     # Algorithmic FLOP per pixel = 2 * (unique outputs): the symmetric 513x513
     # A factor counted once (513*514/2) plus the 513x64 [dW;db] block
-    # (DESIGN.md "Roofline").  The kernel executes 14 128x128 tiles per pixel
-    # (2*14*128*128 FLOP), reported as executed_tflops.
+    # (DESIGN.md "Roofline").  The slab-grouped kernel (symred.hpp) executes 44
+    # 64x64 sub-tiles per pixel (2*44*64*64 FLOP), reported as executed_tflops.
     M = N * T
     rows = 81 * M
     if acktr:
         kern_flops = 2.0 * (513 * 514 / 2 + 513 * 64) * rows
-        exec_flops = 2.0 * 14 * 128 * 128 * rows
+        exec_flops = 2.0 * 44 * 64 * 64 * rows
         kern_name = 'conv2 wgrad + K-FAC A-factor reduction GEMM (f32 MFMA)'
     else:
         kern_flops = 2.0 * 513 * 64 * rows

@@ -1,0 +1,58 @@
+"""HBM traffic per launch of the bench's roofline kernel from scripts/pmc.sh's
+FETCH_SIZE and WRITE_SIZE passes (separate rocprofv3 runs), with the gfx950
+correction of MI355X_MICROARCH.md (FETCH_SIZE x2, WRITE_SIZE as reported; both
+in KB), written as the profiles/<round>/pmc_traffic.json that bench.py reads.
+
+  python scripts/pmc_traffic.py gpurun_out/pmc_bench3 profiles/r01/pmc_traffic.json
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+KERNEL = 'conv2 wgrad + K-FAC A-factor reduction GEMM (f32 MFMA)'
+MATCH = 'symred_kernel<16, acmi::CatRowsI<acmi::ConvRows<float, 20, 20, 32, 4, 4, 2>'
+WORKLOAD = 'Breakout ACKTR 512 envs/GPU x 20 steps'
+ALGO_INPUT_BYTES = 736624640  # a1 patches source + d2 read once (DESIGN.md Roofline)
+
+
+def per_dispatch(d, counter):
+    vals = collections.defaultdict(float)
+    for f in glob.glob(os.path.join(d, '*', '*_counter_collection.csv')):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row['Counter_Name'] == counter and MATCH in row['Kernel_Name']:
+                    vals[row['Dispatch_Id']] += float(row['Counter_Value'])
+    return list(vals.values())
+
+
+def main(d, out):
+    fetch = per_dispatch(d, 'FETCH_SIZE')
+    write = per_dispatch(d, 'WRITE_SIZE')
+    if not fetch or not write:
+        raise SystemExit('no FETCH_SIZE/WRITE_SIZE samples for ' + MATCH)
+    f_kb = sum(fetch) / len(fetch)
+    w_kb = sum(write) / len(write)
+    res = {
+        'kernel': KERNEL,
+        'kernel_symbol_match': MATCH,
+        'workload': WORKLOAD,
+        'launches_sampled': min(len(fetch), len(write)),
+        'fetch_size_kb_raw': f_kb,
+        'write_size_kb_raw': w_kb,
+        'correction': 'FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads, MI355X_MICROARCH.md '
+                      'HBM section); WRITE_SIZE as reported',
+        'hbm_bytes_per_launch': (2 * f_kb + w_kb) * 1024.0,
+        'algorithmic_input_bytes': ALGO_INPUT_BYTES,
+        'source': 'rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE, separate passes, '
+                  'bench.py --steps 5 --warmup 2',
+    }
+    with open(out, 'w') as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == '__main__':
+    main(sys.argv[1], sys.argv[2])
