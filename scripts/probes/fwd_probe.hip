@@ -3,8 +3,12 @@
 //     scripts/probes/fwd_probe.hip -o scripts/probes/fwd_probe
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
+#include <vector>
+#include <algorithm>
 
 #include "../../actor-critic_amd/csrc/gemm_stream.hpp"
+#include "../../actor-critic_amd/csrc/wsgemm.hpp"
 
 namespace acmi {
 void set_error(const char*, ...) {}
@@ -83,6 +87,36 @@ int main(int argc, char** argv) {
     printf("%-34s %7.1f us  %6.1f TF\n", name, us, (fl) / us / 1e6); \
   }
   printf("M=%d\n", M);
+  {  // correctness of the wave-split kernel against gemm_kernel (same epilogue)
+    auto cmp = [&](const char* name, float* out, long long n, auto ref, auto test) {
+      float* r;
+      CK(hipMalloc(&r, n * 4));
+      ref();
+      CK(hipMemcpy(r, out, n * 4, hipMemcpyDeviceToDevice));
+      CK(hipMemset(out, 0, n * 4));
+      test();
+      CK(hipDeviceSynchronize());
+      std::vector<float> h1(n), h2(n);
+      CK(hipMemcpy(h1.data(), r, n * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(h2.data(), out, n * 4, hipMemcpyDeviceToHost));
+      double md = 0, mx = 0;
+      for (long long i = 0; i < n; ++i) {
+        md = std::max(md, (double)std::fabs(h1[i] - h2[i]));
+        mx = std::max(mx, (double)std::fabs(h1[i]));
+      }
+      printf("check %-10s max|diff| %.3g (max|ref| %.3g)\n", name, md, mx);
+      CK(hipFree(r));
+    };
+    cmp("conv1", a1, (long long)M * 12800,
+        [&] { launch_gemm<128, 32, 32, 1, 1, false, false>(A1, B1, E1, M * 400, 32, 256, 1, 0, 0); },
+        [&] { launch_gemm_ws<2, 2, 1, 32>(A1, B1, E1, M * 400, 32, 256, 0); });
+    cmp("conv2", a2, (long long)M * 5184,
+        [&] { launch_gemm<64, 64, 32, 1, 1, false, false>(A2, B2, E2, M * 81, 64, 512, 1, 0, 0); },
+        [&] { launch_gemm_ws<1, 4, 2, 16>(A2, B2, E2, M * 81, 64, 512, 0); });
+    cmp("conv3", a3, (long long)M * 1568,
+        [&] { launch_gemm<128, 32, 32, 1, 1, false, false>(A3, B3, E3, M * 49, 32, 576, 1, 0, 0); },
+        [&] { launch_gemm_ws<1, 4, 1, 32>(A3, B3, E3, M * 49, 32, 576, 0); });
+  }
   RUN("conv1 256x32x32", f1, (launch_gemm<256, 32, 32, 2, 1, false, false>(A1, B1, E1, M * 400, 32, 256, 1, 0, 0)));
   RUN("conv1 128x32x32", f1, (launch_gemm<128, 32, 32, 1, 1, false, false>(A1, B1, E1, M * 400, 32, 256, 1, 0, 0)));
   RUN("conv1 128x32x32 depth2", f1, (launch_gemm<128, 32, 32, 1, 1, false, false, 2>(A1, B1, E1, M * 400, 32, 256, 1, 0, 0)));
@@ -98,6 +132,16 @@ int main(int argc, char** argv) {
   RUN("conv2 128x32x32", f2, (launch_gemm<128, 32, 32, 1, 1, false, false>(A2, B2, E2, M * 81, 64, 512, 1, 0, 0)));
   RUN("conv2 64x64x16", f2, (launch_gemm<64, 64, 16, 1, 1, false, false>(A2, B2, E2, M * 81, 64, 512, 1, 0, 0)));
   RUN("conv3 128x32x32", f3, (launch_gemm<128, 32, 32, 1, 1, false, false>(A3, B3, E3, M * 49, 32, 576, 1, 0, 0)));
+  RUN("conv1 ws 2x2 BK32", f1, (launch_gemm_ws<2, 2, 1, 32>(A1, B1, E1, M * 400, 32, 256, 0)));
+  RUN("conv1 ws 1x4 BK32", f1, (launch_gemm_ws<1, 4, 1, 32>(A1, B1, E1, M * 400, 32, 256, 0)));
+  RUN("conv1 ws 4x1 BK32", f1, (launch_gemm_ws<4, 1, 1, 32>(A1, B1, E1, M * 400, 32, 256, 0)));
+  RUN("conv2 ws 1x4 n64 BK32", f2, (launch_gemm_ws<1, 4, 2, 32>(A2, B2, E2, M * 81, 64, 512, 0)));
+  RUN("conv2 ws 1x4 n64 BK16", f2, (launch_gemm_ws<1, 4, 2, 16>(A2, B2, E2, M * 81, 64, 512, 0)));
+  RUN("conv2 ws 2x2 n64 BK32", f2, (launch_gemm_ws<2, 2, 2, 32>(A2, B2, E2, M * 81, 64, 512, 0)));
+  RUN("conv2 ws 1x4 n32 BK32", f2, (launch_gemm_ws<1, 4, 1, 32>(A2, B2, E2, M * 81, 64, 512, 0)));
+  RUN("conv3 ws 1x4 BK32", f3, (launch_gemm_ws<1, 4, 1, 32>(A3, B3, E3, M * 49, 32, 576, 0)));
+  RUN("conv3 ws 1x4 BK16", f3, (launch_gemm_ws<1, 4, 1, 16>(A3, B3, E3, M * 49, 32, 576, 0)));
+  RUN("conv3 ws 2x2 BK32", f3, (launch_gemm_ws<2, 2, 1, 32>(A3, B3, E3, M * 49, 32, 576, 0)));
   {
     // conv3 split-K into 3 (partials only; the reduce is a separate small kernel)
     EpiPartial P{part, M * 49, 32};
@@ -105,6 +149,47 @@ int main(int argc, char** argv) {
         (launch_gemm<128, 32, 32, 1, 1, true, false>(A3, B3, P, M * 49, 32, 576, 3, 192, 0)));
     RUN("conv3 128x32x32 splitK6 (no reduce)", f3,
         (launch_gemm<128, 32, 32, 1, 1, true, false>(A3, B3, P, M * 49, 32, 576, 6, 96, 0)));
+  }
+  {  // one full-batch chain vs two half-batch chains on two streams
+    hipStream_t s1, s2;
+    CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    const int H = M / 2;
+    auto chain = [&](int n, int off, hipStream_t st) {
+      RowsAsK<S1> a1_{S1{obs + (long long)off * 28224, 28224, n * 400}};
+      EpiBiasAct e1_{a1 + (long long)off * 12800, 32, b, 1};
+      launch_gemm<128, 32, 32, 1, 1, false, false>(a1_, B1, e1_, n * 400, 32, 256, 1, 0, st);
+      RowsAsK<S2> a2_{S2{a1 + (long long)off * 12800, 12800, n * 81}};
+      EpiBiasAct e2_{a2 + (long long)off * 5184, 64, b, 1};
+      launch_gemm<64, 64, 32, 1, 1, false, false>(a2_, B2, e2_, n * 81, 64, 512, 1, 0, st);
+      RowsAsK<S3> a3_{S3{a2 + (long long)off * 5184, 5184, n * 49}};
+      EpiBiasAct e3_{a3 + (long long)off * 1568, 32, b, 1};
+      launch_gemm<128, 32, 32, 1, 1, false, false>(a3_, B3, e3_, n * 49, 32, 576, 1, 0, st);
+    };
+    hipEvent_t ev0, ev1, j1, j2;
+    CK(hipEventCreate(&ev0)); CK(hipEventCreate(&ev1)); CK(hipEventCreate(&j1)); CK(hipEventCreate(&j2));
+    for (int pass = 0; pass < 2; ++pass) {
+      const int reps = 50;
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(ev0, s1));
+      for (int r = 0; r < reps; ++r) {
+        if (pass == 0) {
+          chain(M, 0, s1);
+        } else {
+          CK(hipEventRecord(j1, s1));
+          CK(hipStreamWaitEvent(s2, j1, 0));
+          chain(H, 0, s1);
+          chain(M - H, H, s2);
+          CK(hipEventRecord(j2, s2));
+          CK(hipStreamWaitEvent(s1, j2, 0));
+        }
+      }
+      CK(hipEventRecord(ev1, s1));
+      CK(hipEventSynchronize(ev1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, ev0, ev1));
+      printf("conv1-3 chain %s: %.1f us per forward\n", pass ? "2 streams x M/2" : "1 stream x M", ms / reps * 1e3f);
+    }
   }
   CK(hipGetLastError());
   return 0;
