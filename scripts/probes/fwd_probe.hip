@@ -8,7 +8,7 @@
 #include <algorithm>
 
 #include "../../actor-critic_amd/csrc/gemm_stream.hpp"
-#include "../../actor-critic_amd/csrc/wsgemm.hpp"
+#include "wsgemm.hpp"
 
 namespace acmi {
 void set_error(const char*, ...) {}

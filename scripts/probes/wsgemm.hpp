@@ -1,3 +1,4 @@
+// PROBE ONLY (not in libacmi): measured no faster than gemm_kernel at rollout batch.
 // Wave-split GEMM for the rollout-size forward convolutions (B = 512 images).
 //
 // At rollout batch the forward GEMMs are latency-bound, not MFMA-bound: conv3
@@ -17,7 +18,7 @@
 // OpA: KCONTIG row source (RowsAsK<ConvRows<..>>), OpB: MatI (B[k][n] row-major).
 #pragma once
 
-#include "gemm.hpp"
+#include "../../actor-critic_amd/csrc/gemm.hpp"
 
 namespace acmi {
 
