@@ -140,6 +140,55 @@ constexpr int gemm_blocks_per_cu() {
   return std::min(8, 160 * 1024 / gemm_lds_bytes<BM, BN, BK, KA, KB>());
 }
 
+// Epilogues with LDS_T take their float4 row runs (aux4/store4, as VEC4) after a
+// transpose through LDS: the C map gives a lane 4 consecutive rows of ONE column
+// (32 columns per instruction, 16-32 bytes each), so for an output whose rows
+// are contiguous in memory (EpiConvT: channels of a pixel) each access touches
+// 32 lines.  Through LDS ([col][row] per 32x32 block) 8 lanes cover 32 rows of
+// one column: one instruction moves 8 whole 128-byte runs.  The caller has
+// synchronised the block (the LDS staging buffers are free); each wave uses
+// its own 32x36-float region and reads back only what it wrote.
+template <class T, class = void>
+struct has_ldst : std::false_type {};
+template <class T>
+struct has_ldst<T, std::void_t<decltype(T::LDS_T)>> : std::integral_constant<bool, T::LDS_T> {};
+
+template <int WTM, int WTN, class Epi, class Acc>
+__device__ __forceinline__ void store_tile_lds(const Epi& epi, const Acc& acc, int ib, int jb,
+                                               int lane, float* wlds, int I, int J) {
+  constexpr int S = 36;  // [32 columns][32 rows + 4]
+  const int khalf = lane >> 5, c = lane & 31;
+  const int ri = 4 * (lane & 7), cj = lane >> 3;  // read-back map: rows ri..ri+3 of column cj+8p
+#pragma unroll
+  for (int tm = 0; tm < WTM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < WTN; ++tn) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(wlds + c * S + 8 * g + 4 * khalf) =
+            make_float4(acc[tm][tn][4 * g], acc[tm][tn][4 * g + 1], acc[tm][tn][4 * g + 2],
+                        acc[tm][tn][4 * g + 3]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float4 v[4], x[4];
+      const int i0 = ib + tm * 32 + ri;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        v[p] = *reinterpret_cast<const float4*>(wlds + (cj + 8 * p) * S + ri);
+        x[p] = epi.aux4(min(i0, I - 4), min(jb + tn * 32 + cj + 8 * p, J - 1));
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int j = jb + tn * 32 + cj + 8 * p;
+        if (i0 < I && j < J) epi.store4(i0, j, v[p], x[p]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 // DEPTH: K-tiles of staging loads in flight (register sets): 1 = the next
 // tile's loads overlap the current tile's MFMAs; 2 = two tiles ahead, for
 // latency-bound shapes (short per-tile MFMA work, L2-missing gathers).
@@ -425,7 +474,13 @@ void gemm_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, in
 
   // epilogue: acc[tm][tn][r] -> C[i][j],  j = lane&31 (+tile),
   // i = (r&3) + 8*(r>>2) + 4*(lane>>5) (+tile)   (gfx950 32x32 C/D map)
-  store_tile<WTM, WTN>(epi, acc, i0 + wm * WTM * 32, j0 + wn * WTN * 32, lane, I, J);
+  if constexpr (has_ldst<Epi>::value && 2 * (ABUF + BBUF) >= 4 * 32 * 36) {
+    __syncthreads();  // every wave is done with the staging buffers
+    store_tile_lds<WTM, WTN>(epi, acc, i0 + wm * WTM * 32, j0 + wn * WTN * 32, lane,
+                             lds + wave * 32 * 36, I, J);
+  } else {
+    store_tile<WTM, WTN>(epi, acc, i0 + wm * WTM * 32, j0 + wn * WTN * 32, lane, I, J);
+  }
   if constexpr (COLSUM) {
     if (bx == 0 && wm == 0) {
 #pragma unroll
@@ -481,11 +536,13 @@ struct EpiReluGrad {
 
 // input-gradient of a strided conv as the TRANSPOSED product: row i =
 // (ph, pw, ci) (all stride phases), column j = super-pixel (img, ih', iw') ->
-// NHWC pixel (S*ih'+ph, S*iw'+pw), channel ci; masked by ReLU'.  A lane's four
-// consecutive rows are four consecutive channels of one pixel (VEC4).
+// NHWC pixel (S*ih'+ph, S*iw'+pw), channel ci; masked by ReLU'.  Four
+// consecutive rows are four consecutive channels of one pixel (VEC4), written
+// after the LDS transpose (LDS_T) as whole 128-byte channel runs.
 template <int IH, int IW, int S, int CIN>
 struct EpiConvT {
   static constexpr bool VEC4 = true;
+  static constexpr bool LDS_T = true;
   static_assert(CIN % 4 == 0, "channel runs of 4");
   float* out;
   const float* act;
