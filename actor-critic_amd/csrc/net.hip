@@ -12,6 +12,7 @@
 
 #include "gemm.hpp"
 #include "symred.hpp"
+#include "conv1u8.hpp"
 
 namespace acmi {
 
@@ -215,17 +216,12 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // act_img_stride: images between consecutive batch rows in the activation
   // buffers (1 = contiguous; T = rollout step t of an env-major buffer).
   const long long st = act_img_stride;
-  {  // conv1: [B,84,84,4]u8 -> [B,20,20,32]
+  {  // conv1: [B,84,84,4]u8 -> [B,20,20,32]; the u8 patches stay bytes in LDS
     using Src = ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>;
-    RowsAsK<Src> opA{Src{obs, (uint32_t)img_stride, B * 400}};
-    MatI<true> opB{P + L.off[0], 32, 256, 32};
+    MatI<true> w{P + L.off[0], 32, 256, 32};
     EpiAct epi{a->a1, P + L.off[1], 32, 400, st * 400 * 32, 1.0f / 255.0f};
     prof_begin(ACMI_PROF_CONV1_FWD, s);
-    // rollout-size batches fill the chip better with 128-row tiles
-    if (B <= 2048)
-      launch_gemm<128, 32, 32, 1, 1, false, false>(opA, opB, epi, B * 400, 32, 256, 1, 0, s);
-    else
-      launch_gemm<256, 32, 32, 2, 1, false, false>(opA, opB, epi, B * 400, 32, 256, 1, 0, s);
+    launch_conv1_fwd_u8<32>(Src{obs, (uint32_t)img_stride, B * 400}, w, epi, B * 400, 256, s);
     prof_end(ACMI_PROF_CONV1_FWD, s);
   }
   {  // conv2: -> [B,9,9,64]

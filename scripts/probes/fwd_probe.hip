@@ -9,6 +9,7 @@
 
 #include "../../actor-critic_amd/csrc/gemm_stream.hpp"
 #include "wsgemm.hpp"
+#include "../../actor-critic_amd/csrc/conv1u8.hpp"
 
 namespace acmi {
 void set_error(const char*, ...) {}
@@ -110,6 +111,9 @@ int main(int argc, char** argv) {
     cmp("conv1", a1, (long long)M * 12800,
         [&] { launch_gemm<128, 32, 32, 1, 1, false, false>(A1, B1, E1, M * 400, 32, 256, 1, 0, 0); },
         [&] { launch_gemm_ws<2, 2, 1, 32>(A1, B1, E1, M * 400, 32, 256, 0); });
+    cmp("conv1 u8img", a1, (long long)M * 12800,
+        [&] { launch_gemm<128, 32, 32, 1, 1, false, false>(A1, B1, E1, M * 400, 32, 256, 1, 0, 0); },
+        [&] { launch_conv1_fwd_u8<32>(S1{obs, 28224, M * 400}, B1, E1, M * 400, 256, 0); });
     cmp("conv2", a2, (long long)M * 5184,
         [&] { launch_gemm<64, 64, 32, 1, 1, false, false>(A2, B2, E2, M * 81, 64, 512, 1, 0, 0); },
         [&] { launch_gemm_ws<1, 4, 2, 16>(A2, B2, E2, M * 81, 64, 512, 0); });
@@ -132,6 +136,9 @@ int main(int argc, char** argv) {
   RUN("conv2 128x32x32", f2, (launch_gemm<128, 32, 32, 1, 1, false, false>(A2, B2, E2, M * 81, 64, 512, 1, 0, 0)));
   RUN("conv2 64x64x16", f2, (launch_gemm<64, 64, 16, 1, 1, false, false>(A2, B2, E2, M * 81, 64, 512, 1, 0, 0)));
   RUN("conv3 128x32x32", f3, (launch_gemm<128, 32, 32, 1, 1, false, false>(A3, B3, E3, M * 49, 32, 576, 1, 0, 0)));
+  RUN("conv1 u8 image BK32", f1, (launch_conv1_fwd_u8<32>(S1{obs, 28224, M * 400}, B1, E1, M * 400, 256, 0)));
+  RUN("conv1 u8 image BK64", f1, (launch_conv1_fwd_u8<64>(S1{obs, 28224, M * 400}, B1, E1, M * 400, 256, 0)));
+  RUN("conv1 u8 image BK16", f1, (launch_conv1_fwd_u8<16>(S1{obs, 28224, M * 400}, B1, E1, M * 400, 256, 0)));
   RUN("conv1 ws 2x2 BK32", f1, (launch_gemm_ws<2, 2, 1, 32>(A1, B1, E1, M * 400, 32, 256, 0)));
   RUN("conv1 ws 1x4 BK32", f1, (launch_gemm_ws<1, 4, 1, 32>(A1, B1, E1, M * 400, 32, 256, 0)));
   RUN("conv1 ws 4x1 BK32", f1, (launch_gemm_ws<4, 1, 1, 32>(A1, B1, E1, M * 400, 32, 256, 0)));
