@@ -175,9 +175,12 @@ void symred_kernel(Op op, Epi epi, SymPlan plan, int I, int J, int K, int k_chun
   }
   __syncthreads();
 
-  auto step = [&](int kt, int cur, auto MF, auto CS) {
+  // NT: column blocks of 32 the wave multiplies (1 when its second half lies
+  // past J: a dY slab of cout_pad <= 32, e.g. conv3's 32 filters)
+  auto step = [&](int kt, int cur, auto MF, auto CS, auto NTc) {
     constexpr bool mf = decltype(MF)::value;
     constexpr bool cs = decltype(CS)::value;
+    constexpr int NT = decltype(NTc)::value;
     fetch(kbeg + (kt + 1) * BK);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (mf) {
@@ -199,13 +202,13 @@ void symred_kernel(Op op, Epi epi, SymPlan plan, int I, int J, int K, int k_chun
           }
         }
         if constexpr (cs) {
-          csum[0] += bb[0];
-          csum[1] += bb[1];
+#pragma unroll
+          for (int tn = 0; tn < NT; ++tn) csum[tn] += bb[tn];
         }
 #pragma unroll
         for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
-          for (int tn = 0; tn < 2; ++tn)
+          for (int tn = 0; tn < NT; ++tn)
             acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[tm], bb[tn], acc[tm][tn], 0, 0, 0);
         if (kk + 2 < BK) {
 #pragma unroll
@@ -222,13 +225,23 @@ void symred_kernel(Op op, Epi epi, SymPlan plan, int I, int J, int K, int k_chun
   };
   using T = std::integral_constant<bool, true>;
   using F = std::integral_constant<bool, false>;
-  // three uniform loop variants: MFMAs + column sums, MFMAs only, staging only
-  if (do_cs) {
-    for (int kt = 0; kt < nk; ++kt) step(kt, kt & 1, T{}, T{});
-  } else if (!idle) {
-    for (int kt = 0; kt < nk; ++kt) step(kt, kt & 1, T{}, F{});
+  using N2 = std::integral_constant<int, 2>;
+  using N1 = std::integral_constant<int, 1>;
+  const bool half = jb + 32 >= J;
+  // wave-uniform loop variants: MFMAs (+ column sums) on 64 or 32 columns, or
+  // staging only
+  if (idle) {
+    for (int kt = 0; kt < nk; ++kt) step(kt, kt & 1, F{}, F{}, N2{});
+  } else if (do_cs) {
+    if (half)
+      for (int kt = 0; kt < nk; ++kt) step(kt, kt & 1, T{}, T{}, N1{});
+    else
+      for (int kt = 0; kt < nk; ++kt) step(kt, kt & 1, T{}, T{}, N2{});
   } else {
-    for (int kt = 0; kt < nk; ++kt) step(kt, kt & 1, F{}, F{});
+    if (half)
+      for (int kt = 0; kt < nk; ++kt) step(kt, kt & 1, T{}, F{}, N1{});
+    else
+      for (int kt = 0; kt < nk; ++kt) step(kt, kt & 1, T{}, F{}, N2{});
   }
   if (idle) return;
 
