@@ -86,22 +86,29 @@ __global__ __launch_bounds__(256) void conv1_afactor_i8_kernel(const uint8_t* ob
   const int coffB = col_off(tb);
 
   // raw patch bytes; the XOR (x = u ^ 0x80) is applied at commit, after the
-  // MFMAs, so nothing waits on the loads at fetch time
+  // MFMAs, so nothing waits on the loads at fetch time.  A thread's 4 rows
+  // r .. r+3 (r % 4 == 0: chunks are multiples of 64 rows, every r_end a
+  // multiple of 400) are 4 consecutive output columns of ONE output row, i.e.
+  // the same patch 16 bytes further on: one row decode per stage, one validity
+  // test (the rows are all valid or all past r_end), 32-bit offsets (the host
+  // checks the frames span < 2^32 bytes).
   uint2 ra[4], rb[4];
   const uint8_t* x0 = reinterpret_cast<const uint8_t*>(kX0Run);
+  const uint32_t istride = (uint32_t)img_stride;
   auto fetch = [&](int r0) {
+    const int r = r0 + 4 * q4;
+    const bool ok = r < r_end;
+    const uint32_t rr = ok ? (uint32_t)r : (uint32_t)r_begin;
+    const uint32_t img = rr / 400u;
+    const uint32_t p = rr - img * 400u;
+    const uint32_t oh = p / 20u;
+    const uint32_t ow = p - oh * 20u;
+    const uint32_t off = img * istride + (oh * 4 * AF_OBS_W + ow * 4) * 4;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int r = r0 + 4 * q4 + q;
-      const bool ok = r < r_end;
-      const uint32_t rr = ok ? (uint32_t)r : (uint32_t)r_begin;
-      const uint32_t img = rr / 400u;
-      const uint32_t p = rr - img * 400u;
-      const uint32_t oh = p / 20u;
-      const uint32_t ow = p - oh * 20u;
-      const uint8_t* base = obs + (long long)img * img_stride + (oh * 4 * AF_OBS_W + ow * 4) * 4;
-      ra[q] = *reinterpret_cast<const uint2*>(ok ? base + coffA : x0);
-      if (!diag) rb[q] = *reinterpret_cast<const uint2*>(ok ? base + coffB : x0);
+      ra[q] = *reinterpret_cast<const uint2*>(ok ? obs + (off + (uint32_t)(coffA + 16 * q)) : x0);
+      if (!diag)
+        rb[q] = *reinterpret_cast<const uint2*>(ok ? obs + (off + (uint32_t)(coffB + 16 * q)) : x0);
     }
   };
   // 4 rows x 4 bytes -> 4 column words of 4 consecutive rows (v_perm_b32)
@@ -260,6 +267,8 @@ int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* ast
   ACMI_REQUIRE(conv1_afactor_ws_ints(rows) <= ws_ints, ACMI_ERR_WS,
                "conv1 A-factor workspace too small");
   ACMI_REQUIRE(img_stride % 8 == 0, ACMI_ERR_ARG, "conv1 A factor needs 8-byte aligned images");
+  ACMI_REQUIRE(img_stride > 0 && (long long)B * img_stride < (1LL << 32), ACMI_ERR_ARG,
+               "conv1 A factor: frames must span < 2^32 bytes");
   int* part = ws;
   int* colsum = ws + (long long)nchunk * 65536;
   hipLaunchKernelGGL(conv1_afactor_i8_kernel, dim3(3 * nchunk), dim3(256), 0, s, obs, img_stride,
