@@ -484,7 +484,7 @@ struct WgradPlan {
   long long floats;
 };
 
-static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows) {
+static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows, bool u8 = false) {
   WgradPlan p;
   p.cout_pad = roundup4(cout);
   p.kp = with_stats ? K : 0;
@@ -493,7 +493,9 @@ static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows) {
   // column-sum row's P part, by symmetry
   p.J = p.kp + p.cout_pad;
   p.slabs = with_stats && sym_plan(K, p.cout_pad, &p.sp);  // (f32 patch sources only)
-  if (p.slabs)
+  if (u8)  // conv1 weight gradient: conv1_wgrad_u8_kernel, one 256x32 block per chunk
+    conv1_wgrad_u8_plan(rows, &p.nc, &p.ch);
+  else if (p.slabs)
     plan_rounds(rows, p.sp.ngroups, kCUs * std::min(8, 160 * 1024 / symred_lds_bytes<16>()), &p.nc,
                 &p.ch);
   else if (with_stats)
@@ -537,7 +539,8 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
                        long long part_cap, float* gradA, int nsplit,
                        float* gradB, float* astat, hipStream_t s, int site = 0,
                        float wscale = 1.f) {
-  const WgradPlan pl = wgrad_plan(K, cout, with_stats, rows);
+  constexpr bool kU8 = !std::is_same<typename Src::elem_t, float>::value;
+  const WgradPlan pl = wgrad_plan(K, cout, with_stats, rows, kU8);
   const int I = pl.I, J = pl.J, kp = pl.kp, nc = pl.nc, ch = pl.ch;
   RowsAsI<Src> opA{src};
   CatRowsI<Src> opB{src, kp, dy, ldy, cout, pl.cout_pad, (int)rows};
@@ -554,8 +557,9 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
       launch_gemm<128, 128, 16, 2, 2, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s, K);
     else
       launch_gemm<128, 32, 32, 1, 1, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s);
-  } else {  // u8 patches: weight gradient only
-    launch_gemm<128, 32, 32, 1, 1, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s);
+  } else {  // u8 patches (conv1): weight gradient only, bytes in LDS
+    ACMI_REQUIRE(K == 256 && cout == 32 && ldy == 32, ACMI_ERR_ARG, "conv1 weight gradient shape");
+    launch_conv1_wgrad_u8(src, dy, (int)rows, nc, ch, epi, s);
   }
   prof_end(site, s);
   WgradDesc d{part, nc, I, J, kp, cout, gradA, nsplit, gradB, astat, (int)rows, wscale};
@@ -610,7 +614,7 @@ static long long bwd_partial_cap(int B, int A, int C3) {
   const int co[5] = {32, 64, C3, 512, A + 1};
   for (int l = 0; l < 5; ++l) {
     m = std::max(m, wgrad_plan(Ks[l], co[l], true, rowsL[l]).floats);
-    m = std::max(m, wgrad_plan(Ks[l], co[l], false, rowsL[l]).floats);
+    m = std::max(m, wgrad_plan(Ks[l], co[l], false, rowsL[l], l == 0).floats);
     // G factors of the same layer's output
     if (co[l] <= 64) {
       int nc;
