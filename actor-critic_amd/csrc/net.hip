@@ -10,6 +10,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <vector>
+
 #include "gemm.hpp"
 #include "symred.hpp"
 #include "conv1u8.hpp"
@@ -947,6 +949,43 @@ int acmi_prof_collect(double* total_ms, int* count) {
   *count = g_prof_n;
   g_prof_n = 0;
   return ACMI_OK;
+}
+
+// Host-only check of the launch planners (no GPU): every sub-tile of the
+// upper triangle of P^T P and every (P, dY) sub-tile is produced by sym_plan's
+// groups, each column's sum by exactly one wave, for K = 64..max_k; and
+// plan_rounds' chunks cover the rows exactly.  0 = ok, else the failing K.
+int acmi_selftest_plans(int max_k) {
+  for (int K = 64; K <= max_k; K += 32) {
+    SymPlan p;
+    if (!sym_plan(K, 64, &p)) continue;  // shape falls back to the 128x128 tiles
+    const int J = K + 64;
+    std::vector<unsigned char> cov((size_t)K * J, 0);
+    std::vector<int> cs(J, 0);
+    for (int g = 0; g < p.ngroups; ++g)
+      for (int w = 0; w < 4; ++w) {
+        if (p.g[g].wa[w] < 0) continue;
+        const int a = p.g[g].base[p.g[g].wa[w]], b = p.g[g].base[p.g[g].wb[w]];
+        if (a < 0 || b < 0 || a >= K) return K;
+        for (int i = a; i < a + 64 && i < K; ++i)
+          for (int j = b; j < b + 64 && j < J; ++j) cov[(size_t)i * J + j] = 1;
+        if (a == 0)
+          for (int j = b; j < b + 64 && j < J; ++j) cs[j]++;
+      }
+    for (int i = 0; i < K; ++i)
+      for (int j = i; j < J; ++j)
+        if (!cov[(size_t)i * J + j]) return K;
+    for (int j = 0; j < J; ++j)
+      if (cs[j] < 1) return K;
+  }
+  for (long long rows : {1000LL, 4096000LL, 829440LL, 501760LL, 10240LL}) {
+    for (int live : {1, 3, 11, 14, 90}) {
+      int nc, ch;
+      plan_rounds(rows, live, 1024, &nc, &ch);
+      if (ch % 32 != 0 || (long long)nc * ch < rows || (long long)(nc - 1) * ch >= rows) return -1;
+    }
+  }
+  return 0;
 }
 
 int acmi_gemm_f32(const float* A, const float* B, float* C, int M, int N, int K,

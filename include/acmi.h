@@ -295,6 +295,12 @@ int acmi_forward_strided(const acmi_net_t* net, const uint8_t* obs,
  * Building blocks exposed for parity tests and the bench (not needed by a
  * reference-shaped caller).
  * ---------------------------------------------------------------------- */
+/* Host-only self-check of the GEMM launch planners (no GPU needed): the
+ * slab groups of the fused wgrad/A-factor reduction cover every needed
+ * sub-tile and column sum for K = 64..max_k, split-K chunks cover the rows.
+ * Returns 0, or the first failing K (-1: chunk plan). */
+int acmi_selftest_plans(int max_k);
+
 /* C[M][N] = A[M][K] @ B[K][N], row-major fp32, f32-input MFMA */
 int acmi_gemm_f32(const float* A, const float* B, float* C, int M, int N,
                   int K, acmi_stream_t stream);

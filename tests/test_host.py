@@ -31,6 +31,12 @@ def test_library_exports_every_declared_symbol(lib):
     assert lib.acmi_abi_version() == 1
 
 
+def test_gemm_launch_plans_cover_every_tile(lib):
+    # host-only planner check inside libacmi: slab groups of the fused
+    # wgrad/A-factor reduction (symred.hpp) and split-K chunking
+    assert lib.acmi_selftest_plans(2048) == 0
+
+
 def test_layout_counts_match_survey(lib):
     # 865,413 params ACKTR / 1,686,693 A2C; 3,655,382 factor floats
     assert lib.acmi_param_count(4, 32) == 865413
