@@ -213,6 +213,28 @@ class NetEngine(object):
             k = st.red.numel() if with_stats else st.n_grad_red
             parallel.allreduce_sum_(st.red[:k])
 
+    def allreduce_begin(self, st, with_stats):
+        """Starts summing what acmi_backward produced -- [grads | losses (| A factor
+        stats)], a prefix of ``red`` -- over ranks without waiting: RCCL runs it on its
+        own stream while the sampled-loss backward (acmi_kfac_output_stats, which writes
+        only the G part) computes on this one.  Returns the pending handle (None on one
+        rank); allreduce_end completes the buffer."""
+        if self.world_size <= 1:
+            return None
+        from actorcritic import parallel
+        k = st.n_grad_red + (self.layout.stat_off[5] if with_stats else 0)
+        return parallel.allreduce_sum_async(st.red[:k])
+
+    def allreduce_end(self, st, with_stats, pending):
+        """Sums the G factor stats (if any) and makes this stream wait for the pending
+        prefix sum, so ``red`` is fully reduced for the kernels enqueued next."""
+        if self.world_size <= 1:
+            return
+        from actorcritic import parallel
+        if with_stats:
+            parallel.allreduce_sum_(st.red[st.n_grad_red + self.layout.stat_off[5]:])
+        pending.wait()
+
     # -- plumbing ------------------------------------------------------------
     def net(self):
         return _lib.Net(self.A, self.C3, self.params.data_ptr())

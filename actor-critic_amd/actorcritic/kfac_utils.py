@@ -144,8 +144,9 @@ class KfacOptimizer(Optimizer):
         lr = self._lr(ctx)
         gs = global_step.value if global_step is not None else self.cov_updates
         eng.backward(st.fwd, st, with_stats=True)
+        pending = eng.allreduce_begin(st, with_stats=True)  # overlaps the G statistics
         self._stats(eng, st.fwd, st, gs)
-        eng.allreduce(st, with_stats=True)
+        eng.allreduce_end(st, True, pending)
         self._cov_update(eng, st)
         self._inv_update(eng)
         self._kfac_apply(eng, st.grads, lr)
@@ -195,9 +196,10 @@ class ColdStartPeriodicInvUpdateKfacOpt(KfacOptimizer):
         cold, cov, inv, gs_after = schedule(global_step.value, self._num_cold_updates, self._invert_every)
         self.last_flags = (cold, cov, inv)
         eng.backward(st.fwd, st, with_stats=cov)
+        pending = eng.allreduce_begin(st, with_stats=cov)  # overlaps the G statistics
         if cov:
             self._stats(eng, st.fwd, st, global_step.value)
-        eng.allreduce(st, with_stats=cov)
+        eng.allreduce_end(st, cov, pending)
         if cold:
             self._cold_optimizer._apply_dense(ctx, eng, st.grads, 0.0)
         else:

@@ -53,6 +53,12 @@ def allreduce_sum_(t):
     return t
 
 
+def allreduce_sum_async(t):
+    """Starts an in-place SUM all-reduce; the returned work's wait() makes the current
+    stream wait for it (RCCL/NCCL runs collectives on its own stream)."""
+    return dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
+
+
 def broadcast_(t, src=0):
     if world_size() > 1:
         dist.broadcast(t, src)

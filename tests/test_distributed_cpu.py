@@ -46,7 +46,15 @@ def _worker(rank, world, port, out_dir):
                                with_a_factors=True)
     stats = np.concatenate([f.ravel() for f in af])
     red = torch.from_numpy(np.concatenate([g, [1.0, 2.0, 3.0, 0.0], stats]))
+    # the split path of a K-FAC update (engine.allreduce_begin/_end): the prefix
+    # [grads | losses | A stats] asynchronously, the G tail synchronously, then wait
+    red2 = red.clone()
+    split = g.size + 4 + stats.size // 2
+    pending = parallel.allreduce_sum_async(red2[:split])
+    parallel.allreduce_sum_(red2[split:])
+    pending.wait()
     parallel.allreduce_sum_(red)
+    assert torch.equal(red, red2)
     n = g.size
     grads = red[:n].numpy()
     stats_mean = red[n + 4:].numpy() / world
