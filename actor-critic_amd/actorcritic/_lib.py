@@ -48,6 +48,8 @@ class EnvState(ctypes.Structure):
 _SIGS = {
     'acmi_last_error': (ctypes.c_char_p, []),
     'acmi_abi_version': (c_int, []),
+    'acmi_set_gemm_mode': (c_int, [c_int]),
+    'acmi_get_gemm_mode': (c_int, []),
     'acmi_param_count': (c_i64, [c_int, c_int]),
     'acmi_param_offsets': (c_int, [c_int, c_int, ctypes.POINTER(c_i64)]),
     'acmi_kfac_layout': (c_int, [c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
@@ -90,6 +92,9 @@ _SIGS = {
     'acmi_prof_enable': (c_int, [c_int, c_int]),
     'acmi_prof_collect': (c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int)]),
 }
+
+GEMM_F32 = 0  # acmi_set_gemm_mode: v_mfma_f32_32x32x2_f32
+GEMM_X3 = 1   # bf16x3 split operands on the bf16 matrix cores (default)
 
 PROF_CONV1_WGRAD = 1
 PROF_CONV2_WGRAD = 2

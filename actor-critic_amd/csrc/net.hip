@@ -6,6 +6,7 @@
 // baselines.py:55-69 (predictive distributions), objectives.py:78 (the
 // tf.gradients of the shared loss).  See include/acmi.h for the contract.
 #include <math.h>
+#include <stdlib.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -13,7 +14,7 @@
 #include <vector>
 
 #include "gemm.hpp"
-#include "symred.hpp"
+#include "symred3.hpp"
 #include "conv1u8.hpp"
 
 namespace acmi {
@@ -479,6 +480,15 @@ __global__ __launch_bounds__(256) void gram_small_kernel(const float* D, int ld,
 // MI355X has 256 CUs; blocks per CU follow from each config's LDS image
 constexpr int kCUs = 256;
 
+// Arithmetic of the slab-grouped wgrad + A-factor reductions (acmi_set_gemm_mode):
+// ACMI_GEMM_X3 = bf16x3 split operands on the bf16 matrix cores (symred3.hpp,
+// f32-accurate), ACMI_GEMM_F32 = v_mfma_f32_32x32x2_f32 (symred.hpp).  Initial
+// value from the environment variable ACMI_GEMM ("f32" or "x3"), default x3.
+static int g_gemm_mode = [] {
+  const char* e = getenv("ACMI_GEMM");
+  return (e && e[0] == 'f') ? ACMI_GEMM_F32 : ACMI_GEMM_X3;
+}();
+
 struct WgradPlan {
   int I, J, kp, cout_pad, nc, ch;
   bool slabs;  // symred_kernel (slab groups) instead of 128x128 live tiles
@@ -486,7 +496,8 @@ struct WgradPlan {
   long long floats;
 };
 
-static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows, bool u8 = false) {
+static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows, bool u8 = false,
+                            int mode = g_gemm_mode) {
   WgradPlan p;
   p.cout_pad = roundup4(cout);
   p.kp = with_stats ? K : 0;
@@ -497,6 +508,9 @@ static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows, bo
   p.slabs = with_stats && sym_plan(K, p.cout_pad, &p.sp);  // (f32 patch sources only)
   if (u8)  // conv1 weight gradient: conv1_wgrad_u8_kernel, one 256x32 block per chunk
     conv1_wgrad_u8_plan(rows, &p.nc, &p.ch);
+  else if (p.slabs && mode == ACMI_GEMM_X3)
+    plan_rounds(rows, p.sp.ngroups, kCUs * std::min(8, 160 * 1024 / symred3_lds_bytes()), &p.nc,
+                &p.ch);
   else if (p.slabs)
     plan_rounds(rows, p.sp.ngroups, kCUs * std::min(8, 160 * 1024 / symred_lds_bytes<16>()), &p.nc,
                 &p.ch);
@@ -542,7 +556,8 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
                        float* gradB, float* astat, hipStream_t s, int site = 0,
                        float wscale = 1.f) {
   constexpr bool kU8 = !std::is_same<typename Src::elem_t, float>::value;
-  const WgradPlan pl = wgrad_plan(K, cout, with_stats, rows, kU8);
+  const int mode = g_gemm_mode;
+  const WgradPlan pl = wgrad_plan(K, cout, with_stats, rows, kU8, mode);
   const int I = pl.I, J = pl.J, kp = pl.kp, nc = pl.nc, ch = pl.ch;
   RowsAsI<Src> opA{src};
   CatRowsI<Src> opB{src, kp, dy, ldy, cout, pl.cout_pad, (int)rows};
@@ -553,7 +568,9 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
   EpiPartial epi{part, I, J};
   prof_begin(site, s);
   if constexpr (std::is_same<typename Src::elem_t, float>::value) {
-    if (pl.slabs)  // slab groups over the upper triangle of P^T P and the dY columns
+    if (pl.slabs && mode == ACMI_GEMM_X3)  // slab groups, bf16x3 split operands
+      launch_symred3(opB, epi, pl.sp, I, J, (int)rows, nc, ch, s);
+    else if (pl.slabs)  // slab groups over the upper triangle of P^T P and the dY columns
       launch_symred<16>(opB, epi, pl.sp, I, J, (int)rows, nc, ch, s);
     else if (with_stats)  // 128x128 live tiles (fc4: K not a multiple of 64)
       launch_gemm<128, 128, 16, 2, 2, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s, K);
@@ -615,7 +632,8 @@ static long long bwd_partial_cap(int B, int A, int C3) {
   const int Ks[5] = {256, 512, 576, 49 * C3, 512};
   const int co[5] = {32, 64, C3, 512, A + 1};
   for (int l = 0; l < 5; ++l) {
-    m = std::max(m, wgrad_plan(Ks[l], co[l], true, rowsL[l]).floats);
+    for (int mode : {ACMI_GEMM_F32, ACMI_GEMM_X3})
+      m = std::max(m, wgrad_plan(Ks[l], co[l], true, rowsL[l], false, mode).floats);
     m = std::max(m, wgrad_plan(Ks[l], co[l], false, rowsL[l], l == 0).floats);
     // G factors of the same layer's output
     if (co[l] <= 64) {
@@ -785,6 +803,14 @@ extern "C" {
 
 const char* acmi_last_error(void) { return g_err; }
 int acmi_abi_version(void) { return ACMI_ABI_VERSION; }
+
+int acmi_set_gemm_mode(int mode) {
+  ACMI_REQUIRE(mode == ACMI_GEMM_F32 || mode == ACMI_GEMM_X3, ACMI_ERR_ARG,
+               "acmi_set_gemm_mode: unknown mode %d", mode);
+  g_gemm_mode = mode;
+  return ACMI_OK;
+}
+int acmi_get_gemm_mode(void) { return g_gemm_mode; }
 
 int64_t acmi_param_count(int A, int C3) {
   Layout L;

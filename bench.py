@@ -29,6 +29,10 @@ for _p in (os.path.join(ROOT, 'actor-critic_amd'), ROOT):
 import torch  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32-input MFMA peak
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA: 256 CUs x 4 SIMDs x 1024 FLOP/clk x 2.4 GHz
+# bf16x3 split operands: six bf16 MFMAs per f32-accurate product tile, so the
+# f32-equivalent ceiling of that arithmetic is the bf16 peak / 6
+X3_F32EQ_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
 HBM_PEAK_GBS = 8000.0
 
 
@@ -149,22 +153,32 @@ def main():
     # 64x64 sub-tiles per pixel (2*44*64*64 FLOP), reported as executed_tflops.
     M = N * T
     rows = 81 * M
+    x3 = acktr and _lib.load().acmi_get_gemm_mode() == _lib.GEMM_X3
     if acktr:
         kern_flops = 2.0 * (513 * 514 / 2 + 513 * 64) * rows
         exec_flops = 2.0 * 44 * 64 * 64 * rows
-        kern_name = 'conv2 wgrad + K-FAC A-factor reduction GEMM (f32 MFMA)'
+        kern_name = ('conv2 wgrad + K-FAC A-factor reduction GEMM (bf16x3 split-operand MFMA, f32-accurate)'
+                     if x3 else 'conv2 wgrad + K-FAC A-factor reduction GEMM (f32 MFMA)')
     else:
         kern_flops = 2.0 * 513 * 64 * rows
         exec_flops = 2.0 * 8 * 128 * 32 * rows
         kern_name = 'conv2 wgrad reduction GEMM (f32 MFMA)'
+    peak = X3_F32EQ_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
     kern_ms = tot_ms.value / max(1, cnt.value)
     achieved = kern_flops / (kern_ms * 1e-3) / 1e12 if cnt.value else None
+    executed = exec_flops / (kern_ms * 1e-3) / 1e12 if cnt.value else None
     traffic = measured_traffic(kern_name, 'Breakout {} {} envs/GPU x {} steps'.format(args.algo.upper(), N, T))
     roofline = {'bound': 'mfma', 'kernel': kern_name,
-                'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                'frac': (achieved / FP32_MFMA_PEAK_TFLOPS) if achieved else None, 'traffic': traffic,
+                'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
+                'frac': (achieved / peak) if achieved else None, 'traffic': traffic,
                 'launches': cnt.value, 'avg_ms': kern_ms, 'flops_per_launch': kern_flops,
-                'executed_tflops': exec_flops / (kern_ms * 1e-3) / 1e12 if cnt.value else None}
+                'executed_tflops': executed}
+    if x3 and achieved:
+        # peak = bf16 dense peak / 6 (f32-equivalent); the same rate against the
+        # f32-input MFMA peak, and the bf16 MFMA work actually issued
+        roofline['frac_of_f32_mfma_peak'] = achieved / FP32_MFMA_PEAK_TFLOPS
+        roofline['executed_bf16_tflops'] = 6 * executed
+        roofline['executed_frac_of_bf16_peak'] = 6 * executed / BF16_MFMA_PEAK_TFLOPS
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

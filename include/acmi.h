@@ -36,6 +36,18 @@ typedef void* acmi_stream_t; /* hipStream_t */
 const char* acmi_last_error(void);
 int acmi_abi_version(void);
 
+/* Arithmetic of the fused weight-gradient + K-FAC A-factor reductions (conv2,
+ * conv3, heads; the dominant K-FAC covariance work, kfac cov_update_thunks,
+ * actorcritic/kfac_utils.py:39,44).  Both modes are fp32-accurate:
+ *   ACMI_GEMM_X3  bf16x3 split operands on the bf16 matrix cores (default)
+ *   ACMI_GEMM_F32 v_mfma_f32_32x32x2_f32
+ * Initial mode from the environment variable ACMI_GEMM ("x3" / "f32").
+ * Not stream-ordered: set it between launches. */
+#define ACMI_GEMM_F32 0
+#define ACMI_GEMM_X3 1
+int acmi_set_gemm_mode(int mode);
+int acmi_get_gemm_mode(void);
+
 /* ------------------------------------------------------------------------
  * Model layout.  Replaces AtariModel._build_params
  * (actorcritic/envs/atari/model.py:129-170, nn.py:8-84).

@@ -107,10 +107,13 @@ def test_forward_matches_torch(lib, cuda, A, C3, B):
         assert rel < 1e-5, (name, rel)
 
 
-def test_backward_and_astats_match_torch(lib, cuda):
-    A, C3, B = 4, 32, 6
-    params = rand_params(A, C3, cuda, seed=3)
-    g = torch.Generator().manual_seed(4)
+def _backward_errors(lib, cuda, B=6, seed=3):
+    """max relative errors of acmi_backward's parameter gradients and A factors
+    against float64 autograd / patch products"""
+    errs = {}
+    A, C3 = 4, 32
+    params = rand_params(A, C3, cuda, seed=seed)
+    g = torch.Generator().manual_seed(seed + 1)
     obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8)
     t, acts = alloc_acts(B, A, C3, cuda)
     net = _net(params, A, C3)
@@ -148,8 +151,7 @@ def test_backward_and_astats_match_torch(lib, cuda):
     ends = off[1:] + [n]
     for i, (o, e) in enumerate(zip(off, ends)):
         r = ref[o:e]
-        rel = (got[o:e] - r).abs().max().item() / max(1e-12, r.abs().max().item())
-        assert rel < 2e-5, ('param block', i, rel)
+        errs[('param block', i)] = (got[o:e] - r).abs().max().item() / max(1e-12, r.abs().max().item())
     # A factors: mean over rows of [x;1][x;1]^T
     x = obs.double() / 255.0
 
@@ -163,8 +165,34 @@ def test_backward_and_astats_match_torch(lib, cuda):
         xb = torch.cat([xin, torch.ones(xin.shape[0], 1, dtype=xin.dtype)], 1)
         r = xb.t() @ xb / xb.shape[0]
         got_f = a_host[so[f]:so[f] + din[f] * din[f]].reshape(din[f], din[f])
-        rel = (got_f - r).abs().max().item() / r.abs().max().item()
-        assert rel < 2e-5, ('A factor', f, rel)
+        errs[('A factor', f)] = (got_f - r).abs().max().item() / r.abs().max().item()
+    return errs
+
+
+def _with_mode(lib, mode, fn, *a, **k):
+    prev = lib.acmi_get_gemm_mode()
+    _lib.call('acmi_set_gemm_mode', mode)
+    try:
+        return fn(*a, **k)
+    finally:
+        _lib.call('acmi_set_gemm_mode', prev)
+
+
+def test_backward_and_astats_match_torch(lib, cuda):
+    for key, rel in _backward_errors(lib, cuda).items():
+        assert rel < 2e-5, (key, rel)
+
+
+def test_x3_reductions_as_accurate_as_f32(lib, cuda):
+    """The bf16x3 split-operand reductions (symred3.hpp) are f32-class: against
+    float64, every gradient block and A factor is within 2x (+1e-7) of the error of
+    the v_mfma_f32_32x32x2_f32 path on the same inputs."""
+    ex3 = _with_mode(lib, _lib.GEMM_X3, _backward_errors, lib, cuda, B=32, seed=21)
+    ef32 = _with_mode(lib, _lib.GEMM_F32, _backward_errors, lib, cuda, B=32, seed=21)
+    for key in ef32:
+        print(key, 'x3 %.3g  f32 %.3g' % (ex3[key], ef32[key]))
+    for key in ef32:
+        assert ex3[key] <= 2 * ef32[key] + 1e-7, (key, ex3[key], ef32[key])
 
 
 def test_kfac_inverse_matches_numpy(lib, cuda):

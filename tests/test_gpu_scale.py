@@ -45,9 +45,21 @@ def test_forward_batch_regimes_match_torch(lib, cuda, B):
         assert rel < 1e-5, (B, name, rel)
 
 
-def test_backward_multichunk_matches_torch(lib, cuda):
+@pytest.mark.parametrize('mode', [_lib.GEMM_X3, _lib.GEMM_F32])
+def test_backward_multichunk_matches_torch(lib, cuda, mode):
     """B = 96 images: conv1 has 38400 rows (3 i8 A-factor chunks), every split-K
-    reduction runs several chunks, the narrow Gram kernel several blocks."""
+    reduction runs several chunks, the narrow Gram kernel several blocks.  Both
+    arithmetic modes of the wgrad + A-factor reductions (bf16x3 split operands,
+    f32 MFMA) hold the same float64 tolerance."""
+    prev = lib.acmi_get_gemm_mode()
+    _lib.call('acmi_set_gemm_mode', mode)
+    try:
+        _backward_multichunk(lib, cuda)
+    finally:
+        _lib.call('acmi_set_gemm_mode', prev)
+
+
+def _backward_multichunk(lib, cuda):
     A, C3, B = 6, 32, 96
     params = rand_params(A, C3, cuda, seed=13)
     g = torch.Generator().manual_seed(14)
