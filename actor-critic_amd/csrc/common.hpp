@@ -101,6 +101,9 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// GEMM arithmetic mode (ACMI_GEMM_X3 / ACMI_GEMM_F32, acmi_set_gemm_mode; net.hip)
+extern int g_gemm_mode;
+
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // afactor_u8.hip: exact-integer conv1 A factor on the i8 matrix cores

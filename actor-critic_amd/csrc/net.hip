@@ -14,7 +14,7 @@
 #include <vector>
 
 #include "gemm.hpp"
-#include "symred3.hpp"
+#include "gemm3.hpp"
 #include "conv1u8.hpp"
 
 namespace acmi {
@@ -233,9 +233,9 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     MatI<true> opB{P + L.off[2], 64, 512, 64};
     EpiAct epi{a->a2, P + L.off[3], 64, 81, st * 81 * 64};
     if (B <= 2048)
-      launch_gemm<64, 64, 32, 1, 1, false, false>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
+      launch_mm<64, 64, 32, 1, 1, false, false, 16>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
     else
-      launch_gemm<128, 64, 32, 2, 1, false, false>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
+      launch_mm<128, 64, 32, 2, 1, false, false, 16>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
   }
   {  // conv3: -> [B,7,7,C3]
     using Src = ConvRows<float, 9, 9, 64, 3, 3, 1>;
@@ -243,9 +243,11 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     MatI<true> opB{P + L.off[4], C3, 576, C3};
     EpiAct epi{a->a3, P + L.off[5], C3, 49, st * 49 * C3};
     if constexpr (C3 == 32)
+      // (f32 MFMA: the 128x32 bf16x3 tile needs BK = 32 and fits 2 blocks per CU;
+      // measured slower than this at B = 512, 21.1 vs 19.6 us)
       launch_gemm<128, 32, 32, 1, 1, false, false>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
     else
-      launch_gemm<128, 64, 32, 2, 1, false, false>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
+      launch_mm<128, 64, 32, 2, 1, false, false, 16>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
   }
   // fc4: [B,49*C3] -> [B,512]
   const int K4 = 49 * C3;
@@ -259,10 +261,10 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     // small (rollout) batches: split K over chunks; the heads kernel reduces
     // the slabs in fixed order and applies bias + relu
     EpiPartial epi{a->ws, B, 512};
-    launch_gemm<64, 128, 32, 1, 2, true, false>(opA4, opB4, epi, B, 512, K4, nz, chunk, s);
+    launch_mm<64, 128, 32, 1, 2, true, false, 16>(opA4, opB4, epi, B, 512, K4, nz, chunk, s);
   } else {
     EpiAct epi{a->a4, P + L.off[7], 512, 1, st * 512};
-    launch_gemm<64, 128, 32, 1, 2, false, false>(opA4, opB4, epi, B, 512, K4, 1, 0, s);
+    launch_mm<64, 128, 32, 1, 2, false, false, 16>(opA4, opB4, epi, B, 512, K4, 1, 0, s);
   }
   // heads: [B,512] -> logits [B,A], value [B]
   const dim3 hg(cdiv(B, 4)), hb(256);
@@ -484,7 +486,7 @@ constexpr int kCUs = 256;
 // ACMI_GEMM_X3 = bf16x3 split operands on the bf16 matrix cores (symred3.hpp,
 // f32-accurate), ACMI_GEMM_F32 = v_mfma_f32_32x32x2_f32 (symred.hpp).  Initial
 // value from the environment variable ACMI_GEMM ("f32" or "x3"), default x3.
-static int g_gemm_mode = [] {
+int g_gemm_mode = [] {
   const char* e = getenv("ACMI_GEMM");
   return (e && e[0] == 'f') ? ACMI_GEMM_F32 : ACMI_GEMM_X3;
 }();
@@ -573,9 +575,9 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
     else if (pl.slabs)  // slab groups over the upper triangle of P^T P and the dY columns
       launch_symred<16>(opB, epi, pl.sp, I, J, (int)rows, nc, ch, s);
     else if (with_stats)  // 128x128 live tiles (fc4: K not a multiple of 64)
-      launch_gemm<128, 128, 16, 2, 2, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s, K);
+      launch_mm<128, 128, 16, 2, 2, true, true, 16>(opA, opB, epi, I, J, (int)rows, nc, ch, s, K);
     else
-      launch_gemm<128, 32, 32, 1, 1, true, true>(opA, opB, epi, I, J, (int)rows, nc, ch, s);
+      launch_mm<128, 32, 32, 1, 1, true, true, 32>(opA, opB, epi, I, J, (int)rows, nc, ch, s);
   } else {  // u8 patches (conv1): weight gradient only, bytes in LDS
     ACMI_REQUIRE(K == 256 && cout == 32 && ldy == 32, ACMI_ERR_ARG, "conv1 weight gradient shape");
     launch_conv1_wgrad_u8(src, dy, (int)rows, nc, ch, epi, s);
@@ -610,7 +612,7 @@ static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
     RowsAsI<DenseRows> op{src};
     ACMI_REQUIRE(pl.floats <= part_cap, ACMI_ERR_WS, "gcov workspace too small");
     EpiPartial epi{part, np, np};
-    launch_gemm<64, 64, 32, 1, 1, true, false>(op, op, epi, np, np, (int)rows, nc, pl.ch, s, np);
+    launch_mm<64, 64, 32, 1, 1, true, false, 16>(op, op, epi, np, np, (int)rows, nc, pl.ch, s, np);
   }
   if (nc <= 64)
     hipLaunchKernelGGL(finalize_cov_thread_kernel, dim3(cdiv((long long)sub * sub, 256)), dim3(256), 0,
@@ -665,7 +667,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     RowsAsK<DenseRows> opA{DenseRows{bw->d4, 512, B, 512}};
     MatTK<true> opB{P + L.off[6], 512, 512, K3};
     EpiReluGrad epi{bw->d3, a->a3, K3};
-    launch_gemm<64, 128, 32, 1, 2, false, false>(opA, opB, epi, B, K3, 512, 1, 0, s);
+    launch_mm<64, 128, 32, 1, 2, false, false, 16>(opA, opB, epi, B, K3, 512, 1, 0, s);
   }
   // conv input gradients as transposed products: rows = (phase, channel) of
   // the weights, columns = (super-)pixels gathering dY (EpiConvT, float4 rows)
@@ -675,7 +677,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     W opA{P + L.off[4]};
     RowsAsK<Src> opB{Src{bw->d3, B * Src::L}};
     EpiConvT<9, 9, 1, 64> epi{bw->d2, a->a2};
-    launch_gemm<64, 128, 16, 1, 2, false, false>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
+    launch_mm<64, 128, 16, 1, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
   }
   {  // conv2 -> d1 (stride 2: the four phases of a 2x2 super-pixel are the
      // 4 x 32 rows of one product over the 10x10 super-pixels)
@@ -685,7 +687,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     RowsAsK<Src> opB{Src{bw->d2, B * Src::L}};
     EpiConvT<20, 20, 2, 32> epi{bw->d1, a->a1};
     prof_begin(ACMI_PROF_CONV2_DX, s);
-    launch_gemm<128, 128, 16, 2, 2, false, false>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
+    launch_mm<128, 128, 16, 2, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
     prof_end(ACMI_PROF_CONV2_DX, s);
   }
   ACMI_LAUNCH_CHECK("dx_chain");

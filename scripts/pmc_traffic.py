@@ -12,8 +12,8 @@ import json
 import os
 import sys
 
-KERNEL = 'conv2 wgrad + K-FAC A-factor reduction GEMM (f32 MFMA)'
-MATCH = 'symred_kernel<16, acmi::CatRowsI<acmi::ConvRows<float, 20, 20, 32, 4, 4, 2>'
+KERNEL = 'conv2 wgrad + K-FAC A-factor reduction GEMM (bf16x3 split-operand MFMA, f32-accurate)'
+MATCH = 'symred3_kernel<acmi::CatRowsI<acmi::ConvRows<float, 20, 20, 32, 4, 4, 2>'
 WORKLOAD = 'Breakout ACKTR 512 envs/GPU x 20 steps'
 ALGO_INPUT_BYTES = 736624640  # a1 patches source + d2 read once (DESIGN.md Roofline)
 

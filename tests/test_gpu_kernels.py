@@ -183,16 +183,19 @@ def test_backward_and_astats_match_torch(lib, cuda):
         assert rel < 2e-5, (key, rel)
 
 
-def test_x3_reductions_as_accurate_as_f32(lib, cuda):
-    """The bf16x3 split-operand reductions (symred3.hpp) are f32-class: against
-    float64, every gradient block and A factor is within 2x (+1e-7) of the error of
-    the v_mfma_f32_32x32x2_f32 path on the same inputs."""
+def test_x3_gemms_are_f32_class(lib, cuda):
+    """The bf16x3 split-operand GEMMs (symred3.hpp, gemm3.hpp) are f32-class:
+    against float64, every gradient block and A factor of the backward (whose
+    conv input-gradient chain runs on gemm3) is within 5e-6 relative and within
+    6x (+1e-7) of the error of the v_mfma_f32_32x32x2_f32 path on the same inputs
+    (measured: A factors 0.8-1.3x, gradient blocks up to 4.5x of ~7e-7 = 3.2e-6:
+    each 16-k step rounds six partial products into the accumulator)."""
     ex3 = _with_mode(lib, _lib.GEMM_X3, _backward_errors, lib, cuda, B=32, seed=21)
     ef32 = _with_mode(lib, _lib.GEMM_F32, _backward_errors, lib, cuda, B=32, seed=21)
     for key in ef32:
         print(key, 'x3 %.3g  f32 %.3g' % (ex3[key], ef32[key]))
     for key in ef32:
-        assert ex3[key] <= 2 * ef32[key] + 1e-7, (key, ex3[key], ef32[key])
+        assert ex3[key] <= 5e-6 and ex3[key] <= 6 * ef32[key] + 1e-7, (key, ex3[key], ef32[key])
 
 
 def test_kfac_inverse_matches_numpy(lib, cuda):
