@@ -508,8 +508,8 @@ static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows, bo
   // column-sum row's P part, by symmetry
   p.J = p.kp + p.cout_pad;
   p.slabs = with_stats && sym_plan(K, p.cout_pad, &p.sp);  // (f32 patch sources only)
-  if (u8)  // conv1 weight gradient: conv1_wgrad_u8_kernel, one 256x32 block per chunk
-    conv1_wgrad_u8_plan(rows, &p.nc, &p.ch);
+  if (u8)  // conv1 weight gradient: conv1_wgrad_u8/x3_kernel, one 256x32 block per chunk
+    conv1_wgrad_u8_plan(rows, &p.nc, &p.ch, mode);
   else if (p.slabs && mode == ACMI_GEMM_X3)
     plan_rounds(rows, p.sp.ngroups, kCUs * std::min(8, 160 * 1024 / symred3_lds_bytes()), &p.nc,
                 &p.ch);
@@ -636,7 +636,8 @@ static long long bwd_partial_cap(int B, int A, int C3) {
   for (int l = 0; l < 5; ++l) {
     for (int mode : {ACMI_GEMM_F32, ACMI_GEMM_X3})
       m = std::max(m, wgrad_plan(Ks[l], co[l], true, rowsL[l], false, mode).floats);
-    m = std::max(m, wgrad_plan(Ks[l], co[l], false, rowsL[l], l == 0).floats);
+    for (int mode : {ACMI_GEMM_F32, ACMI_GEMM_X3})
+      m = std::max(m, wgrad_plan(Ks[l], co[l], false, rowsL[l], l == 0, mode).floats);
     // G factors of the same layer's output
     if (co[l] <= 64) {
       int nc;
