@@ -135,6 +135,41 @@ struct ConvRows {
     const uint32_t ch = rem - kw * C;
     return Cp{(kh * W + kw) * C + ch, ok};
   }
+  // Row iterator for loops that walk rows r0, r0 + STEP, ... (symred3): the
+  // (oh, ow) decode is carried along with adds and selects instead of the two
+  // constant divisions and three multiplies of row() per row (quarter-rate
+  // v_mul_hi/lo_u32 on the VALU that the staging shares with the MFMAs).
+  struct It {
+    uint32_t off;
+    int oh, ow, r;
+  };
+  __device__ __forceinline__ It iter(int r0) const {
+    const uint32_t r = r0 < rows ? (uint32_t)r0 : 0u;
+    const uint32_t img = r / L;
+    const uint32_t p = r - img * L;
+    const uint32_t oh = p / OW;
+    const uint32_t ow = p - oh * OW;
+    return It{img * img_stride + (oh * (S * W) + ow * S) * C, (int)oh, (int)ow, r0};
+  }
+  template <int STEP>
+  __device__ __forceinline__ void advance(It& it) const {
+    static_assert(STEP < L, "one image boundary per step at most");
+    constexpr int DR = STEP / OW, DC = STEP % OW;
+    constexpr uint32_t ROW = S * W * C, COL = S * C;
+    it.r += STEP;
+    it.ow += DC;
+    it.oh += DR;
+    it.off += DR * ROW + DC * COL;
+    const bool w1 = it.ow >= OW;
+    it.ow -= w1 ? OW : 0;
+    it.oh += w1 ? 1 : 0;
+    it.off += w1 ? ROW - OW * COL : 0u;
+    const bool w2 = it.oh >= OH;
+    it.oh -= w2 ? OH : 0;
+    it.off += w2 ? img_stride - OH * ROW : 0u;
+  }
+  __device__ __forceinline__ R row_of(const It& it) const { return R{it.off, it.r < rows}; }
+
   using St = typename std::conditional<sizeof(T) == 1, StU8, StF4>::type;
   __device__ __forceinline__ St stage(const R& r, const Cp& c, bool in) const {
     const bool ok = in && r.ok && c.ok;
@@ -160,6 +195,19 @@ struct DenseRows {
     return R{(uint32_t)r * (uint32_t)ld, r < rows};
   }
   __device__ __forceinline__ Cp col(int c) const { return Cp{(uint32_t)c, c < cols}; }
+  struct It {
+    uint32_t off;
+    int r;
+  };
+  __device__ __forceinline__ It iter(int r0) const {
+    return It{(uint32_t)(r0 < rows ? r0 : 0) * (uint32_t)ld, r0};
+  }
+  template <int STEP>
+  __device__ __forceinline__ void advance(It& it) const {
+    it.r += STEP;
+    it.off += (uint32_t)(STEP * ld);
+  }
+  __device__ __forceinline__ R row_of(const It& it) const { return R{it.off, it.r < rows}; }
   using St = StF4;
   __device__ __forceinline__ St stage(const R& r, const Cp& c, bool in) const {
     const bool ok = in && r.ok && c.ok;
@@ -285,6 +333,41 @@ struct CatRowsI {
     c.jj = j - kp;
     c.seg = j < kp ? 0 : (c.jj < cout_pad ? 1 : 3);
     return c;
+  }
+  // Row iterator over the P source and the dY rows together (symred3)
+  struct It {
+    typename Src::It p;
+    uint32_t dyoff;
+    int r;
+  };
+  __device__ __forceinline__ It iter(int r0) const {
+    return It{src.iter(r0 < rows ? r0 : 0), (r0 < rows ? (uint32_t)r0 : 0u) * (uint32_t)ldy, r0};
+  }
+  template <int STEP>
+  __device__ __forceinline__ void advance(It& it) const {
+    src.template advance<STEP>(it.p);
+    it.dyoff += (uint32_t)(STEP * ldy);
+    it.r += STEP;
+  }
+  // A thread's column run resolved once: its segment's base pointer (P column
+  // offset or dY column folded in) and validity, so a staged run costs one
+  // 32-bit select of the row offset, one 64-bit add and the zero-run select.
+  struct CB {
+    const float* base;
+    bool isp;
+    bool ok;
+  };
+  __device__ __forceinline__ CB col_base(int j) const {
+    const C c = col(j);
+    if constexpr (std::is_same<typename Src::elem_t, float>::value) {
+      if (c.seg == 0) return CB{src.x + c.p.off, true, c.p.ok};
+    }
+    return CB{dy + (c.seg == 1 ? c.jj : 0), false, c.seg == 1};
+  }
+  __device__ __forceinline__ StF4 stage_it(const It& it, const CB& cb, bool in) const {
+    const bool ok = in && cb.ok && it.r < rows;
+    const uint32_t roff = cb.isp ? it.p.off : it.dyoff;
+    return *reinterpret_cast<const float4*>(ok ? cb.base + roff : zero_run());
   }
   // One float4 load per element: P and dY are both float rows, so the
   // column's segment (fixed per thread) just selects the address.
