@@ -494,7 +494,9 @@ int g_gemm_mode = [] {
 struct WgradPlan {
   int I, J, kp, cout_pad, nc, ch;
   bool slabs;  // symred_kernel (slab groups) instead of 128x128 live tiles
+  bool six;    // bf16x3 six-slab groups (symred6_kernel)
   SymPlan sp;
+  SymPlan6 sp6;
   long long floats;
 };
 
@@ -508,8 +510,11 @@ static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows, bo
   // column-sum row's P part, by symmetry
   p.J = p.kp + p.cout_pad;
   p.slabs = with_stats && sym_plan(K, p.cout_pad, &p.sp);  // (f32 patch sources only)
+  p.six = p.slabs && mode == ACMI_GEMM_X3 && (symred_variant() == 0 || symred_variant() == 5) && sym_plan6(K, p.cout_pad, &p.sp6);
   if (u8)  // conv1 weight gradient: conv1_wgrad_u8/x3_kernel, one 256x32 block per chunk
     conv1_wgrad_u8_plan(rows, &p.nc, &p.ch, mode);
+  else if (p.six)  // one 512-thread block per CU (2 x 64 accumulators per wave)
+    plan_rounds(rows, p.sp6.ngroups, kCUs, &p.nc, &p.ch);
   else if (p.slabs && mode == ACMI_GEMM_X3)
     plan_rounds(rows, p.sp.ngroups, kCUs * std::min(8, 160 * 1024 / symred3_lds_bytes()), &p.nc,
                 &p.ch);
@@ -570,7 +575,9 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
   EpiPartial epi{part, I, J};
   prof_begin(site, s);
   if constexpr (std::is_same<typename Src::elem_t, float>::value) {
-    if (pl.slabs && mode == ACMI_GEMM_X3)  // slab groups, bf16x3 split operands
+    if (pl.six)  // six-slab groups, bf16x3 split operands
+      launch_symred6(opB, epi, pl.sp6, I, J, (int)rows, nc, ch, s);
+    else if (pl.slabs && mode == ACMI_GEMM_X3)  // slab groups, bf16x3 split operands
       launch_symred3(opB, epi, pl.sp, I, J, (int)rows, nc, ch, s);
     else if (pl.slabs)  // slab groups over the upper triangle of P^T P and the dY columns
       launch_symred<16>(opB, epi, pl.sp, I, J, (int)rows, nc, ch, s);
@@ -1007,6 +1014,39 @@ int acmi_selftest_plans(int max_k) {
     for (int j = 0; j < J; ++j)
       if (cs[j] < 1) return K;
   }
+  // six-slab groups (symred6_kernel): every needed sub-tile exactly once, at
+  // most 16 per group and 2 per wave, each column's sum by exactly one wave
+  for (int K : {512, 576})
+    for (int cp : {8, 32, 64}) {
+      SymPlan6 p;
+      if (!sym_plan6(K, cp, &p)) return -(K + cp);
+      const int nb = K / 64;
+      std::vector<int> cov((size_t)(nb + 1) * (nb + 1), 0), cs(nb + 1, 0);
+      for (int g = 0; g < p.ngroups; ++g) {
+        int n = 0;
+        for (int w = 0; w < 8; ++w)
+          for (int t = 0; t < 2; ++t) {
+            const int ra = p.g[g].ra[w][t], cb = p.g[g].cb[w][t];
+            if (ra < 0) {
+              if (t == 0 && p.g[g].ra[w][1] >= 0) return -(K + cp);  // tile 1 without tile 0
+              continue;
+            }
+            ++n;
+            const int a = p.g[g].base[ra], b = p.g[g].base[cb];
+            if (a < 0 || b < 0 || a % 64 || a >= K || b < a) return -(K + cp);
+            cov[(size_t)(a / 64) * (nb + 1) + b / 64]++;
+            if (a == 0) cs[b / 64]++;
+            // a half-width (dY) tile in slot 0 needs slot 1 half as well (kernel variants)
+            if (t == 1 && p.g[g].base[p.g[g].cb[w][0]] == K && b != K) return -(K + cp);
+          }
+        if (n > 16) return -(K + cp);
+      }
+      for (int a = 0; a < nb; ++a)
+        for (int b = a; b <= nb; ++b)
+          if (cov[(size_t)a * (nb + 1) + b] != 1) return -(K + cp);
+      for (int b = 0; b <= nb; ++b)
+        if (cs[b] != 1) return -(K + cp);
+    }
   for (long long rows : {1000LL, 4096000LL, 829440LL, 501760LL, 10240LL}) {
     for (int live : {1, 3, 11, 14, 90}) {
       int nc, ch;

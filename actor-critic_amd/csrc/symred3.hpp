@@ -35,6 +35,8 @@
 
 #include <stdlib.h>
 
+#include <functional>
+
 #include "symred.hpp"
 
 namespace acmi {
@@ -431,12 +433,603 @@ void symred3i_kernel(Op op, Epi epi, SymPlan plan, int I, int J, int K, int k_ch
   }
 }
 
-// ACMI_SYMRED=i selects symred3i_kernel (A/B timing); =n / =m the no-split /
-// no-MFMA timing probes of symred3_kernel (wrong results)
+// ---------------------------------------------------------------------------
+// Wide groups: two 64x64 sub-tiles per wave, eight per block from the same
+// four staged slabs.  The split-K reduction streams every staged row from L2
+// once per group, and with one sub-tile per wave the load rate it needs to keep
+// the MFMAs busy (~10 TB/s chip-wide at conv2's shape) is about twice what the
+// gather sustains (the no-MFMA probe: 0.87 ms of 1.5); eight sub-tiles per
+// staged byte halve the groups (conv2 11 -> 6, conv3 14 -> 7).  Accumulators
+// 2 x 64 registers -> 2 waves per SIMD, 2 blocks per CU.
+// ---------------------------------------------------------------------------
+struct SymGroup2 {
+  int16_t base[4];  // first [P | dY] column of each staged slab (-1: none)
+  int8_t ra[4][2];  // per wave and tile: staged slab of the rows (-1: no tile)
+  int8_t cb[4][2];  // per wave and tile: staged slab of the columns
+};
+constexpr int kSym2MaxGroups = 48;
+struct SymPlan2 {
+  int ngroups;
+  SymGroup2 g[kSym2MaxGroups];
+};
+
+// Greedy cover of the needed sub-tiles -- (a, b), a <= b < nb over the P slabs
+// and (a, dY) -- by groups of <= 4 slabs and <= 8 sub-tiles: each round takes
+// the slab set that covers the most remaining sub-tiles.  Within a wave the
+// dY sub-tile (possibly a half slab) comes second, so the kernel needs only
+// the (1 or 2 tiles) x (second tile half or not) loop variants.  K % 64 == 0.
+inline bool sym_plan2(int K, int cout_pad, SymPlan2* p) {
+  if (K % 64 != 0 || cout_pad > 64 || cout_pad <= 0) return false;
+  const int nb = K / 64, ns = nb + 1;  // slab nb = dY
+  if (ns > 16) return false;
+  bool need[16][16] = {};
+  int left = 0;
+  for (int a = 0; a < nb; ++a)
+    for (int b = a; b < ns; ++b) need[a][b] = true, ++left;
+  int n = 0;
+  while (left > 0) {
+    if (n >= kSym2MaxGroups) return false;
+    int best = -1, bestc = 0, bs[4] = {0, 0, 0, 0};
+    for (int s0 = 0; s0 < ns; ++s0)
+      for (int s1 = s0 + 1; s1 < ns; ++s1)
+        for (int s2 = s1 + 1; s2 < ns; ++s2)
+          for (int s3 = s2 + 1; s3 <= ns; ++s3) {  // s3 == ns: three slabs
+            const int sl[4] = {s0, s1, s2, s3 < ns ? s3 : -1};
+            int c = 0;
+            for (int x = 0; x < 4; ++x)
+              for (int y = x; y < 4; ++y)
+                if (sl[x] >= 0 && sl[y] >= 0 && need[sl[x]][sl[y]]) ++c;
+            c = std::min(c, 8);
+            if (c > bestc) {
+              bestc = c;
+              best = 1;
+              for (int x = 0; x < 4; ++x) bs[x] = sl[x];
+            }
+          }
+    if (best < 0) {  // fewer than 3 slabs' worth left (e.g. only (0,0) with nb == 1)
+      for (int a = 0; a < nb && best < 0; ++a)
+        for (int b = a; b < ns && best < 0; ++b)
+          if (need[a][b]) {
+            bs[0] = a;
+            bs[1] = b != a ? b : -1;
+            bs[2] = bs[3] = -1;
+            best = 1;
+          }
+    }
+    // collect up to 8 tiles of this slab set: P x P first, dY tiles last
+    int ta[8], tb[8], nt = 0;
+    for (int pass = 0; pass < 2; ++pass)
+      for (int x = 0; x < 4; ++x)
+        for (int y = 0; y < 4; ++y) {
+          if (bs[x] < 0 || bs[y] < 0 || nt >= 8) continue;
+          const int a = bs[x], b = bs[y];
+          if (a > b || !need[a][b] || (b == nb) != (pass == 1)) continue;
+          need[a][b] = false;
+          --left;
+          ta[nt] = x;
+          tb[nt] = y;
+          ++nt;
+        }
+    // waves take tiles in pairs; P x P tiles fill first-tile slots, so a dY
+    // tile is a wave's second tile unless both of its tiles are dY tiles
+    SymGroup2& G = p->g[n++];
+    for (int x = 0; x < 4; ++x) G.base[x] = (int16_t)(bs[x] < 0 ? -1 : (bs[x] == nb ? K : 64 * bs[x]));
+    for (int w = 0; w < 4; ++w)
+      for (int t = 0; t < 2; ++t) G.ra[w][t] = G.cb[w][t] = -1;
+    // order: the P x P tiles (first nt_p), then dY tiles; wave w gets tiles
+    // w and w + 4 so dY tiles (the tail) land in second slots first
+    for (int i = 0; i < nt; ++i) {
+      const int w = i % 4, t = i / 4;
+      G.ra[w][t] = (int8_t)ta[i];
+      G.cb[w][t] = (int8_t)tb[i];
+    }
+    // a wave with only a dY tile in slot 0 is fine (variant 1 tile, half)
+  }
+  p->ngroups = n;
+  return true;
+}
+
+template <class Op, class Epi>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void symred3w_kernel(Op op, Epi epi, SymPlan2 plan, int I, int J, int K, int k_chunk) {
+  constexpr int BK = kX3Rows;
+  constexpr int NR = BK / 8;
+  __shared__ __attribute__((aligned(16))) char lds[2 * kX3Buf];
+
+  const int total = gridDim.x;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, base8 = total >> 3, rem = total & 7;
+  const int l = xcd * base8 + min(xcd, rem) + (b >> 3);
+  const int ng = plan.ngroups;
+  const int bz = l / ng;
+  const SymGroup2& G = plan.g[l - bz * ng];
+  set_z(epi, bz);
+  const int kbeg = bz * k_chunk;
+  const int kend = min(K, kbeg + k_chunk);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int c16 = tid & 31;
+  const int scol = c16 * 8;
+  const int sbase = G.base[scol >> 6];
+  const int jcol = sbase >= 0 ? sbase + (scol & 63) : J;
+  const typename Op::CB c0 = op.col_base(jcol), c1 = op.col_base(jcol + 4);
+  typename Op::St ra[NR][2];
+  float csum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+  typename Op::It it[NR];
+#pragma unroll
+  for (int rr = 0; rr < NR; ++rr) it[rr] = op.iter(kbeg + (tid >> 5) + 8 * rr);
+
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      const int k = k0 + (tid >> 5) + 8 * rr;
+      ra[rr][0] = op.stage_it(it[rr], c0, k < kend);
+      ra[rr][1] = op.stage_it(it[rr], c1, k < kend);
+      op.template advance<BK>(it[rr]);
+    }
+  };
+  auto commit = [&](int buf) {
+    char* s = lds + buf * kX3Buf;
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      const int k = (tid >> 5) + 8 * rr;
+      const float4 x0 = finish(ra[rr][0]);
+      const float4 x1 = finish(ra[rr][1]);
+      csum[0] += x0.x;
+      csum[1] += x0.y;
+      csum[2] += x0.z;
+      csum[3] += x0.w;
+      csum[4] += x1.x;
+      csum[5] += x1.y;
+      csum[6] += x1.z;
+      csum[7] += x1.w;
+      uint4 h, m, lo;
+      split3(x0.x, x0.y, h.x, m.x, lo.x);
+      split3(x0.z, x0.w, h.y, m.y, lo.y);
+      split3(x1.x, x1.y, h.z, m.z, lo.z);
+      split3(x1.z, x1.w, h.w, m.w, lo.w);
+      const int off = k * kX3RowBytes + 16 * (c16 ^ (4 * (k & 3)));
+      *reinterpret_cast<uint4*>(s + off) = h;
+      *reinterpret_cast<uint4*>(s + kX3Part + off) = m;
+      *reinterpret_cast<uint4*>(s + 2 * kX3Part + off) = lo;
+    }
+  };
+
+  const int q = (lane >> 2) & 3, p = lane & 3, g = (lane >> 4) & 1, kh = lane >> 5;
+  auto slot_off = [&](int colblock) {
+    const int slot = (colblock >> 2) + 4 * g + p;
+    return (8 * kh + q) * kX3RowBytes + 8 * (slot ^ (8 * q));
+  };
+  int ib[2], jb[2], aoff[2][2], boff[2][2];
+  bool half[2];
+  const int ntile = (G.ra[wave][0] >= 0) + (G.ra[wave][1] >= 0);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int sa = G.ra[wave][t] < 0 ? 0 : G.ra[wave][t];
+    const int sb = G.cb[wave][t] < 0 ? 0 : G.cb[wave][t];
+    ib[t] = G.base[sa];
+    jb[t] = G.base[sb];
+    half[t] = jb[t] + 32 >= J;
+    aoff[t][0] = slot_off(64 * sa);
+    aoff[t][1] = slot_off(64 * sa + 32);
+    boff[t][0] = slot_off(64 * sb);
+    boff[t][1] = slot_off(64 * sb + 32);
+  }
+
+  f32x16 acc[2][2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][x][y][r] = 0.f;
+
+  if (nk > 0) {
+    fetch(kbeg);
+    commit(0);
+  }
+  __syncthreads();
+
+  auto tile = [&](const char* s, int t, auto NTc) {
+    constexpr int NT = decltype(NTc)::value;
+    bf16x8 a[2][3], bb[2][3];
+#pragma unroll
+    for (int pt = 0; pt < 3; ++pt) {
+      const char* sp = s + pt * kX3Part;
+      a[0][pt] = cat8(ds_tr16(sp + aoff[t][0]), ds_tr16(sp + aoff[t][0] + 4 * kX3RowBytes));
+      a[1][pt] = cat8(ds_tr16(sp + aoff[t][1]), ds_tr16(sp + aoff[t][1] + 4 * kX3RowBytes));
+      bb[0][pt] = cat8(ds_tr16(sp + boff[t][0]), ds_tr16(sp + boff[t][0] + 4 * kX3RowBytes));
+      if constexpr (NT == 2)
+        bb[1][pt] = cat8(ds_tr16(sp + boff[t][1]), ds_tr16(sp + boff[t][1] + 4 * kX3RowBytes));
+    }
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < NT; ++tn) acc[t][tm][tn] = mfma_x3(a[tm], bb[tn], acc[t][tm][tn]);
+  };
+  // NTILE tiles, N0 / N1 column blocks in tile 0 / 1 (wave-uniform variants)
+  auto step = [&](int kt, int cur, auto NTILE, auto N0, auto N1) {
+    constexpr int nt = decltype(NTILE)::value;
+    fetch(kbeg + (kt + 1) * BK);
+    __builtin_amdgcn_sched_barrier(0);
+    const char* s = lds + cur * kX3Buf;
+    if constexpr (nt >= 1) tile(s, 0, N0);
+    if constexpr (nt >= 2) tile(s, 1, N1);
+    __builtin_amdgcn_sched_barrier(0);
+    commit(cur ^ 1);
+    __syncthreads();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  auto run = [&](auto NTILE, auto N0, auto N1) {
+    for (int kt = 0; kt < nk; ++kt) step(kt, kt & 1, NTILE, N0, N1);
+  };
+  if (ntile == 0) run(I0{}, I2{}, I2{});
+  else if (ntile == 1) {
+    if (half[0]) run(I1{}, I1{}, I2{});
+    else run(I1{}, I2{}, I2{});
+  } else {
+    if (half[0]) run(I2{}, I1{}, I1{});  // both tiles are dY tiles
+    else if (half[1]) run(I2{}, I2{}, I1{});
+    else run(I2{}, I2{}, I2{});
+  }
+
+  float* cs = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[(tid >> 5) * 256 + scol + e] = csum[e];
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (t >= ntile) break;
+    store_tile<2, 2>(epi, acc[t], ib[t], jb[t], lane, I, J);
+    if (ib[t] == 0) {  // the (0, b) sub-tile is unique: its wave writes column sums of slab b
+      const int col = 64 * G.cb[wave][t] + lane;
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v += cs[r * 256 + col];
+      if (jb[t] + lane < J) epi.colsum(jb[t] + lane, v);
+    }
+  }
+}
+
+template <class Op, class Epi>
+inline void launch_symred3w(const Op& op, const Epi& e, const SymPlan2& plan, int I, int J, int K,
+                            int nchunk, int k_chunk, hipStream_t s) {
+  hipLaunchKernelGGL((symred3w_kernel<Op, Epi>), dim3(plan.ngroups * nchunk), dim3(256), 0, s, op, e,
+                     plan, I, J, K, k_chunk);
+}
+
+// ---------------------------------------------------------------------------
+// Six-slab groups: 8 waves (512 threads), two 64x64 sub-tiles per wave, six
+// staged slabs (384 columns) per block.  The no-MFMA probe of symred3_kernel
+// (ACMI_SYMRED=m: 0.87 of 1.50 ms at conv2's shape) shows the staging gather
+// alone is as long as the MFMA work: with one sub-tile per staged slab the
+// loads would need ~10 TB/s from L2 to keep the matrix cores busy.  Covering
+// the needed sub-tiles with 6-slab groups of <= 16 sub-tiles takes 3 groups
+// for conv2 / the heads (8 P slabs + dY; 11 groups of 4 slabs before) and 4
+// for conv3 (9 P slabs + dY; 14 before): ~2.4x fewer staged bytes per MFMA.
+// 72 KB of LDS and 2 x 64 accumulator registers per wave: one block per CU.
+// The slab sets are fixed coverings of the slab pairs (found offline by a
+// local search over 6-subsets: every pair of slabs, the dY slab included, lies
+// in some set); sym_plan6 assigns the sub-tiles to them by bipartite matching
+// with a balanced per-group capacity.
+// ---------------------------------------------------------------------------
+constexpr int kSixSlabs = 6;
+constexpr int kSixRowBytes = kSixSlabs * 64 * 2;      // 768
+constexpr int kSixPart = kX3Rows * kSixRowBytes;      // 12 KB
+constexpr int kSixBuf = 3 * kSixPart;                 // 36 KB
+constexpr int symred6_lds_bytes() { return 2 * kSixBuf; }
+
+struct SymGroup6 {
+  int16_t base[kSixSlabs];  // first [P | dY] column of each staged slab
+  int8_t ra[8][2];          // per wave and tile: staged slab of the rows (-1: no tile)
+  int8_t cb[8][2];          // per wave and tile: staged slab of the columns
+};
+constexpr int kSym6MaxGroups = 8;
+struct SymPlan6 {
+  int ngroups;
+  SymGroup6 g[kSym6MaxGroups];
+};
+
+inline bool sym_plan6(int K, int cout_pad, SymPlan6* p) {
+  if (cout_pad > 64 || cout_pad <= 0 || (K != 512 && K != 576)) return false;
+  static const int8_t sets8[3][6] = {{0, 1, 2, 4, 6, 8}, {1, 2, 3, 5, 7, 8}, {0, 3, 4, 5, 6, 7}};
+  static const int8_t sets9[4][6] = {
+      {0, 1, 2, 5, 7, 9}, {1, 3, 4, 6, 7, 8}, {0, 2, 3, 4, 6, 8}, {3, 4, 5, 6, 8, 9}};
+  const int nb = K / 64, ng = nb == 8 ? 3 : 4;
+  const int8_t(*sets)[6] = nb == 8 ? sets8 : sets9;
+  // sub-tiles (a, b), a <= b <= nb (b == nb: the dY slab)
+  int ta[64], tb[64], nt = 0;
+  for (int a = 0; a < nb; ++a)
+    for (int b = a; b <= nb; ++b) ta[nt] = a, tb[nt] = b, ++nt;
+  auto in = [&](int g, int x) {
+    for (int i = 0; i < 6; ++i)
+      if (sets[g][i] == x) return i;
+    return -1;
+  };
+  int owner[64];
+  for (int cap = (nt + ng - 1) / ng; cap <= 16; ++cap) {
+    int load[8] = {0};
+    for (int t = 0; t < nt; ++t) owner[t] = -1;
+    // augmenting paths (Kuhn) with capacity cap per group
+    bool ok = true;
+    for (int t = 0; t < nt && ok; ++t) {
+      int seen[8];
+      std::function<bool(int)> aug = [&](int u) -> bool {
+        for (int g = 0; g < ng; ++g) {
+          if (seen[g] || in(g, ta[u]) < 0 || in(g, tb[u]) < 0) continue;
+          seen[g] = 1;
+          if (load[g] < cap) {
+            owner[u] = g;
+            ++load[g];
+            return true;
+          }
+          for (int v = 0; v < nt; ++v)
+            if (owner[v] == g && aug(v)) {
+              owner[u] = g;
+              return true;
+            }
+        }
+        return false;
+      };
+      for (int g = 0; g < 8; ++g) seen[g] = 0;
+      ok = aug(t);
+    }
+    if (!ok) continue;
+    p->ngroups = ng;
+    for (int g = 0; g < ng; ++g) {
+      SymGroup6& G = p->g[g];
+      for (int i = 0; i < 6; ++i) G.base[i] = (int16_t)(sets[g][i] == nb ? K : 64 * sets[g][i]);
+      for (int w = 0; w < 8; ++w) G.ra[w][0] = G.ra[w][1] = G.cb[w][0] = G.cb[w][1] = -1;
+      int n = 0;
+      for (int pass = 0; pass < 2; ++pass)  // P x P sub-tiles first, dY sub-tiles last
+        for (int t = 0; t < nt; ++t) {
+          if (owner[t] != g || (tb[t] == nb) != (pass == 1)) continue;
+          const int w = n % 8, s = n / 8;
+          G.ra[w][s] = (int8_t)in(g, ta[t]);
+          G.cb[w][s] = (int8_t)in(g, tb[t]);
+          ++n;
+        }
+    }
+    return true;
+  }
+  return false;
+}
+
+// PIPE: the K-tile loads run two tiles ahead, and tile kt+1's split + LDS
+// commit is issued between tile kt's first sub-tile MFMAs (sched_group_barrier)
+// instead of after both sub-tiles.  With one 512-thread block per CU the two
+// waves of a SIMD share the block's barrier phase, so without this a SIMD's
+// MFMA pipe idles through every commit.
+template <class Op, class Epi, bool PIPE = false>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_chunk) {
+  constexpr int BK = kX3Rows;
+  __shared__ __attribute__((aligned(16))) char lds[2 * kSixBuf];
+
+  const int total = gridDim.x;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, base8 = total >> 3, rem = total & 7;
+  const int l = xcd * base8 + min(xcd, rem) + (b >> 3);
+  const int ng = plan.ngroups;
+  const int bz = l / ng;
+  const SymGroup6& G = plan.g[l - bz * ng];
+  set_z(epi, bz);
+  const int kbeg = bz * k_chunk;
+  const int kend = min(K, kbeg + k_chunk);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  // staging: thread -> k-row tid/32 (16 rows), 12 consecutive staged columns
+  // 12*(tid&31) .. +11 = three float4 runs (a run never crosses a slab)
+  const int srow = tid >> 5;
+  const int scol = 12 * (tid & 31);
+  typename Op::CB cbs[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int c = scol + 4 * u;
+    const int base = G.base[c >> 6];
+    cbs[u] = op.col_base(base >= 0 ? base + (c & 63) : J);
+  }
+  typename Op::It it = op.iter(kbeg + srow);
+  typename Op::St ra[PIPE ? 2 : 1][3];
+  float csum[12];
+#pragma unroll
+  for (int e = 0; e < 12; ++e) csum[e] = 0.f;
+
+  auto fetch = [&](int k0, auto S) {
+    constexpr int set = decltype(S)::value;
+    const int k = k0 + srow;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) ra[set][u] = op.stage_it(it, cbs[u], k < kend);
+    op.template advance<BK>(it);
+  };
+  auto commit = [&](int buf, auto S) {
+    constexpr int set = decltype(S)::value;
+    char* s = lds + buf * kSixBuf + srow * kSixRowBytes;
+    const int q8 = 8 * (srow & 3);
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const float4 x = finish(ra[set][u]);
+      csum[4 * u] += x.x;
+      csum[4 * u + 1] += x.y;
+      csum[4 * u + 2] += x.z;
+      csum[4 * u + 3] += x.w;
+      uint2 h, m, lo;
+      split3(x.x, x.y, h.x, m.x, lo.x);
+      split3(x.z, x.w, h.y, m.y, lo.y);
+      const int off = 8 * (((scol >> 2) + u) ^ q8);
+      *reinterpret_cast<uint2*>(s + off) = h;
+      *reinterpret_cast<uint2*>(s + kSixPart + off) = m;
+      *reinterpret_cast<uint2*>(s + 2 * kSixPart + off) = lo;
+    }
+  };
+
+  const int q = (lane >> 2) & 3, p = lane & 3, g = (lane >> 4) & 1, kh = lane >> 5;
+  auto slot_off = [&](int colblock) {
+    const int slot = (colblock >> 2) + 4 * g + p;
+    return (8 * kh + q) * kSixRowBytes + 8 * (slot ^ (8 * q));
+  };
+  int ib[2], jb[2], aoff[2][2], boff[2][2];
+  bool half[2];
+  const int ntile = (G.ra[wave][0] >= 0) + (G.ra[wave][1] >= 0);
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int sa = G.ra[wave][t] < 0 ? 0 : G.ra[wave][t];
+    const int sb = G.cb[wave][t] < 0 ? 0 : G.cb[wave][t];
+    ib[t] = G.base[sa];
+    jb[t] = G.base[sb];
+    half[t] = jb[t] + 32 >= J;
+    aoff[t][0] = slot_off(64 * sa);
+    aoff[t][1] = slot_off(64 * sa + 32);
+    boff[t][0] = slot_off(64 * sb);
+    boff[t][1] = slot_off(64 * sb + 32);
+  }
+
+  f32x16 acc[2][2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][x][y][r] = 0.f;
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if (nk > 0) {
+    fetch(kbeg, S0{});
+    if constexpr (PIPE) fetch(kbeg + BK, S1{});
+    commit(0, S0{});
+  }
+  __syncthreads();
+
+  auto tile = [&](const char* s, int t, auto NTc) {
+    constexpr int NT = decltype(NTc)::value;
+    bf16x8 a[2][3], bb[2][3];
+#pragma unroll
+    for (int pt = 0; pt < 3; ++pt) {
+      const char* sp = s + pt * kSixPart;
+      a[0][pt] = cat8(ds_tr16(sp + aoff[t][0]), ds_tr16(sp + aoff[t][0] + 4 * kSixRowBytes));
+      a[1][pt] = cat8(ds_tr16(sp + aoff[t][1]), ds_tr16(sp + aoff[t][1] + 4 * kSixRowBytes));
+      bb[0][pt] = cat8(ds_tr16(sp + boff[t][0]), ds_tr16(sp + boff[t][0] + 4 * kSixRowBytes));
+      if constexpr (NT == 2)
+        bb[1][pt] = cat8(ds_tr16(sp + boff[t][1]), ds_tr16(sp + boff[t][1] + 4 * kSixRowBytes));
+    }
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < NT; ++tn) acc[t][tm][tn] = mfma_x3(a[tm], bb[tn], acc[t][tm][tn]);
+  };
+  // SN: register set holding tile kt+1 (PIPE) / receiving it (plain)
+  auto step = [&](int kt, int cur, auto NTILE, auto N0, auto N1, auto SN) {
+    constexpr int nt = decltype(NTILE)::value;
+    constexpr int sn = decltype(SN)::value;
+    const char* s = lds + cur * kSixBuf;
+    if constexpr (PIPE) {
+      fetch(kbeg + (kt + 2) * BK, std::integral_constant<int, sn ^ 1>{});
+      if constexpr (nt >= 1) {
+        tile(s, 0, N0);
+        if (kt + 1 < nk) commit(cur ^ 1, SN);
+        constexpr int nm = 6 * 2 * decltype(N0)::value;
+        __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);             // the loads
+        __builtin_amdgcn_sched_group_barrier(0x100, 6 * (2 + decltype(N0)::value), 0);  // fragments
+#pragma unroll
+        for (int i = 0; i < nm; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        if (kt + 1 < nk) commit(cur ^ 1, SN);
+      }
+      if constexpr (nt >= 2) tile(s, 1, N1);
+    } else {
+      fetch(kbeg + (kt + 1) * BK, S0{});
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (nt >= 1) tile(s, 0, N0);
+      if constexpr (nt >= 2) tile(s, 1, N1);
+      __builtin_amdgcn_sched_barrier(0);
+      commit(cur ^ 1, S0{});
+    }
+    __syncthreads();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  auto run = [&](auto NTILE, auto N0, auto N1) {
+    if constexpr (PIPE) {
+      for (int kt = 0; kt < nk; kt += 2) {
+        step(kt, 0, NTILE, N0, N1, S1{});
+        if (kt + 1 < nk) step(kt + 1, 1, NTILE, N0, N1, S0{});
+      }
+    } else {
+      for (int kt = 0; kt < nk; ++kt) step(kt, kt & 1, NTILE, N0, N1, S0{});
+    }
+  };
+  if (ntile == 0) run(I0{}, I2{}, I2{});
+  else if (ntile == 1) {
+    if (half[0]) run(I1{}, I1{}, I2{});
+    else run(I1{}, I2{}, I2{});
+  } else {
+    if (half[0]) run(I2{}, I1{}, I1{});
+    else if (half[1]) run(I2{}, I2{}, I1{});
+    else run(I2{}, I2{}, I2{});
+  }
+
+  // column sums: [16 k-row threads][384 staged columns] through the free LDS
+  float* cs = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int e = 0; e < 12; ++e) cs[srow * 384 + scol + e] = csum[e];
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (t >= ntile) break;
+    store_tile<2, 2>(epi, acc[t], ib[t], jb[t], lane, I, J);
+    if (ib[t] == 0) {  // the (0, b) sub-tile is unique: its wave writes slab b's column sums
+      const int col = 64 * G.cb[wave][t] + lane;
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v += cs[r * 384 + col];
+      if (jb[t] + lane < J) epi.colsum(jb[t] + lane, v);
+    }
+  }
+}
+
+inline int symred_variant();
+template <class Op, class Epi>
+inline void launch_symred6(const Op& op, const Epi& e, const SymPlan6& plan, int I, int J, int K,
+                           int nchunk, int k_chunk, hipStream_t s) {
+  if (symred_variant() != 5)
+    hipLaunchKernelGGL((symred6_kernel<Op, Epi, true>), dim3(plan.ngroups * nchunk), dim3(512), 0, s,
+                       op, e, plan, I, J, K, k_chunk);
+  else
+    hipLaunchKernelGGL((symred6_kernel<Op, Epi, false>), dim3(plan.ngroups * nchunk), dim3(512), 0, s,
+                       op, e, plan, I, J, K, k_chunk);
+}
+
+// ACMI_SYMRED: default six-slab groups (symred6_kernel, PIPE) where sym_plan6
+// has a covering; =s the same without PIPE; =4 four-slab groups
+// (symred3_kernel); =i its interleaved variant; =n / =m its no-split / no-MFMA
+// timing probes (wrong results).  Measured at the bench shape (conv2, M =
+// 10240): six PIPE 1.27 ms, six 1.36, four 1.52, four interleaved 1.50, four
+// without the split 1.43, four without MFMAs 0.87.
 inline int symred_variant() {
   static const int v = [] {
     const char* e = getenv("ACMI_SYMRED");
-    return !e ? 0 : e[0] == 'i' ? 1 : e[0] == 'n' ? 2 : e[0] == 'm' ? 3 : 0;
+    return !e ? 0 : e[0] == 'i' ? 1 : e[0] == 'n' ? 2 : e[0] == 'm' ? 3 : e[0] == '4' ? 4 : e[0] == 's' ? 5 : 0;
   }();
   return v;
 }
