@@ -233,7 +233,7 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     MatI<true> opB{P + L.off[2], 64, 512, 64};
     EpiAct epi{a->a2, P + L.off[3], 64, 81, st * 81 * 64};
     if (B <= 2048)
-      launch_mm<64, 64, 32, 1, 1, false, false, 16>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
+      launch_mm<64, 64, 32, 1, 1, false, false, 32>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
     else
       launch_mm<128, 64, 32, 2, 1, false, false, 16>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
   }

@@ -13,7 +13,7 @@ import os
 import sys
 
 KERNEL = 'conv2 wgrad + K-FAC A-factor reduction GEMM (bf16x3 split-operand MFMA, f32-accurate)'
-MATCH = 'symred3_kernel<acmi::CatRowsI<acmi::ConvRows<float, 20, 20, 32, 4, 4, 2>'
+MATCH = 'symred6_kernel<acmi::CatRowsI<acmi::ConvRows<float, 20, 20, 32, 4, 4, 2>'
 WORKLOAD = 'Breakout ACKTR 512 envs/GPU x 20 steps'
 ALGO_INPUT_BYTES = 736624640  # a1 patches source + d2 read once (DESIGN.md Roofline)
 
@@ -47,7 +47,7 @@ def main(d, out):
         'hbm_bytes_per_launch': (2 * f_kb + w_kb) * 1024.0,
         'algorithmic_input_bytes': ALGO_INPUT_BYTES,
         'source': 'rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE, separate passes, '
-                  'bench.py --steps 5 --warmup 2',
+                  'bench.py --steps 3 --warmup 1 --no-cpu-baseline',
     }
     with open(out, 'w') as fh:
         json.dump(res, fh, indent=1)
