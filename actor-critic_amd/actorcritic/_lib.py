@@ -60,6 +60,10 @@ _SIGS = {
                                      c_i64, c_vp]),
     'acmi_sample_actions': (c_int, [c_vp, c_int, c_int, c_int, c_u32, c_u32, c_u32, c_vp, c_int, c_vp,
                                     c_vp, c_vp]),
+    'acmi_sample_actions_at': (c_int, [c_vp, c_int, c_int, c_int, c_u32, c_u32, c_u32, c_int, c_vp, c_int,
+                                       c_vp, c_vp, c_vp]),
+    'acmi_sample_actions_dev': (c_int, [c_vp, c_int, c_int, c_int, c_u32, c_u32, c_vp, c_u32, c_int, c_vp,
+                                        c_int, c_vp, c_vp, c_vp]),
     'acmi_categorical': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     'acmi_returns': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     'acmi_a2c_loss_ws_floats': (c_i64, [c_int]),

@@ -7,7 +7,19 @@ activations straight into the update's [N*T] buffers (row n*T + t), one sampling
 kernel, one stepper kernel that writes the next stacked frame into the [N, T+1]
 observation buffer — no host copies, no Python lists.  Anything else takes the
 reference's list-based loop.
+
+Two opt-in variants, bit-identical to the one-chain rollout (test_two_stream_rollout_
+is_bit_identical): ACMI_ROLLOUT_SPLIT=1 runs the two env halves as two chains on two
+HIP streams (the sampler keys its RNG by the global row, acmi_sample_actions_at, the
+stepper by the global env id); ACMI_ROLLOUT_GRAPH=1 captures the rollout once as a
+hipGraph and replays it (the RNG counter read from device memory,
+acmi_sample_actions_dev).  Neither is faster on one MI355X at 512 envs (2.21-2.25 ms
+per 20-step rollout in all four combinations): the per-step kernels are GPU-bound,
+half-batch kernels cost 70-80 % of full-batch ones, and the host keeps up.  They are
+kept for hosts where launch overhead is not hidden.
 """
+
+import os
 
 from abc import ABCMeta, abstractmethod
 
@@ -64,6 +76,15 @@ class _RolloutBuffers(object):
         self.acts = engine.activations(N * T, 'rollout')
         self.bad_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self.bad_event = None
+        # two-chain rollout: env halves on the current stream and a side stream,
+        # each with its own forward workspace (fc4 split-K slabs)
+        self.halves = (os.environ.get('ACMI_ROLLOUT_SPLIT', '0') == '1' and N >= 256 and N % 2 == 0)
+        self.side = torch.cuda.Stream(device=dev) if self.halves else None
+        need = int(_lib.load().acmi_forward_ws_floats(N // 2 if self.halves else N))
+        self.ws = [torch.zeros(max(need, 1), dtype=torch.float32, device=dev) for _ in range(2)]
+        self.use_graph = os.environ.get('ACMI_ROLLOUT_GRAPH', '0') == '1'
+        self.graph, self.graph_key, self.warm = None, None, False
+        self.ctr_dev = torch.zeros(1, dtype=torch.int32, device=dev)
 
 
 class MultiEnvAgent(Agent):
@@ -104,6 +125,48 @@ class MultiEnvAgent(Agent):
                 transpose_list(terminal_steps), next_observations, transpose_list(info_steps))
 
     # -- device rollout ------------------------------------------------------------
+    def _rollout_halves(self, eng, env, rb, N, T, A, seed, dev_ctr=False):
+        """The T-step rollout as one chain (rb.halves False) or as the two env halves'
+        chains on the current stream and rb.side."""
+        main = torch.cuda.current_stream(eng.device)
+        rb.obs[:, 0].copy_(rb.next_obs)
+        if rb.halves:
+            rb.side.wait_stream(main)
+        N2 = N // 2 if rb.halves else N
+        for t in range(T):
+            _half_step(eng, env, rb, 0, N2, T, A, t, seed, dev_ctr)
+            if rb.halves:
+                with torch.cuda.stream(rb.side):
+                    _half_step(eng, env, rb, 1, N2, T, A, t, seed, dev_ctr)
+            if not dev_ctr:
+                eng.sample_counter += 1
+        if rb.halves:
+            main.wait_stream(rb.side)
+        rb.actions.copy_(rb.actions_tn.t())
+
+    def _rollout_graph(self, eng, env, rb, N, T, A, seed):
+        """The two-chain rollout as one hipGraph (torch.cuda.CUDAGraph over the
+        libacmi launches): captured on the second rollout with these buffers, then
+        replayed -- ~280 launches per rollout stop costing host time.  Everything
+        that differs between rollouts lives in device memory (observations, env
+        states, parameters updated in place); the RNG counter is refreshed in
+        rb.ctr_dev before each replay."""
+        key = (eng.params.data_ptr(), id(env), seed, eng.rank)
+        if rb.graph is None or rb.graph_key != key:
+            if not rb.warm:  # first rollout eager: loads the code objects, sizes workspaces
+                rb.warm = True
+                self._rollout_halves(eng, env, rb, N, T, A, seed)
+                return
+            rb.ctr_dev.fill_(eng.sample_counter & 0xFFFFFFFF)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._rollout_halves(eng, env, rb, N, T, A, seed, dev_ctr=True)
+            rb.graph, rb.graph_key = g, key
+        else:
+            rb.ctr_dev.fill_(eng.sample_counter & 0xFFFFFFFF)
+        rb.graph.replay()
+        eng.sample_counter += T
+
     def _interact_device(self):
         from actorcritic.envs.atari.model import ForwardOut
         from actorcritic.envs.atari.wrappers import EpisodeInfoBatch
@@ -119,26 +182,32 @@ class MultiEnvAgent(Agent):
                 eng.check_bad_rows()
         if self._observations is None:
             env.reset_into(rb.next_obs.data_ptr())
-        rb.obs[:, 0].copy_(rb.next_obs)
         stream = eng.stream()
         A = eng.A
         obs0 = rb.obs.data_ptr()
         rew0, term0, ep0 = rb.rewards.data_ptr(), rb.terminals.data_ptr(), rb.episode_rewards.data_ptr()
         seed = (self._model._random_seed or 0) & 0xFFFFFFFF
-        for t in range(T):
-            src = obs0 + t * OBS_BYTES
-            eng.forward(src, N, rb.acts.view(t, T), want_value=True, img_stride=T * OBS_BYTES, act_stride=T)
-            act_t = rb.actions_tn[t]
-            _lib.call('acmi_sample_actions', _lib.c_vp(rb.acts.logits.data_ptr() + 4 * t * A), T * A, N, A, seed,
-                      eng.rank, eng.sample_counter, None, 0, _lib.c_vp(act_t.data_ptr()),
-                      _lib.c_vp(eng._bad_rows.data_ptr()), stream)
-            eng.sample_counter += 1
-            if t + 1 < T:
-                dst, dstride = obs0 + (t + 1) * OBS_BYTES, T * OBS_BYTES
-            else:
-                dst, dstride = rb.next_obs.data_ptr(), OBS_BYTES
-            env.step_into(act_t.data_ptr(), src, T * OBS_BYTES, dst, dstride, rew0 + 4 * t, term0 + t, ep0 + 4 * t, T)
-        rb.actions.copy_(rb.actions_tn.t())
+        if rb.use_graph:
+            self._rollout_graph(eng, env, rb, N, T, A, seed)
+        elif rb.halves:
+            self._rollout_halves(eng, env, rb, N, T, A, seed)
+        else:
+            rb.obs[:, 0].copy_(rb.next_obs)
+            for t in range(T):
+                src = obs0 + t * OBS_BYTES
+                eng.forward(src, N, rb.acts.view(t, T), want_value=True, img_stride=T * OBS_BYTES, act_stride=T)
+                act_t = rb.actions_tn[t]
+                _lib.call('acmi_sample_actions', _lib.c_vp(rb.acts.logits.data_ptr() + 4 * t * A), T * A, N, A,
+                          seed, eng.rank, eng.sample_counter, None, 0, _lib.c_vp(act_t.data_ptr()),
+                          _lib.c_vp(eng._bad_rows.data_ptr()), stream)
+                eng.sample_counter += 1
+                if t + 1 < T:
+                    dst, dstride = obs0 + (t + 1) * OBS_BYTES, T * OBS_BYTES
+                else:
+                    dst, dstride = rb.next_obs.data_ptr(), OBS_BYTES
+                env.step_into(act_t.data_ptr(), src, T * OBS_BYTES, dst, dstride, rew0 + 4 * t, term0 + t,
+                              ep0 + 4 * t, T)
+            rb.actions.copy_(rb.actions_tn.t())
         rb.bad_host.copy_(eng._bad_rows, non_blocking=True)
         rb.bad_event = torch.cuda.Event()
         rb.bad_event.record()
@@ -147,6 +216,34 @@ class MultiEnvAgent(Agent):
         self._observations = rb.next_obs
         return (rb.obs, rb.actions, rb.rewards, rb.terminals.view(torch.bool), rb.next_obs,
                 EpisodeInfoBatch(rb.episode_rewards))
+
+
+def _half_step(eng, env, rb, h, N2, T, A, t, seed, dev_ctr=False):
+    """Rollout step t of env half h (envs h*N2 .. h*N2+N2-1) on the current stream.
+    dev_ctr: the sampler's RNG counter is rb.ctr_dev + t (graph capture) instead of
+    the host eng.sample_counter."""
+    n0 = h * N2
+    row = n0 * T + t
+    obs0 = rb.obs.data_ptr()
+    src = obs0 + row * OBS_BYTES
+    acts = rb.acts.view(row, T, ws_rows=N2)
+    acts.ws = rb.ws[h].data_ptr()
+    acts.ws_floats = rb.ws[h].numel()
+    eng.forward(src, N2, acts, want_value=True, img_stride=T * OBS_BYTES, act_stride=T)
+    act_t = rb.actions_tn[t].data_ptr() + 4 * n0
+    if dev_ctr:
+        ctr_dev, ctr = _lib.c_vp(rb.ctr_dev.data_ptr()), t
+    else:
+        ctr_dev, ctr = None, eng.sample_counter & 0xFFFFFFFF
+    _lib.call('acmi_sample_actions_dev', _lib.c_vp(rb.acts.logits.data_ptr() + 4 * row * A), T * A, N2, A,
+              seed, eng.rank, ctr_dev, ctr, n0, None, 0, _lib.c_vp(act_t),
+              _lib.c_vp(eng._bad_rows.data_ptr()), eng.stream())
+    if t + 1 < T:
+        dst, dstride = src + OBS_BYTES, T * OBS_BYTES
+    else:
+        dst, dstride = rb.next_obs.data_ptr() + n0 * OBS_BYTES, OBS_BYTES
+    env.step_range_into(n0, N2, act_t, src, T * OBS_BYTES, dst, dstride, rb.rewards.data_ptr() + 4 * row,
+                        rb.terminals.data_ptr() + row, rb.episode_rewards.data_ptr() + 4 * row, T)
 
 
 def transpose_list(values):

@@ -98,6 +98,22 @@ class SyntheticAtariEnvs(object):
                   out_stride, ctypes.c_void_p(rew_ptr), ctypes.c_void_p(term_ptr), ctypes.c_void_p(ep_ptr), ld,
                   self._stream())
 
+    def step_range_into(self, n0, n, actions_ptr, obs_in_ptr, in_stride, obs_out_ptr, out_stride, rew_ptr,
+                        term_ptr, ep_ptr, ld):
+        """step_into for envs n0 .. n0+n-1 only (every pointer already at env n0)."""
+        if not hasattr(self, '_range_states'):
+            self._range_states = {}
+        st = self._range_states.get(n0)
+        if st is None:
+            st = _lib.EnvState(self._episode[n0:].data_ptr(), self._step[n0:].data_ptr(),
+                               self._length[n0:].data_ptr(), self._total[n0:].data_ptr(),
+                               self._done[n0:].data_ptr())
+            self._range_states[n0] = st
+        _lib.call('acmi_env_step', ctypes.byref(st), n, self.env_offset + n0, self.seed,
+                  ctypes.c_void_p(actions_ptr), ctypes.c_void_p(obs_in_ptr), in_stride, ctypes.c_void_p(obs_out_ptr),
+                  out_stride, ctypes.c_void_p(rew_ptr), ctypes.c_void_p(term_ptr), ctypes.c_void_p(ep_ptr), ld,
+                  self._stream())
+
     # -- gym-like batched API --------------------------------------------------
     def reset(self):
         self.reset_into(self._obs.data_ptr())

@@ -11,11 +11,16 @@ namespace acmi {
 // ---------------------------------------------------------------------------
 // sampling (policies.py:86 Categorical.sample / :87 mode)
 // ---------------------------------------------------------------------------
+// row_offset: global row index of local row 0 (a batch sampled in pieces draws
+// the same uniforms as in one launch)
+// ctr_dev (nullable): device counter base added to ctr (graph-replayed rollouts)
 __global__ void sample_kernel(const float* logits, int ld, int B, int A, uint32_t seed,
-                              uint32_t sid, uint32_t ctr, const float* uniforms, int mode,
+                              uint32_t sid, uint32_t ctr, const uint32_t* ctr_dev,
+                              uint32_t row_offset, const float* uniforms, int mode,
                               int32_t* actions, int32_t* bad) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= B) return;
+  if (ctr_dev) ctr += *ctr_dev;
   const float* z = logits + (long long)m * ld;
   float mx = -INFINITY;
   bool finite = true;
@@ -36,7 +41,7 @@ __global__ void sample_kernel(const float* logits, int ld, int B, int A, uint32_
   }
   float se = 0.f;
   for (int a = 0; a < A; ++a) se += expf(z[a] - mx);
-  const float u = uniforms ? uniforms[m] : u01(key4(seed, sid, ctr, (uint32_t)m));
+  const float u = uniforms ? uniforms[m] : u01(key4(seed, sid, ctr, (uint32_t)m + row_offset));
   const float target = u * se;
   float c = 0.f;
   int y = A - 1;
@@ -366,12 +371,28 @@ extern "C" {
 int acmi_sample_actions(const float* logits, int ld, int B, int A, uint32_t seed,
                         uint32_t stream_id, uint32_t counter, const float* uniforms, int mode,
                         int32_t* actions, int32_t* bad_rows, acmi_stream_t stream) {
-  ACMI_REQUIRE(logits && actions && bad_rows && B >= 0 && A >= 1 && ld >= A, ACMI_ERR_ARG,
-               "acmi_sample_actions: bad arguments");
+  return acmi_sample_actions_at(logits, ld, B, A, seed, stream_id, counter, 0, uniforms, mode,
+                                actions, bad_rows, stream);
+}
+
+int acmi_sample_actions_at(const float* logits, int ld, int B, int A, uint32_t seed,
+                           uint32_t stream_id, uint32_t counter, int row_offset,
+                           const float* uniforms, int mode, int32_t* actions, int32_t* bad_rows,
+                           acmi_stream_t stream) {
+  return acmi_sample_actions_dev(logits, ld, B, A, seed, stream_id, nullptr, counter, row_offset,
+                                 uniforms, mode, actions, bad_rows, stream);
+}
+
+int acmi_sample_actions_dev(const float* logits, int ld, int B, int A, uint32_t seed,
+                            uint32_t stream_id, const uint32_t* counter_dev, uint32_t counter_add,
+                            int row_offset, const float* uniforms, int mode, int32_t* actions,
+                            int32_t* bad_rows, acmi_stream_t stream) {
+  ACMI_REQUIRE(logits && actions && bad_rows && B >= 0 && A >= 1 && ld >= A && row_offset >= 0,
+               ACMI_ERR_ARG, "acmi_sample_actions: bad arguments");
   if (B == 0) return ACMI_OK;
   hipLaunchKernelGGL(sample_kernel, dim3(cdiv(B, 256)), dim3(256), 0, (hipStream_t)stream,
-                     logits, ld, B, A, seed, stream_id, counter, uniforms, mode, actions,
-                     bad_rows);
+                     logits, ld, B, A, seed, stream_id, counter_add, counter_dev,
+                     (uint32_t)row_offset, uniforms, mode, actions, bad_rows);
   ACMI_LAUNCH_CHECK("acmi_sample_actions");
   return ACMI_OK;
 }

@@ -118,6 +118,23 @@ int acmi_sample_actions(const float* logits, int ld, int B, int A,
                         uint32_t seed, uint32_t stream_id, uint32_t counter,
                         const float* uniforms, int mode, int32_t* actions,
                         int32_t* bad_rows, acmi_stream_t stream);
+/* The same for rows row_offset .. row_offset+B-1 of a larger batch (the RNG
+ * key uses the global row): a batch sampled in pieces (the rollout's env
+ * halves on two streams) draws exactly the actions of one launch. */
+int acmi_sample_actions_at(const float* logits, int ld, int B, int A,
+                           uint32_t seed, uint32_t stream_id, uint32_t counter,
+                           int row_offset, const float* uniforms, int mode,
+                           int32_t* actions, int32_t* bad_rows,
+                           acmi_stream_t stream);
+/* counter = *counter_dev + counter_add (counter_dev: device uint32, nullable):
+ * a rollout captured once in a hipGraph and replayed reads its RNG counter
+ * from device memory, the host refreshing it before each replay. */
+int acmi_sample_actions_dev(const float* logits, int ld, int B, int A,
+                            uint32_t seed, uint32_t stream_id,
+                            const uint32_t* counter_dev, uint32_t counter_add,
+                            int row_offset, const float* uniforms, int mode,
+                            int32_t* actions, int32_t* bad_rows,
+                            acmi_stream_t stream);
 
 /* Per-row Categorical.entropy and log_prob(actions) (policies.py:87-89);
  * either output may be NULL (log_prob needs actions). */

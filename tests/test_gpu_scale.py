@@ -181,3 +181,35 @@ def test_full_size_updates_are_bit_identical_and_factors_well_formed(lib, cuda):
         # zero-debiased f32 EMA of two of them is 1 to within its rounding
         assert abs(m[d - 1, d - 1].item() - 1.0) < 1e-5, (f, m[d - 1, d - 1].item())
     assert torch.isfinite(p1).all()
+
+
+def test_two_stream_rollout_is_bit_identical(lib, cuda, monkeypatch):
+    """512 envs: the rollout's two env halves on two HIP streams (agents.py
+    _rollout_halves), eagerly and replayed from a captured hipGraph
+    (_rollout_graph: rollout 1 eager, 2 captured + replayed, 3 replayed), give
+    exactly the single-chain rollout: observations, actions, rewards, terminals,
+    episode rewards, next observations and every activation row, three rollouts
+    in a row (the later ones start mid-episode from auto-reset states)."""
+    from actorcritic import session as sess
+    outs = []
+    for split, graph in (('0', '0'), ('1', '0'), ('1', '1'), ('0', '1')):
+        monkeypatch.setenv('ACMI_ROLLOUT_SPLIT', split)
+        monkeypatch.setenv('ACMI_ROLLOUT_GRAPH', graph)
+        env, model, agent, obj, gs, opt, op = _bench_like()
+        got = []
+        with sess.Session() as s:
+            for _ in range(3):
+                obs, act, rew, term, nxt, info = agent.interact(s)
+                acts = agent._bufs.acts
+                got += [x.clone() for x in (obs, act, rew, term, nxt, info.episode_rewards, acts.a1, acts.a4,
+                                            acts.logits, acts.value)]
+        torch.cuda.synchronize()
+        assert agent._bufs.halves == (split == '1')
+        assert (agent._bufs.graph is not None) == (graph == '1')
+        outs.append(got)
+    for other in outs[1:]:
+        for i, (a, b) in enumerate(zip(outs[0], other)):
+            if a.is_floating_point():  # episode rewards are NaN where no episode ended
+                assert torch.equal(torch.isnan(a), torch.isnan(b)), i
+                a, b = torch.nan_to_num(a, nan=0.0), torch.nan_to_num(b, nan=0.0)
+            assert torch.equal(a, b), i
