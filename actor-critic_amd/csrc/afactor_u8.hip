@@ -203,6 +203,159 @@ __global__ __launch_bounds__(256) void conv1_afactor_i8_kernel(const uint8_t* ob
   if (diag && tid < 128) colsum[(long long)chunk * 256 + 128 * ta + tid] = csum;
 }
 
+// One block per chunk for the whole upper triangle (ACMI_GEMM_X3 mode; the
+// 3-block form above stages each row's patch bytes 4 times over its tile pairs
+// -- 512 bytes per row -- and is bound by that gather): 8 waves, all 256 patch
+// columns staged once per 64-row stage (256 bytes per row), 36 upper-triangle
+// 32x32 tiles dealt as rows (r, 7-r) to wave pairs, at most two distinct row
+// blocks per wave (kTri).  Same partial layout, so conv1_afactor_finalize is
+// shared.  40 KB of LDS, 5 x 16 accumulator registers.
+__constant__ int8_t kTri[8][5][2] = {
+    {{0, 0}, {0, 1}, {0, 2}, {0, 3}, {0, 4}}, {{0, 5}, {0, 6}, {0, 7}, {7, 7}, {-1, -1}},
+    {{1, 1}, {1, 2}, {1, 3}, {1, 4}, {1, 5}}, {{1, 6}, {1, 7}, {6, 6}, {6, 7}, {-1, -1}},
+    {{2, 2}, {2, 3}, {2, 4}, {2, 5}, {2, 6}}, {{2, 7}, {5, 5}, {5, 6}, {5, 7}, {-1, -1}},
+    {{3, 3}, {3, 4}, {3, 5}, {3, 6}, {3, 7}}, {{4, 4}, {4, 5}, {4, 6}, {4, 7}, {-1, -1}}};
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv1_afactor_i8_tri_kernel(const uint8_t* obs,
+                                                                   long long img_stride, int rows,
+                                                                   int chunk_rows, int* part,
+                                                                   int* colsum) {
+  const int total = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, base_l = total >> 3, rem = total & 7;
+  const int chunk = xcd * base_l + min(xcd, rem) + (b >> 3);
+  const int r_begin = chunk * chunk_rows;
+  const int r_end = min(rows, r_begin + chunk_rows);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2][256 * AF_LINE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  // staging map: 4 rows (4*q4 .. +3) x 8 columns (8*cg .. +7) per thread, cg < 32
+  const int q4 = tid & 15;
+  const int cg = tid >> 4;
+  const int c = 8 * cg;
+  const int coff = (((c >> 5) * AF_OBS_W) + ((c & 31) >> 2)) * 4;  // (kh, kw0) of the 8 bytes
+
+  uint2 ra[4];
+  const uint8_t* x0 = reinterpret_cast<const uint8_t*>(kX0Run);
+  const uint32_t istride = (uint32_t)img_stride;
+  auto fetch = [&](int r0) {
+    const int r = r0 + 4 * q4;
+    const bool ok = r < r_end;
+    const uint32_t rr = ok ? (uint32_t)r : (uint32_t)r_begin;
+    const uint32_t img = rr / 400u;
+    const uint32_t p = rr - img * 400u;
+    const uint32_t oh = p / 20u;
+    const uint32_t ow = p - oh * 20u;
+    const uint32_t off = img * istride + (oh * 4 * AF_OBS_W + ow * 4) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      ra[q] = *reinterpret_cast<const uint2*>(ok ? obs + (off + (uint32_t)(coff + 16 * q)) : x0);
+  };
+  auto transpose4 = [](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t* out) {
+    const uint32_t p01l = __builtin_amdgcn_perm(w1, w0, 0x05010400u);
+    const uint32_t p01h = __builtin_amdgcn_perm(w1, w0, 0x07030602u);
+    const uint32_t p23l = __builtin_amdgcn_perm(w3, w2, 0x05010400u);
+    const uint32_t p23h = __builtin_amdgcn_perm(w3, w2, 0x07030602u);
+    out[0] = __builtin_amdgcn_perm(p23l, p01l, 0x05040100u);
+    out[1] = __builtin_amdgcn_perm(p23l, p01l, 0x07060302u);
+    out[2] = __builtin_amdgcn_perm(p23h, p01h, 0x05040100u);
+    out[3] = __builtin_amdgcn_perm(p23h, p01h, 0x07060302u);
+  };
+  auto commit = [&](int buf) {
+    constexpr uint32_t F = 0x80808080u;
+    uint32_t cols[8];
+    transpose4(ra[0].x ^ F, ra[1].x ^ F, ra[2].x ^ F, ra[3].x ^ F, cols);
+    transpose4(ra[0].y ^ F, ra[1].y ^ F, ra[2].y ^ F, ra[3].y ^ F, cols + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      *reinterpret_cast<uint32_t*>(lds[buf] + (c + j) * AF_LINE + 4 * q4) = cols[j];
+  };
+
+  int ti[5], tj[5];
+  const int wu = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the table in SGPRs
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    ti[t] = kTri[wu][t][0];
+    tj[t] = kTri[wu][t][1];
+  }
+  const int ntile = tj[4] >= 0 ? 5 : 4;
+  const int row0 = ti[0];
+  int row1 = row0;  // the wave's other row block (if any)
+#pragma unroll
+  for (int t = 1; t < 5; ++t)
+    if (tj[t] >= 0 && ti[t] != row0) row1 = ti[t];
+
+  v16i acc[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0;
+  int csum = 0;
+
+  const int nst = r_end > r_begin ? (r_end - r_begin + AF_BK - 1) / AF_BK : 0;
+  if (nst > 0) {
+    fetch(r_begin);
+    commit(0);
+  }
+  __syncthreads();
+  const int half = lane >> 5;
+  auto stage = [&](int st, auto NTc) {
+    constexpr int NT = decltype(NTc)::value;
+    const int cur = st & 1;
+    fetch(r_begin + (st + 1) * AF_BK);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint8_t* S = lds[cur] + (lane & 31) * AF_LINE + 16 * half;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const v4i a0 = *reinterpret_cast<const v4i*>(S + row0 * 32 * AF_LINE + 32 * s);
+      const v4i a1 = *reinterpret_cast<const v4i*>(S + row1 * 32 * AF_LINE + 32 * s);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const v4i bb = *reinterpret_cast<const v4i*>(S + tj[t] * 32 * AF_LINE + 32 * s);
+        acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ti[t] == row0 ? a0 : a1, bb, acc[t], 0, 0, 0);
+      }
+    }
+    if (tid < 256) {  // column sums of x over the staged rows
+      const uint32_t* line = reinterpret_cast<const uint32_t*>(lds[cur] + tid * AF_LINE);
+#pragma unroll
+      for (int w = 0; w < AF_BK / 4; ++w) csum = __builtin_amdgcn_sdot4((int)line[w], 0x01010101, csum, false);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    commit(cur ^ 1);
+    __syncthreads();
+  };
+  if (ntile == 5)
+    for (int st = 0; st < nst; ++st) stage(st, std::integral_constant<int, 5>{});
+  else
+    for (int st = 0; st < nst; ++st) stage(st, std::integral_constant<int, 4>{});
+
+  int* out = part + (long long)chunk * 65536;
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    if (t >= ntile) break;
+    const int col = 32 * tj[t] + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 32 * ti[t] + (r & 3) + 8 * (r >> 2) + 4 * half;
+      out[row * 256 + col] = acc[t][r];
+    }
+  }
+  if (tid < 256) colsum[(long long)chunk * 256 + tid] = csum;
+}
+
+// chunks for the one-block-per-chunk kernel: 2 blocks per CU resident
+static void af_plan_tri(long long rows, int* nchunk, int* chunk) {
+  const long long slots = 256 * 2;
+  const long long nc0 = std::max<long long>(1, (rows + AF_CHUNK - 1) / AF_CHUNK);
+  const long long rounds = (nc0 + slots - 1) / slots;
+  const long long nc = std::max<long long>(nc0, rounds * slots);
+  long long ch = (rows + nc - 1) / nc;
+  ch = (ch + AF_BK - 1) / AF_BK * AF_BK;
+  *chunk = (int)std::max<long long>(ch, AF_BK);
+  *nchunk = (int)((rows + *chunk - 1) / *chunk);
+}
+
 // A (257 x 257, f32) from the exact integer sums; element (a, b), a,b <= 256
 __global__ void conv1_afactor_finalize(const int* part, const int* colsum, int nchunk, int rows,
                                        float* astat) {
@@ -254,16 +407,21 @@ __global__ void conv1_afactor_finalize(const int* part, const int* colsum, int n
 }
 
 long long conv1_afactor_ws_ints(long long rows) {
-  int nchunk, chunk;
+  int nchunk, chunk, nt, ct;
   af_plan(rows, &nchunk, &chunk);
-  return (long long)nchunk * (65536 + 256);
+  af_plan_tri(rows, &nt, &ct);
+  return (long long)std::max(nchunk, nt) * (65536 + 256);
 }
 
 int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* astat, int* ws,
                      long long ws_ints, hipStream_t s) {
   const long long rows = 400LL * B;
+  const bool tri = g_gemm_mode == ACMI_GEMM_X3;
   int nchunk, chunk;
-  af_plan(rows, &nchunk, &chunk);
+  if (tri)
+    af_plan_tri(rows, &nchunk, &chunk);
+  else
+    af_plan(rows, &nchunk, &chunk);
   ACMI_REQUIRE(conv1_afactor_ws_ints(rows) <= ws_ints, ACMI_ERR_WS,
                "conv1 A-factor workspace too small");
   ACMI_REQUIRE(img_stride % 8 == 0, ACMI_ERR_ARG, "conv1 A factor needs 8-byte aligned images");
@@ -271,8 +429,12 @@ int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* ast
                "conv1 A factor: frames must span < 2^32 bytes");
   int* part = ws;
   int* colsum = ws + (long long)nchunk * 65536;
-  hipLaunchKernelGGL(conv1_afactor_i8_kernel, dim3(3 * nchunk), dim3(256), 0, s, obs, img_stride,
-                     (int)rows, chunk, part, colsum);
+  if (tri)
+    hipLaunchKernelGGL(conv1_afactor_i8_tri_kernel, dim3(nchunk), dim3(512), 0, s, obs, img_stride,
+                       (int)rows, chunk, part, colsum);
+  else
+    hipLaunchKernelGGL(conv1_afactor_i8_kernel, dim3(3 * nchunk), dim3(256), 0, s, obs, img_stride,
+                       (int)rows, chunk, part, colsum);
   hipLaunchKernelGGL(conv1_afactor_finalize, dim3(cdiv(257 * 257, 256)), dim3(256), 0, s, part,
                      colsum, nchunk, (int)rows, astat);
   ACMI_LAUNCH_CHECK("conv1_afactor_u8");
