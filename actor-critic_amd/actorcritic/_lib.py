@@ -44,6 +44,13 @@ class EnvState(ctypes.Structure):
     _fields_ = [('episode', c_vp), ('step', c_vp), ('length', c_vp), ('total', c_vp), ('done', c_vp)]
 
 
+class RolloutIO(ctypes.Structure):
+    _fields_ = [('seed', c_u32), ('stream_id', c_u32), ('counter', c_u32), ('counter_dev', c_vp),
+                ('row_offset', c_int), ('actions', c_vp), ('bad_rows', c_vp), ('state', EnvState),
+                ('env_offset', c_int), ('env_seed', c_u32), ('obs_out', c_vp), ('out_stride', c_i64),
+                ('rewards', c_vp), ('terminals', c_vp), ('episode_rewards', c_vp), ('ld', c_i64)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     'acmi_last_error': (ctypes.c_char_p, []),
@@ -64,6 +71,8 @@ _SIGS = {
                                        c_vp, c_vp, c_vp]),
     'acmi_sample_actions_dev': (c_int, [c_vp, c_int, c_int, c_int, c_u32, c_u32, c_vp, c_u32, c_int, c_vp,
                                         c_int, c_vp, c_vp, c_vp]),
+    'acmi_rollout_step': (c_int, [ctypes.POINTER(Net), c_vp, c_i64, c_int, ctypes.POINTER(Acts), c_i64,
+                                  ctypes.POINTER(RolloutIO), c_vp]),
     'acmi_categorical': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     'acmi_returns': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     'acmi_a2c_loss_ws_floats': (c_i64, [c_int]),

@@ -19,6 +19,7 @@ half-batch kernels cost 70-80 % of full-batch ones, and the host keeps up.  They
 kept for hosts where launch overhead is not hidden.
 """
 
+import ctypes
 import os
 
 from abc import ABCMeta, abstractmethod
@@ -83,6 +84,7 @@ class _RolloutBuffers(object):
         need = int(_lib.load().acmi_forward_ws_floats(N // 2 if self.halves else N))
         self.ws = [torch.zeros(max(need, 1), dtype=torch.float32, device=dev) for _ in range(2)]
         self.use_graph = os.environ.get('ACMI_ROLLOUT_GRAPH', '0') == '1'
+        self.fused = os.environ.get('ACMI_ROLLOUT_FUSED', '1') != '0'
         self.graph, self.graph_key, self.warm = None, None, False
         self.ctr_dev = torch.zeros(1, dtype=torch.int32, device=dev)
 
@@ -189,7 +191,7 @@ class MultiEnvAgent(Agent):
         seed = (self._model._random_seed or 0) & 0xFFFFFFFF
         if rb.use_graph:
             self._rollout_graph(eng, env, rb, N, T, A, seed)
-        elif rb.halves:
+        elif rb.halves or rb.fused:
             self._rollout_halves(eng, env, rb, N, T, A, seed)
         else:
             rb.obs[:, 0].copy_(rb.next_obs)
@@ -229,21 +231,28 @@ def _half_step(eng, env, rb, h, N2, T, A, t, seed, dev_ctr=False):
     acts = rb.acts.view(row, T, ws_rows=N2)
     acts.ws = rb.ws[h].data_ptr()
     acts.ws_floats = rb.ws[h].numel()
-    eng.forward(src, N2, acts, want_value=True, img_stride=T * OBS_BYTES, act_stride=T)
     act_t = rb.actions_tn[t].data_ptr() + 4 * n0
     if dev_ctr:
         ctr_dev, ctr = _lib.c_vp(rb.ctr_dev.data_ptr()), t
     else:
         ctr_dev, ctr = None, eng.sample_counter & 0xFFFFFFFF
-    _lib.call('acmi_sample_actions_dev', _lib.c_vp(rb.acts.logits.data_ptr() + 4 * row * A), T * A, N2, A,
-              seed, eng.rank, ctr_dev, ctr, n0, None, 0, _lib.c_vp(act_t),
-              _lib.c_vp(eng._bad_rows.data_ptr()), eng.stream())
     if t + 1 < T:
         dst, dstride = src + OBS_BYTES, T * OBS_BYTES
     else:
         dst, dstride = rb.next_obs.data_ptr() + n0 * OBS_BYTES, OBS_BYTES
-    env.step_range_into(n0, N2, act_t, src, T * OBS_BYTES, dst, dstride, rb.rewards.data_ptr() + 4 * row,
-                        rb.terminals.data_ptr() + row, rb.episode_rewards.data_ptr() + 4 * row, T)
+    rew, term, ep = rb.rewards.data_ptr() + 4 * row, rb.terminals.data_ptr() + row, \
+        rb.episode_rewards.data_ptr() + 4 * row
+    if rb.fused:  # tower + fused heads/sample/env-step tail (acmi_rollout_step)
+        io = _lib.RolloutIO(seed, eng.rank, ctr, ctr_dev, n0, act_t, eng._bad_rows.data_ptr(), env.range_state(n0),
+                            env.env_offset + n0, env.seed, dst, dstride, rew, term, ep, T)
+        _lib.call('acmi_rollout_step', ctypes.byref(eng.net()), ctypes.c_void_p(src), T * OBS_BYTES, N2,
+                  ctypes.byref(acts), T, ctypes.byref(io), eng.stream())
+        return
+    eng.forward(src, N2, acts, want_value=True, img_stride=T * OBS_BYTES, act_stride=T)
+    _lib.call('acmi_sample_actions_dev', _lib.c_vp(rb.acts.logits.data_ptr() + 4 * row * A), T * A, N2, A,
+              seed, eng.rank, ctr_dev, ctr, n0, None, 0, _lib.c_vp(act_t),
+              _lib.c_vp(eng._bad_rows.data_ptr()), eng.stream())
+    env.step_range_into(n0, N2, act_t, src, T * OBS_BYTES, dst, dstride, rew, term, ep, T)
 
 
 def transpose_list(values):

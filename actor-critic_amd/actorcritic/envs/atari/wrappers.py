@@ -98,9 +98,10 @@ class SyntheticAtariEnvs(object):
                   out_stride, ctypes.c_void_p(rew_ptr), ctypes.c_void_p(term_ptr), ctypes.c_void_p(ep_ptr), ld,
                   self._stream())
 
-    def step_range_into(self, n0, n, actions_ptr, obs_in_ptr, in_stride, obs_out_ptr, out_stride, rew_ptr,
-                        term_ptr, ep_ptr, ld):
-        """step_into for envs n0 .. n0+n-1 only (every pointer already at env n0)."""
+    def range_state(self, n0):
+        """EnvState of envs n0.. (pointers at env n0)."""
+        if n0 == 0:
+            return self.state
         if not hasattr(self, '_range_states'):
             self._range_states = {}
         st = self._range_states.get(n0)
@@ -109,6 +110,12 @@ class SyntheticAtariEnvs(object):
                                self._length[n0:].data_ptr(), self._total[n0:].data_ptr(),
                                self._done[n0:].data_ptr())
             self._range_states[n0] = st
+        return st
+
+    def step_range_into(self, n0, n, actions_ptr, obs_in_ptr, in_stride, obs_out_ptr, out_stride, rew_ptr,
+                        term_ptr, ep_ptr, ld):
+        """step_into for envs n0 .. n0+n-1 only (every pointer already at env n0)."""
+        st = self.range_state(n0)
         _lib.call('acmi_env_step', ctypes.byref(st), n, self.env_offset + n0, self.seed,
                   ctypes.c_void_p(actions_ptr), ctypes.c_void_p(obs_in_ptr), in_stride, ctypes.c_void_p(obs_out_ptr),
                   out_stride, ctypes.c_void_p(rew_ptr), ctypes.c_void_p(term_ptr), ctypes.c_void_p(ep_ptr), ld,

@@ -16,6 +16,7 @@
 #include "gemm.hpp"
 #include "gemm3.hpp"
 #include "conv1u8.hpp"
+#include "stepper.hpp"
 
 namespace acmi {
 
@@ -144,6 +145,77 @@ struct EpiAct {
 };
 
 
+// Fused rollout tail (acmi_rollout_step): one workgroup per env b -- a4 from
+// fc4's split-K slabs (or as stored), the A+1 heads, the categorical draw and
+// the env step, with the arithmetic of heads_kernel / sample_kernel /
+// env_step_kernel (same per-element orders), so the fused step is bit-identical
+// to the three launches it replaces.
+struct TailArgs {
+  acmi_rollout_io_t io;
+  const uint8_t* obs;
+  long long img_stride;
+};
+constexpr int kMaxHeads = 32;
+template <int NZ>
+__global__ __launch_bounds__(256) void rollout_tail_kernel(
+    const float* part, int nz, const float* b4, float* a4, long long a4_stride, int B,
+    const float* wpi, const float* bpi, const float* wv, const float* bv, int A, float* logits,
+    long long l_stride, float* value, long long v_stride, TailArgs ta) {
+  const int row = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ float sx[512];
+  __shared__ float sl[kMaxHeads];
+  __shared__ int s_action;
+  float* x = a4 + (long long)row * a4_stride;
+  for (int j = threadIdx.x; j < 512; j += 256) {
+    float v;
+    if (NZ > 0) {
+      const long long zs = (long long)(B + 1) * 512;
+      float acc = 0.f;
+#pragma unroll
+      for (int z = 0; z < NZ; ++z) acc += part[z * zs + (long long)row * 512 + j];
+      v = fmaxf(acc + b4[j], 0.f);
+      x[j] = v;
+    } else {
+      v = x[j];
+    }
+    sx[j] = v;
+  }
+  __syncthreads();
+  float xv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) xv[e] = sx[lane + 64 * e];
+  for (int a = wave; a <= A; a += 4) {  // head a (a == A: the value head)
+    float s = 0.f;
+    if (a < A) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += xv[e] * wpi[(lane + 64 * e) * A + a];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += xv[e] * wv[lane + 64 * e];
+    }
+    s = wave_sum(s);
+    if (lane == 0) sl[a] = s + (a < A ? bpi[a] : bv[0]);
+  }
+  __syncthreads();
+  const acmi_rollout_io_t& io = ta.io;
+  if (threadIdx.x == 0) {
+    for (int a = 0; a < A; ++a) logits[(long long)row * l_stride + a] = sl[a];
+    if (value) value[(long long)row * v_stride] = sl[A];
+    const uint32_t ctr = io.counter + (io.counter_dev ? *io.counter_dev : 0u);
+    bool bad;
+    const int y = sample_row(sl, A, io.seed, io.stream_id, ctr, (uint32_t)(row + io.row_offset),
+                             nullptr, 0, &bad);
+    if (bad) atomicAdd(io.bad_rows, 1);
+    io.actions[row] = y;
+    s_action = y;
+  }
+  __syncthreads();
+  env_step_block(io.state, row, (uint32_t)(io.env_offset + row), io.env_seed, (uint32_t)s_action,
+                 ta.obs + (long long)row * ta.img_stride, io.obs_out + (long long)row * io.out_stride,
+                 io.rewards, io.terminals, io.episode_rewards, io.ld);
+}
+
 inline int roundup4(int x) { return (x + 3) & ~3; }
 
 // policy/value heads, one wave per row: the 512-long dot products of a4 with
@@ -215,7 +287,7 @@ template <int C3>
 static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
                         long long img_stride, int B, const acmi_acts_t* a,
                         int want_value, long long act_img_stride,
-                        hipStream_t s) {
+                        hipStream_t s, const TailArgs* tail = nullptr) {
   // act_img_stride: images between consecutive batch rows in the activation
   // buffers (1 = contiguous; T = rollout step t of an env-major buffer).
   const long long st = act_img_stride;
@@ -270,10 +342,15 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   const dim3 hg(cdiv(B, 4)), hb(256);
   const float* hp = split ? a->ws : nullptr;
   float* hv = want_value ? a->value : nullptr;
-#define ACMI_HEADS(NZ)                                                                        \
-  hipLaunchKernelGGL(heads_kernel<NZ>, hg, hb, 0, s, hp, nz, P + L.off[7], a->a4, st * 512, B, \
-                     P + L.off[8], P + L.off[9], P + L.off[10], P + L.off[11], L.A, a->logits, \
-                     st * a->ld_logits, hv, st)
+#define ACMI_HEADS(NZ)                                                                          \
+  if (tail)                                                                                     \
+    hipLaunchKernelGGL(rollout_tail_kernel<NZ>, dim3(B), hb, 0, s, hp, nz, P + L.off[7], a->a4,  \
+                       st * 512, B, P + L.off[8], P + L.off[9], P + L.off[10], P + L.off[11],    \
+                       L.A, a->logits, st * a->ld_logits, hv, st, *tail);                        \
+  else                                                                                          \
+    hipLaunchKernelGGL(heads_kernel<NZ>, hg, hb, 0, s, hp, nz, P + L.off[7], a->a4, st * 512, B, \
+                       P + L.off[8], P + L.off[9], P + L.off[10], P + L.off[11], L.A, a->logits, \
+                       st * a->ld_logits, hv, st)
   switch (split ? nz : 0) {
     case 0: ACMI_HEADS(0); break;
     case 2: ACMI_HEADS(2); break;
@@ -856,7 +933,8 @@ static bool spans32(long long rows, long long stride, long long per_row) {
 
 static int forward_dispatch(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride,
                             int B, const acmi_acts_t* acts, int want_value,
-                            long long act_stride, acmi_stream_t stream) {
+                            long long act_stride, acmi_stream_t stream,
+                            const TailArgs* tail = nullptr) {
   Layout L;
   ACMI_REQUIRE(net && acts && obs && net->params, ACMI_ERR_ARG, "acmi_forward: null argument");
   ACMI_REQUIRE(make_layout(net->num_actions, net->conv3_filters, &L), ACMI_ERR_ARG,
@@ -872,8 +950,8 @@ static int forward_dispatch(const acmi_net_t* net, const uint8_t* obs, int64_t i
   if (B == 0) return ACMI_OK;
   hipStream_t s = (hipStream_t)stream;
   if (L.C3 == 32)
-    return forward_impl<32>(L, net->params, obs, img_stride, B, acts, want_value, act_stride, s);
-  return forward_impl<64>(L, net->params, obs, img_stride, B, acts, want_value, act_stride, s);
+    return forward_impl<32>(L, net->params, obs, img_stride, B, acts, want_value, act_stride, s, tail);
+  return forward_impl<64>(L, net->params, obs, img_stride, B, acts, want_value, act_stride, s, tail);
 }
 
 int acmi_forward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,
@@ -887,6 +965,18 @@ int acmi_forward_strided(const acmi_net_t* net, const uint8_t* obs, int64_t img_
                          const acmi_acts_t* acts, int want_value, int64_t act_img_stride,
                          acmi_stream_t stream) {
   return forward_dispatch(net, obs, img_stride, B, acts, want_value, act_img_stride, stream);
+}
+
+int acmi_rollout_step(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,
+                      const acmi_acts_t* acts, int64_t act_img_stride, const acmi_rollout_io_t* io,
+                      acmi_stream_t stream) {
+  ACMI_REQUIRE(io && io->actions && io->bad_rows && io->obs_out && io->rewards && io->terminals &&
+                   io->episode_rewards && io->ld >= 1 && io->out_stride % 16 == 0 &&
+                   img_stride % 16 == 0 && io->row_offset >= 0 && net &&
+                   net->num_actions < kMaxHeads,
+               ACMI_ERR_ARG, "acmi_rollout_step: bad arguments");
+  TailArgs ta{*io, obs, (long long)img_stride};
+  return forward_dispatch(net, obs, img_stride, B, acts, 1, act_img_stride, stream, &ta);
 }
 
 int64_t acmi_forward_ws_floats(int B) {

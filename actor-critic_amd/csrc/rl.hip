@@ -5,6 +5,7 @@
 #include <math.h>
 
 #include "common.hpp"
+#include "stepper.hpp"
 
 namespace acmi {
 
@@ -21,34 +22,10 @@ __global__ void sample_kernel(const float* logits, int ld, int B, int A, uint32_
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= B) return;
   if (ctr_dev) ctr += *ctr_dev;
-  const float* z = logits + (long long)m * ld;
-  float mx = -INFINITY;
-  bool finite = true;
-  int amax = 0;
-  for (int a = 0; a < A; ++a) {
-    const float v = z[a];
-    finite = finite && isfinite(v);
-    if (v > mx) { mx = v; amax = a; }
-  }
-  if (!finite) {
-    actions[m] = -1;
-    atomicAdd(bad, 1);
-    return;
-  }
-  if (mode) {
-    actions[m] = amax;  // first maximal index, like argmax
-    return;
-  }
-  float se = 0.f;
-  for (int a = 0; a < A; ++a) se += expf(z[a] - mx);
-  const float u = uniforms ? uniforms[m] : u01(key4(seed, sid, ctr, (uint32_t)m + row_offset));
-  const float target = u * se;
-  float c = 0.f;
-  int y = A - 1;
-  for (int a = 0; a < A; ++a) {
-    c += expf(z[a] - mx);
-    if (target < c) { y = a; break; }
-  }
+  bool bad_row;
+  const int y = sample_row(logits + (long long)m * ld, A, seed, sid, ctr, (uint32_t)m + row_offset,
+                           uniforms ? uniforms + m : nullptr, mode, &bad_row);
+  if (bad_row) atomicAdd(bad, 1);
   actions[m] = y;
 }
 
@@ -261,20 +238,6 @@ __global__ void rmsprop_kernel(float* p, float* ms, float* mom, const float* g, 
 // batched synthetic Atari stepper (multi_env.py:121-137 + wrappers.py:201-235
 // + wrappers.py:263-323).  One workgroup per env; 1764 words of 4 pixels.
 // ---------------------------------------------------------------------------
-constexpr int FRAME_WORDS = 84 * 84 / 4;
-constexpr uint32_t RESET_TAG = 0xFFFFFFFFu;
-constexpr uint32_t LEN_TAG = 0xFFFFFFFEu;
-constexpr uint32_t REW_SALT = 0x85EBCA6Bu;
-constexpr uint32_t REW_LO = 838861u;      // round(0.05 * 2^24)
-constexpr uint32_t REW_HI = 15938355u;    // 2^24 - REW_LO
-
-__device__ __forceinline__ uint32_t word_hash(uint32_t base, uint32_t g) {
-  return mix32(base ^ (g * 0x9E3779B9u));
-}
-__device__ __forceinline__ int32_t episode_length(uint32_t seed, uint32_t e, uint32_t k) {
-  return 50 + (int32_t)(key4(seed, e, k, LEN_TAG) % 451u);
-}
-
 __global__ __launch_bounds__(256) void env_reset_kernel(acmi_env_state_t st, int env_offset,
                                                         uint32_t seed, uint8_t* obs,
                                                         long long stride) {
@@ -305,61 +268,9 @@ __global__ __launch_bounds__(256) void env_step_kernel(
     const uint8_t* obs_in, long long in_stride, uint8_t* obs_out, long long out_stride,
     float* rewards, uint8_t* terminals, float* ep_rewards, long long ld) {
   const int n = blockIdx.x;
-  const uint32_t e = (uint32_t)(env_offset + n);
-  // every thread reads the (pre-step) state, then a barrier before thread 0
-  // writes the new state
-  const bool was_done = st.done[n] != 0;
-  int32_t k = st.episode[n];
-  int32_t t = st.step[n];
-  int32_t L = st.length[n];
-  float total = st.total[n];
-  __syncthreads();
-  if (was_done) {  // _AutoResetWrapper: reset lazily at the next step
-    k += 1;
-    t = 0;
-    L = episode_length(seed, e, (uint32_t)k);
-    total = 0.f;
-  }
-  t += 1;
-  const uint32_t a = (uint32_t)actions[n] & 255u;
-  const uint32_t base = key4(seed, e, (uint32_t)k, (uint32_t)t * 256u + a);
-  const uint32_t rh = mix32(base ^ REW_SALT) >> 8;
-  const float rew = rh < REW_LO ? -1.f : (rh >= REW_HI ? 1.f : 0.f);
-  const bool term = t >= L;
-  const uint32_t rbase = key4(seed, e, (uint32_t)k, RESET_TAG);
-  const uint4* in = reinterpret_cast<const uint4*>(obs_in + (long long)n * in_stride);
-  uint4* out = reinterpret_cast<uint4*>(obs_out + (long long)n * out_stride);
-  for (int g = threadIdx.x; g < FRAME_WORDS; g += blockDim.x) {
-    uint4 old;
-    if (was_done) {  // FrameStackWrapper.reset: the reset frame repeated 4x
-      const uint32_t w = word_hash(rbase, (uint32_t)g);
-      old.x = (w & 255u) * 0x01010101u;
-      old.y = ((w >> 8) & 255u) * 0x01010101u;
-      old.z = ((w >> 16) & 255u) * 0x01010101u;
-      old.w = (w >> 24) * 0x01010101u;
-    } else {
-      old = in[g];
-    }
-    const uint32_t f = word_hash(base, (uint32_t)g);
-    // np.roll(stack, -1, axis=-1); zero-fill on terminal; last channel = frame
-    uint4 o;
-    o.x = (term ? 0u : (old.x >> 8)) | ((f & 255u) << 24);
-    o.y = (term ? 0u : (old.y >> 8)) | (((f >> 8) & 255u) << 24);
-    o.z = (term ? 0u : (old.z >> 8)) | (((f >> 16) & 255u) << 24);
-    o.w = (term ? 0u : (old.w >> 8)) | ((f >> 24) << 24);
-    out[g] = o;
-  }
-  if (threadIdx.x == 0) {
-    total += rew;
-    rewards[n * ld] = rew;
-    terminals[n * ld] = term ? 1 : 0;
-    ep_rewards[n * ld] = term ? total : __int_as_float(0x7fc00000);
-    st.episode[n] = k;
-    st.step[n] = t;
-    st.length[n] = L;
-    st.total[n] = term ? 0.f : total;
-    st.done[n] = term ? 1 : 0;
-  }
+  env_step_block(st, n, (uint32_t)(env_offset + n), seed, (uint32_t)actions[n],
+                 obs_in + (long long)n * in_stride, obs_out + (long long)n * out_stride, rewards,
+                 terminals, ep_rewards, ld);
 }
 
 }  // namespace acmi

@@ -320,6 +320,34 @@ int acmi_forward_strided(const acmi_net_t* net, const uint8_t* obs,
                          int want_value, int64_t act_img_stride,
                          acmi_stream_t stream);
 
+/* One whole rollout step (MultiEnvAgent.interact's loop body, agents.py:
+ * 199-219: sample_actions + MultiEnv.step) in two launch groups: the tower
+ * of acmi_forward_strided up to fc4, then ONE fused kernel per env (one
+ * workgroup each) that finalises a4, computes the heads, samples the action
+ * (acmi_sample_actions_dev semantics, row = io->row_offset + b) and steps the
+ * env (acmi_env_step semantics, reading the same frames `obs`).  Bit-identical
+ * to acmi_forward_strided + acmi_sample_actions_dev + acmi_env_step. */
+typedef struct acmi_rollout_io {
+  uint32_t seed, stream_id, counter; /* sampler RNG key                      */
+  const uint32_t* counter_dev;       /* nullable: counter += *counter_dev     */
+  int row_offset;                    /* global row of batch row 0            */
+  int32_t* actions;                  /* [B] out                              */
+  int32_t* bad_rows;                 /* device counter of non-finite rows    */
+  acmi_env_state_t state;            /* env state of batch row 0's env       */
+  int env_offset;                    /* global env id of batch row 0         */
+  uint32_t env_seed;
+  uint8_t* obs_out;                  /* next stacked frames, env b at b*out_stride */
+  int64_t out_stride;
+  float* rewards;                    /* element b at [b*ld]                  */
+  uint8_t* terminals;
+  float* episode_rewards;
+  int64_t ld;
+} acmi_rollout_io_t;
+int acmi_rollout_step(const acmi_net_t* net, const uint8_t* obs,
+                      int64_t img_stride, int B, const acmi_acts_t* acts,
+                      int64_t act_img_stride, const acmi_rollout_io_t* io,
+                      acmi_stream_t stream);
+
 /* ------------------------------------------------------------------------
  * Building blocks exposed for parity tests and the bench (not needed by a
  * reference-shaped caller).

@@ -184,17 +184,20 @@ def test_full_size_updates_are_bit_identical_and_factors_well_formed(lib, cuda):
 
 
 def test_two_stream_rollout_is_bit_identical(lib, cuda, monkeypatch):
-    """512 envs: the rollout's two env halves on two HIP streams (agents.py
-    _rollout_halves), eagerly and replayed from a captured hipGraph
+    """512 envs: the fused rollout step (acmi_rollout_step: tower + one
+    heads/sample/env-step kernel), the rollout's two env halves on two HIP streams
+    (agents.py _rollout_halves), eagerly and replayed from a captured hipGraph
     (_rollout_graph: rollout 1 eager, 2 captured + replayed, 3 replayed), give
-    exactly the single-chain rollout: observations, actions, rewards, terminals,
+    exactly the three-launch single-chain rollout: observations, actions, rewards, terminals,
     episode rewards, next observations and every activation row, three rollouts
     in a row (the later ones start mid-episode from auto-reset states)."""
     from actorcritic import session as sess
     outs = []
-    for split, graph in (('0', '0'), ('1', '0'), ('1', '1'), ('0', '1')):
+    for split, graph, fused in (('0', '0', '0'), ('0', '0', '1'), ('1', '0', '0'), ('1', '0', '1'),
+                                ('1', '1', '1'), ('0', '1', '1')):
         monkeypatch.setenv('ACMI_ROLLOUT_SPLIT', split)
         monkeypatch.setenv('ACMI_ROLLOUT_GRAPH', graph)
+        monkeypatch.setenv('ACMI_ROLLOUT_FUSED', fused)
         env, model, agent, obj, gs, opt, op = _bench_like()
         got = []
         with sess.Session() as s:
