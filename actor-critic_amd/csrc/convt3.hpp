@@ -1,0 +1,186 @@
+// Conv input gradient (transposed conv over all stride phases) on bf16x3 with
+// the dY im2col served from LDS.
+//
+// gemm3_kernel runs dX as C[(phase, ci)][super-pixel] = sum_k W(k, i) dY(k, j)
+// with B = RowsAsK<ConvTRows>: every column re-gathers its KHP x KWP dY pixels
+// from L2 (conv3: 9 taps -> each dY value read 9 times) and every 128-column
+// tile re-reads all the weights -- 1.4-2 GB of L2 traffic per launch, gather
+// bound at ~5 TB/s.  Here a block takes all NI rows and NJ super-pixel columns:
+//   * the dY of the (at most NIMG) images its columns touch is copied ONCE into
+//     LDS as f32 ([pixel][COUT], 16-byte chunks XOR-swizzled by pixel so the
+//     fragment reads of 16 lanes at different pixels are bank-conflict free),
+//     plus one zero pixel for taps that fall outside the image;
+//   * the K loop streams only the weights (three-way split at the commit into
+//     gemm3's k-contiguous image, ds_read_b128 fragments);
+//   * a lane's B fragment (8 consecutive k = 8 channels of one tap of its
+//     column) is two ds_read_b128 of its dY pixel, split into h/m/l on the fly.
+// Same arithmetic as gemm3 (six bf16 MFMAs per 32x32x16), same epilogue
+// (EpiConvT through the LDS transpose).
+#pragma once
+
+#include "gemm3.hpp"
+
+namespace acmi {
+
+template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ>
+struct ConvTX3 {
+  static constexpr int PH = IH / S, PW = IW / S, L = PH * PW;
+  static constexpr int OH = (IH - KH) / S + 1, OW = (IW - KW) / S + 1, OP = OH * OW;
+  static constexpr int KHP = KH / S, KWP = KW / S;
+  static constexpr int K = KHP * KWP * COUT;
+  static constexpr int NI = S * S * CIN;
+  static constexpr int WM = NI / 64, WN = 4 / WM;  // waves over rows / columns
+  static constexpr int WCOLS = NJ / WN;            // columns per wave
+  static constexpr int TN = WCOLS / 32;            // 32-column blocks per wave
+  static constexpr int NIMG = (NJ - 1) / L + 2;    // images a block's columns can touch
+  static constexpr int CH = COUT / 4;              // 16-byte chunks per dY pixel
+  static constexpr int PIXW = 256 / (COUT * 4) > 0 ? 256 / (COUT * 4) : 1;  // pixels per bank window
+  static constexpr int ZP = NIMG * OP;             // the zero pixel
+  static constexpr int DY_BYTES = (ZP + 1) * COUT * 4;
+  using IA = X3Image<true, NI, 16>;
+  static constexpr int LDS_BYTES = DY_BYTES + 2 * IA::BYTES;
+  static_assert(NI % 64 == 0 && 4 % WM == 0 && NJ % (32 * WN) == 0 && COUT % 16 == 0, "shape");
+  static_assert(IH % S == 0 && IW % S == 0 && KH % S == 0 && KW % S == 0, "phases");
+  __device__ __forceinline__ static int chunk_pos(int p, int c) {
+    return p * (COUT * 4) + 16 * (c ^ ((p / PIXW) & (CH - 1)));
+  }
+};
+
+template <class CT>
+constexpr int convt_x3_blocks_per_cu() {
+  return std::min(8, 160 * 1024 / CT::LDS_BYTES);
+}
+
+template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, class Epi>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    convt_x3_blocks_per_cu<ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ>>())))
+void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi) {
+  using CT = ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ>;
+  using IA = typename CT::IA;
+  using W = ConvTWeights<KH, KW, S, CIN, COUT>;
+  constexpr int NI = CT::NI, K = CT::K, L = CT::L;
+  constexpr int NA = NI * 16 / 4 / 256;  // weight float4 runs per thread per K-tile
+  __shared__ __attribute__((aligned(16))) char lds[CT::LDS_BYTES];
+  char* dimg = lds;
+  char* abuf = lds + CT::DY_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / CT::WN, wn = wave - wm * CT::WN;
+  const int J = B * L;
+  const int j0 = blockIdx.x * NJ;
+  const int img_lo = j0 / L;
+  const int img_hi = min(B - 1, (j0 + NJ - 1) / L);
+
+  // weights: gemm3's k-contiguous staging (one ConvTWeights run per thread)
+  const W opA{w};
+  typename W::R rowA[NA];
+#pragma unroll
+  for (int v = 0; v < NA; ++v) rowA[v] = opA.row((tid + 256 * v) / 4);
+  StF4 ra[NA];
+  auto fetch = [&](int k0) {
+    const int k = k0 + (tid % 4) * 4;
+    const auto c = opA.col(k);
+#pragma unroll
+    for (int v = 0; v < NA; ++v) ra[v] = opA.stage(rowA[v], c, k < K);
+  };
+  auto commit = [&](int buf) {
+    char* As = abuf + buf * IA::BYTES;
+#pragma unroll
+    for (int v = 0; v < NA; ++v) {
+      const int idx = tid + 256 * v;
+      const int i = idx / 4;
+      IA::write(As, (idx - i * 4) * 4, i, finish(ra[v]));
+    }
+  };
+
+  fetch(0);
+  // dY of images img_lo..img_hi (contiguous [img][OH][OW][COUT]) + the zero pixel
+  {
+    const int n4 = (img_hi - img_lo + 1) * CT::OP * CT::CH;
+    const float4* src = reinterpret_cast<const float4*>(dy + (long long)img_lo * CT::OP * COUT);
+    for (int e = tid; e < n4; e += 256) {
+      const int p = e / CT::CH, c = e - p * CT::CH;
+      *reinterpret_cast<float4*>(dimg + CT::chunk_pos(p, c)) = src[e];
+    }
+    for (int c = tid; c < CT::CH; c += 256)
+      *reinterpret_cast<float4*>(dimg + CT::ZP * COUT * 4 + 16 * c) = f4zero();
+  }
+  commit(0);
+
+  // per column block: the lane's super-pixel (image relative to img_lo, ih', iw')
+  int cimg[CT::TN], cih[CT::TN], ciw[CT::TN];
+  bool cok[CT::TN];
+#pragma unroll
+  for (int t = 0; t < CT::TN; ++t) {
+    const int j = j0 + wn * CT::WCOLS + 32 * t + (lane & 31);
+    cok[t] = j < J;
+    const int jj = cok[t] ? j : j0;
+    const int img = jj / L, p = jj - img * L;
+    cimg[t] = img - img_lo;
+    cih[t] = p / CT::PW;
+    ciw[t] = p - cih[t] * CT::PW;
+  }
+  const int kh8 = 8 * (lane >> 5);
+  int aoff[2];
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm) aoff[tm] = IA::frag_off(lane, 0, wm * 64 + 32 * tm);
+
+  f32x16 acc[2][CT::TN];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < CT::TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  __syncthreads();
+
+  constexpr int NK = K / 16;
+  for (int ks = 0; ks < NK; ++ks) {
+    const int cur = ks & 1;
+    fetch((ks + 1) * 16);
+    __builtin_amdgcn_sched_barrier(0);
+    const char* As = abuf + cur * IA::BYTES;
+    bf16x8 a[2][3];
+#pragma unroll
+    for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm) a[tm][pt] = IA::frag(As + pt * IA::PART, aoff[tm]);
+    // this lane's 8 k: channels co..co+7 of tap (khp, kwp)
+    const int k0 = 16 * ks + kh8;
+    const int tap = k0 / COUT, co = k0 - tap * COUT;
+    const int khp = tap / CT::KWP, kwp = tap - khp * CT::KWP;
+#pragma unroll
+    for (int tn = 0; tn < CT::TN; ++tn) {
+      const int oh = cih[tn] - khp, ow = ciw[tn] - kwp;
+      const bool ok = cok[tn] & (oh >= 0) & (ow >= 0) & (oh < CT::OH) & (ow < CT::OW);
+      const int p = ok ? cimg[tn] * CT::OP + oh * CT::OW + ow : CT::ZP;
+      const float4 x0 = *reinterpret_cast<const float4*>(dimg + CT::chunk_pos(p, co / 4));
+      const float4 x1 = *reinterpret_cast<const float4*>(dimg + CT::chunk_pos(p, co / 4 + 1));
+      uint4 h, m, l;
+      split3(x0.x, x0.y, h.x, m.x, l.x);
+      split3(x0.z, x0.w, h.y, m.y, l.y);
+      split3(x1.x, x1.y, h.z, m.z, l.z);
+      split3(x1.z, x1.w, h.w, m.w, l.w);
+      const bf16x8 b[3] = {__builtin_bit_cast(bf16x8, h), __builtin_bit_cast(bf16x8, m),
+                           __builtin_bit_cast(bf16x8, l)};
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm) acc[tm][tn] = mfma_x3(a[tm], b, acc[tm][tn]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (ks + 1 < NK) commit(cur ^ 1);
+    __syncthreads();
+  }
+  // epilogue through the LDS transpose (the dY image is free now)
+  store_tile_lds<2, CT::TN>(epi, acc, wm * 64, j0 + wn * CT::WCOLS, lane,
+                            reinterpret_cast<float*>(lds) + wave * 32 * 36, NI, J);
+}
+
+template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, class Epi>
+inline void launch_convt_x3(const float* w, const float* dy, int B, const Epi& e, hipStream_t s) {
+  using CT = ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ>;
+  static_assert(CT::DY_BYTES >= 4 * 32 * 36 * 4, "epilogue transpose needs the dY region");
+  hipLaunchKernelGGL((convt_x3_kernel<IH, IW, KH, KW, S, CIN, COUT, NJ, Epi>), dim3(cdiv(B * CT::L, NJ)),
+                     dim3(256), 0, s, w, dy, B, e);
+}
+
+}  // namespace acmi

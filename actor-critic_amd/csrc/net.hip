@@ -16,6 +16,7 @@
 #include "gemm.hpp"
 #include "gemm3.hpp"
 #include "conv1u8.hpp"
+#include "convt3.hpp"
 #include "stepper.hpp"
 
 namespace acmi {
@@ -269,6 +270,16 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* part, int nz, c
     s = wave_sum(s);
     if (lane == 0) value[(long long)row * v_stride] = s + bv[0];
   }
+}
+
+// conv input gradients with the dY im2col in LDS (convt3.hpp): ACMI_CONVT =
+// 1 (default) conv3 only; 0 off (gemm3 over ConvTRows); 2 / 3 conv2 too, with
+// 128- / 64-column blocks.  Measured (M = 10240, per launch): conv3 231 -> 190
+// us; conv2 449 us on gemm3 vs 939 / slower here -- its f32 dY image (3 images x
+// 81 px x 64 ch) leaves one block per CU.
+static int convt_lds() {
+  static const int v = getenv("ACMI_CONVT") ? atoi(getenv("ACMI_CONVT")) : 1;
+  return v;
 }
 
 // split factor for fc4 at small batch (64 x 128 tiles over 512 columns)
@@ -762,7 +773,10 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     W opA{P + L.off[4]};
     RowsAsK<Src> opB{Src{bw->d3, B * Src::L}};
     EpiConvT<9, 9, 1, 64> epi{bw->d2, a->a2};
-    launch_mm<64, 128, 16, 1, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
+    if (g_gemm_mode == ACMI_GEMM_X3 && convt_lds())
+      launch_convt_x3<9, 9, 3, 3, 1, 64, C3, 256>(P + L.off[4], bw->d3, B, epi, s);
+    else
+      launch_mm<64, 128, 16, 1, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
   }
   {  // conv2 -> d1 (stride 2: the four phases of a 2x2 super-pixel are the
      // 4 x 32 rows of one product over the 10x10 super-pixels)
@@ -772,7 +786,12 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     RowsAsK<Src> opB{Src{bw->d2, B * Src::L}};
     EpiConvT<20, 20, 2, 32> epi{bw->d1, a->a1};
     prof_begin(ACMI_PROF_CONV2_DX, s);
-    launch_mm<128, 128, 16, 2, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
+    if (g_gemm_mode == ACMI_GEMM_X3 && convt_lds() == 2)
+      launch_convt_x3<20, 20, 4, 4, 2, 32, 64, 128>(P + L.off[2], bw->d2, B, epi, s);
+    else if (g_gemm_mode == ACMI_GEMM_X3 && convt_lds() == 3)
+      launch_convt_x3<20, 20, 4, 4, 2, 32, 64, 64>(P + L.off[2], bw->d2, B, epi, s);
+    else
+      launch_mm<128, 128, 16, 2, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
     prof_end(ACMI_PROF_CONV2_DX, s);
   }
   ACMI_LAUNCH_CHECK("dx_chain");
