@@ -17,6 +17,7 @@
 #include "gemm3.hpp"
 #include "conv1u8.hpp"
 #include "convt3.hpp"
+#include "convfwd3.hpp"
 #include "stepper.hpp"
 
 namespace acmi {
@@ -282,6 +283,16 @@ static int convt_lds() {
   return v;
 }
 
+// conv forward with the im2col in LDS (convfwd3.hpp): ACMI_CONVF = 1 (default)
+// conv3 only, 0 off, 2 conv1 and conv2 too.  Measured at 512 images per launch:
+// conv3 18.7 us (vs 19.6 on the f32 128x32 tile), conv1 26.5 (= conv1_fwd_x3),
+// conv2 82 (vs 30 on gemm3: its 51 KB image + 48 KB weight stages leave one
+// block per CU; with 16-row stages 50).
+static int convf_lds() {
+  static const int v = getenv("ACMI_CONVF") ? atoi(getenv("ACMI_CONVF")) : 1;
+  return v;
+}
+
 // split factor for fc4 at small batch (64 x 128 tiles over 512 columns)
 static void fc4_plan(int B, int K, int* nz, int* chunk) {
   const int blocks = cdiv(B, 64) * 4;
@@ -307,7 +318,10 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     MatI<true> w{P + L.off[0], 32, 256, 32};
     EpiAct epi{a->a1, P + L.off[1], 32, 400, st * 400 * 32, 1.0f / 255.0f};
     prof_begin(ACMI_PROF_CONV1_FWD, s);
-    launch_conv1_fwd_u8<32>(Src{obs, (uint32_t)img_stride, B * 400}, w, epi, B * 400, 256, s);
+    if (g_gemm_mode == ACMI_GEMM_X3 && convf_lds() == 2)
+      launch_convf_x3<uint8_t, 84, 84, 4, 8, 8, 4, 32, 1, 64>(obs, img_stride, B, P + L.off[0], epi, s);
+    else
+      launch_conv1_fwd_u8<32>(Src{obs, (uint32_t)img_stride, B * 400}, w, epi, B * 400, 256, s);
     prof_end(ACMI_PROF_CONV1_FWD, s);
   }
   {  // conv2: -> [B,9,9,64]
@@ -315,7 +329,9 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     RowsAsK<Src> opA{Src{a->a1, (uint32_t)(st * 400 * 32), B * 81}};
     MatI<true> opB{P + L.off[2], 64, 512, 64};
     EpiAct epi{a->a2, P + L.off[3], 64, 81, st * 81 * 64};
-    if (B <= 2048)
+    if (g_gemm_mode == ACMI_GEMM_X3 && convf_lds() == 2)
+      launch_convf_x3<float, 20, 20, 32, 4, 4, 2, 64, 1, 64>(a->a1, st * 400 * 32, B, P + L.off[2], epi, s);
+    else if (B <= 2048)
       launch_mm<64, 64, 32, 1, 1, false, false, 32>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
     else
       launch_mm<128, 64, 32, 2, 1, false, false, 16>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
@@ -325,7 +341,9 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     RowsAsK<Src> opA{Src{a->a2, (uint32_t)(st * 81 * 64), B * 49}};
     MatI<true> opB{P + L.off[4], C3, 576, C3};
     EpiAct epi{a->a3, P + L.off[5], C3, 49, st * 49 * C3};
-    if constexpr (C3 == 32)
+    if (g_gemm_mode == ACMI_GEMM_X3 && convf_lds())
+      launch_convf_x3<float, 9, 9, 64, 3, 3, 1, C3, 2, 64>(a->a2, st * 81 * 64, B, P + L.off[4], epi, s);
+    else if constexpr (C3 == 32)
       // (f32 MFMA: the 128x32 bf16x3 tile needs BK = 32 and fits 2 blocks per CU;
       // measured slower than this at B = 512, 21.1 vs 19.6 us)
       launch_gemm<128, 32, 32, 1, 1, false, false>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
