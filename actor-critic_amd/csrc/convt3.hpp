@@ -22,14 +22,15 @@
 
 namespace acmi {
 
-template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ>
+template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, int NWAVES = 4>
 struct ConvTX3 {
+  static constexpr int NTHR = 64 * NWAVES;
   static constexpr int PH = IH / S, PW = IW / S, L = PH * PW;
   static constexpr int OH = (IH - KH) / S + 1, OW = (IW - KW) / S + 1, OP = OH * OW;
   static constexpr int KHP = KH / S, KWP = KW / S;
   static constexpr int K = KHP * KWP * COUT;
   static constexpr int NI = S * S * CIN;
-  static constexpr int WM = NI / 64, WN = 4 / WM;  // waves over rows / columns
+  static constexpr int WM = NI / 64, WN = NWAVES / WM;  // waves over rows / columns
   static constexpr int WCOLS = NJ / WN;            // columns per wave
   static constexpr int TN = WCOLS / 32;            // 32-column blocks per wave
   static constexpr int NIMG = (NJ - 1) / L + 2;    // images a block's columns can touch
@@ -39,7 +40,7 @@ struct ConvTX3 {
   static constexpr int DY_BYTES = (ZP + 1) * COUT * 4;
   using IA = X3Image<true, NI, 16>;
   static constexpr int LDS_BYTES = DY_BYTES + 2 * IA::BYTES;
-  static_assert(NI % 64 == 0 && 4 % WM == 0 && NJ % (32 * WN) == 0 && COUT % 16 == 0, "shape");
+  static_assert(NI % 64 == 0 && NWAVES % WM == 0 && NJ % (32 * WN) == 0 && COUT % 16 == 0, "shape");
   static_assert(IH % S == 0 && IW % S == 0 && KH % S == 0 && KW % S == 0, "phases");
   __device__ __forceinline__ static int chunk_pos(int p, int c) {
     return p * (COUT * 4) + 16 * (c ^ ((p / PIXW) & (CH - 1)));
@@ -51,15 +52,16 @@ constexpr int convt_x3_blocks_per_cu() {
   return std::min(8, 160 * 1024 / CT::LDS_BYTES);
 }
 
-template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, class Epi>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    convt_x3_blocks_per_cu<ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ>>())))
+template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, int NWAVES, class Epi>
+__global__ __launch_bounds__(64 * NWAVES) __attribute__((amdgpu_waves_per_eu(
+    convt_x3_blocks_per_cu<ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES>>() * NWAVES / 4)))
 void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi) {
-  using CT = ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ>;
+  using CT = ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES>;
   using IA = typename CT::IA;
   using W = ConvTWeights<KH, KW, S, CIN, COUT>;
-  constexpr int NI = CT::NI, K = CT::K, L = CT::L;
-  constexpr int NA = NI * 16 / 4 / 256;  // weight float4 runs per thread per K-tile
+  constexpr int NI = CT::NI, K = CT::K, L = CT::L, NTHR = CT::NTHR;
+  constexpr int NA = NI * 16 / 4 / NTHR;  // weight float4 runs per thread per K-tile
+  static_assert(NA >= 1 && NI * 16 / 4 == NA * NTHR, "weight staging map");
   __shared__ __attribute__((aligned(16))) char lds[CT::LDS_BYTES];
   char* dimg = lds;
   char* abuf = lds + CT::DY_BYTES;
@@ -75,7 +77,7 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi) {
   const W opA{w};
   typename W::R rowA[NA];
 #pragma unroll
-  for (int v = 0; v < NA; ++v) rowA[v] = opA.row((tid + 256 * v) / 4);
+  for (int v = 0; v < NA; ++v) rowA[v] = opA.row((tid + NTHR * v) / 4);
   StF4 ra[NA];
   auto fetch = [&](int k0) {
     const int k = k0 + (tid % 4) * 4;
@@ -87,7 +89,7 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi) {
     char* As = abuf + buf * IA::BYTES;
 #pragma unroll
     for (int v = 0; v < NA; ++v) {
-      const int idx = tid + 256 * v;
+      const int idx = tid + NTHR * v;
       const int i = idx / 4;
       IA::write(As, (idx - i * 4) * 4, i, finish(ra[v]));
     }
@@ -96,13 +98,24 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi) {
   fetch(0);
   // dY of images img_lo..img_hi (contiguous [img][OH][OW][COUT]) + the zero pixel
   {
+    // all of a thread's loads issued before its stores (one latency, not one per load)
     const int n4 = (img_hi - img_lo + 1) * CT::OP * CT::CH;
     const float4* src = reinterpret_cast<const float4*>(dy + (long long)img_lo * CT::OP * COUT);
-    for (int e = tid; e < n4; e += 256) {
-      const int p = e / CT::CH, c = e - p * CT::CH;
-      *reinterpret_cast<float4*>(dimg + CT::chunk_pos(p, c)) = src[e];
+    constexpr int NPT = (CT::NIMG * CT::OP * CT::CH + NTHR - 1) / NTHR;
+    float4 v[NPT];
+#pragma unroll
+    for (int q = 0; q < NPT; ++q) {
+      const int e = tid + NTHR * q;
+      v[q] = src[e < n4 ? e : 0];
     }
-    for (int c = tid; c < CT::CH; c += 256)
+#pragma unroll
+    for (int q = 0; q < NPT; ++q) {
+      const int e = tid + NTHR * q;
+      if (e >= n4) break;
+      const int p = e / CT::CH, c = e - p * CT::CH;
+      *reinterpret_cast<float4*>(dimg + CT::chunk_pos(p, c)) = v[q];
+    }
+    for (int c = tid; c < CT::CH; c += NTHR)
       *reinterpret_cast<float4*>(dimg + CT::ZP * COUT * 4 + 16 * c) = f4zero();
   }
   commit(0);
@@ -175,12 +188,13 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi) {
                             reinterpret_cast<float*>(lds) + wave * 32 * 36, NI, J);
 }
 
-template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, class Epi>
+template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, int NWAVES = 4,
+          class Epi>
 inline void launch_convt_x3(const float* w, const float* dy, int B, const Epi& e, hipStream_t s) {
-  using CT = ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ>;
-  static_assert(CT::DY_BYTES >= 4 * 32 * 36 * 4, "epilogue transpose needs the dY region");
-  hipLaunchKernelGGL((convt_x3_kernel<IH, IW, KH, KW, S, CIN, COUT, NJ, Epi>), dim3(cdiv(B * CT::L, NJ)),
-                     dim3(256), 0, s, w, dy, B, e);
+  using CT = ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES>;
+  static_assert(CT::DY_BYTES >= NWAVES * 32 * 36 * 4, "epilogue transpose needs the dY region");
+  hipLaunchKernelGGL((convt_x3_kernel<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES, Epi>),
+                     dim3(cdiv(B * CT::L, NJ)), dim3(CT::NTHR), 0, s, w, dy, B, e);
 }
 
 }  // namespace acmi

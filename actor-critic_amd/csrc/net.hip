@@ -274,10 +274,10 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* part, int nz, c
 }
 
 // conv input gradients with the dY im2col in LDS (convt3.hpp): ACMI_CONVT =
-// 1 (default) conv3 only; 0 off (gemm3 over ConvTRows); 2 / 3 conv2 too, with
-// 128- / 64-column blocks.  Measured (M = 10240, per launch): conv3 231 -> 190
-// us; conv2 449 us on gemm3 vs 939 / slower here -- its f32 dY image (3 images x
-// 81 px x 64 ch) leaves one block per CU.
+// 1 (default) conv3 only; 0 off (gemm3 over ConvTRows); 2 / 3 / 4 conv2 too,
+// with 128- / 64- / 256-column (8-wave) blocks.  Measured (M = 10240, per
+// launch): conv3 231 -> 186 us; conv2 444 us on gemm3 vs 939 / slower / 620
+// here -- its f32 dY image (3-4 images x 81 px x 64 ch) leaves one block per CU.
 static int convt_lds() {
   static const int v = getenv("ACMI_CONVT") ? atoi(getenv("ACMI_CONVT")) : 1;
   return v;
@@ -808,6 +808,8 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
       launch_convt_x3<20, 20, 4, 4, 2, 32, 64, 128>(P + L.off[2], bw->d2, B, epi, s);
     else if (g_gemm_mode == ACMI_GEMM_X3 && convt_lds() == 3)
       launch_convt_x3<20, 20, 4, 4, 2, 32, 64, 64>(P + L.off[2], bw->d2, B, epi, s);
+    else if (g_gemm_mode == ACMI_GEMM_X3 && convt_lds() == 4)
+      launch_convt_x3<20, 20, 4, 4, 2, 32, 64, 256, 8>(P + L.off[2], bw->d2, B, epi, s);
     else
       launch_mm<128, 128, 16, 2, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
     prof_end(ACMI_PROF_CONV2_DX, s);
