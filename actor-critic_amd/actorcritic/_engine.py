@@ -6,6 +6,7 @@ size, and the update workspaces.  Every arithmetic call goes through libacmi.so.
 """
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -143,6 +144,25 @@ class UpdateState(object):
                             self.dhead.data_ptr(), eng.ldh)
         self.actions = None
         self.fwd = None
+        self._side = None
+
+    def side(self, eng):
+        """Second backward workspace (d1..d4, dhead, ws) and a side stream: the sampled-
+        loss backward (acmi_kfac_output_stats) runs there concurrently with the loss
+        backward (acmi_backward) -- the two chains share only read-only inputs (the
+        rollout activations, the parameters) and write disjoint parts of ``stats``."""
+        if self._side is None:
+            L, dev, M = eng.layout, eng.device, self.M
+            z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)
+            sd = type('SideState', (), {})()
+            sd.dhead = z(M, eng.ldh)
+            sd.d1, sd.d2, sd.d3, sd.d4 = z(M, 20, 20, 32), z(M, 9, 9, 64), z(M, 7, 7, L.C3), z(M, 512)
+            sd.ws = z(int(eng.lib.acmi_backward_ws_floats(M, L.A, L.C3)))
+            sd.bwd = _lib.Bwd(sd.d1.data_ptr(), sd.d2.data_ptr(), sd.d3.data_ptr(), sd.d4.data_ptr(),
+                              sd.dhead.data_ptr(), eng.ldh)
+            sd.stream = torch.cuda.Stream(device=dev)
+            self._side = sd
+        return self._side
 
 
 class NetEngine(object):
@@ -199,11 +219,36 @@ class NetEngine(object):
                   ctypes.byref(fwd.acts.struct), ctypes.byref(st.bwd), _lib.ptr(st.grads),
                   _lib.ptr(st.astat) if with_stats else None, _lib.ptr(st.bwd_ws), self.stream())
 
-    def output_stats(self, fwd, st, seed, counter):
+    def output_stats(self, fwd, st, seed, counter, side=None):
+        """side: run on UpdateState.side()'s stream and workspace (see there)."""
         net = self.net()
+        bwd, ws = (side.bwd, side.ws) if side is not None else (st.bwd, st.bwd_ws)
         _lib.call('acmi_kfac_output_stats', ctypes.byref(net), fwd.M, ctypes.byref(fwd.acts.struct),
-                  ctypes.byref(st.bwd), seed, self.rank, counter, _lib.ptr(st.gstat), _lib.ptr(st.bwd_ws),
+                  ctypes.byref(bwd), seed, self.rank, counter, _lib.ptr(st.gstat), _lib.ptr(ws),
                   self.stream())
+
+    concurrent_stats = os.environ.get('ACMI_CONCURRENT_STATS', '1') != '0'
+
+    def backward_and_stats(self, fwd, st, with_stats, seed, counter):
+        """acmi_backward (+ A stats) and, with stats, acmi_kfac_output_stats (G stats);
+        starts the data-parallel all-reduce of the backward's prefix of ``red`` as soon
+        as it is enqueued and returns its handle (allreduce_end completes it).  With
+        ``concurrent_stats`` the G chain runs on a side stream next to the backward."""
+        if not (with_stats and self.concurrent_stats):
+            self.backward(fwd, st, with_stats)
+            pending = self.allreduce_begin(st, with_stats)
+            if with_stats:
+                self.output_stats(fwd, st, seed, counter)
+            return pending
+        main = torch.cuda.current_stream(self.device)
+        sd = st.side(self)
+        sd.stream.wait_stream(main)
+        with torch.cuda.stream(sd.stream):
+            self.output_stats(fwd, st, seed, counter, side=sd)
+        self.backward(fwd, st, True)
+        pending = self.allreduce_begin(st, True)
+        main.wait_stream(sd.stream)
+        return pending
 
     def allreduce(self, st, with_stats):
         """Sums [grads | losses (| factor stats)] over ranks (RCCL); the 1/world scale is

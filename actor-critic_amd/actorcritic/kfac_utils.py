@@ -143,9 +143,7 @@ class KfacOptimizer(Optimizer):
         st = eng.update_state(ctx.eval(objective.model._forward).M)
         lr = self._lr(ctx)
         gs = global_step.value if global_step is not None else self.cov_updates
-        eng.backward(st.fwd, st, with_stats=True)
-        pending = eng.allreduce_begin(st, with_stats=True)  # overlaps the G statistics
-        self._stats(eng, st.fwd, st, gs)
+        pending = eng.backward_and_stats(st.fwd, st, True, seed=0x4b464143, counter=gs)
         eng.allreduce_end(st, True, pending)
         self._cov_update(eng, st)
         self._inv_update(eng)
@@ -195,10 +193,7 @@ class ColdStartPeriodicInvUpdateKfacOpt(KfacOptimizer):
         lr = self._lr(ctx)  # learning_rate read once, from the pre-update global_step
         cold, cov, inv, gs_after = schedule(global_step.value, self._num_cold_updates, self._invert_every)
         self.last_flags = (cold, cov, inv)
-        eng.backward(st.fwd, st, with_stats=cov)
-        pending = eng.allreduce_begin(st, with_stats=cov)  # overlaps the G statistics
-        if cov:
-            self._stats(eng, st.fwd, st, global_step.value)
+        pending = eng.backward_and_stats(st.fwd, st, cov, seed=0x4b464143, counter=global_step.value)
         eng.allreduce_end(st, cov, pending)
         if cold:
             self._cold_optimizer._apply_dense(ctx, eng, st.grads, 0.0)

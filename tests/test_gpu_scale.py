@@ -216,3 +216,16 @@ def test_two_stream_rollout_is_bit_identical(lib, cuda, monkeypatch):
                 assert torch.equal(torch.isnan(a), torch.isnan(b)), i
                 a, b = torch.nan_to_num(a, nan=0.0), torch.nan_to_num(b, nan=0.0)
             assert torch.equal(a, b), i
+
+
+def test_concurrent_g_stats_bit_identical(lib, cuda, monkeypatch):
+    """The sampled-loss backward (G statistics) on a side stream concurrently with the
+    loss backward (NetEngine.backward_and_stats) gives bit-identical parameters,
+    factors, inverses and velocities to running the two chains one after the other."""
+    from actorcritic._engine import NetEngine
+    monkeypatch.setattr(NetEngine, 'concurrent_stats', False)
+    serial = _run_two_updates()
+    monkeypatch.setattr(NetEngine, 'concurrent_stats', True)
+    conc = _run_two_updates()
+    for i, (a, b) in enumerate(zip(serial[:4], conc[:4])):
+        assert torch.equal(a, b), i
