@@ -762,9 +762,37 @@ static long long bwd_partial_cap(int B, int A, int C3) {
       m = std::max(m, gcov_plan(co[l], rowsL[l]).floats);
     }
   }
-  m = std::max(m, conv1_afactor_ws_ints(rowsL[0]));
   return m;
 }
+
+// The conv1 A factor reads only the frames: it can run on a library-owned side
+// stream (one per device) concurrently with the input-gradient chain and the
+// other reductions, in its own workspace region after the shared partials.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+static SideStream* side_stream() {
+  // opt-in (ACMI_SIDE=1): at the bench shape the overlap costs more than it
+  // hides (update 5.69 vs 5.64 ms -- the i8 gather competes with the
+  // symmetric reductions for L2 and LDS)
+  static const bool on = getenv("ACMI_SIDE") && atoi(getenv("ACMI_SIDE")) == 1;
+  if (!on) return nullptr;
+  static SideStream ss[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  SideStream& x = ss[dev];
+  if (!x.s) {
+    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) {
+      x.s = nullptr;
+      return nullptr;
+    }
+  }
+  return &x;
+}
+static long long afactor_ws_floats(int B) { return conv1_afactor_ws_ints(400LL * B); }
 
 // ---------------------------------------------------------------------------
 // backward (dX chain) shared by the loss backward and the sampled backward
@@ -823,9 +851,27 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
                          long long img_stride, int B, const acmi_acts_t* a,
                          const acmi_bwd_t* bw, float* grads, float* astat,
                          float* ws, long long ws_cap, hipStream_t s) {
+  const bool st = astat != nullptr;
+  // conv1 A factor first, on the side stream (its int partials after the shared
+  // split-K partials); falls back to this stream when no side stream exists
+  SideStream* side = st ? side_stream() : nullptr;
+  if (st) {
+    const long long pcap = bwd_partial_cap(B, L.A, L.C3);
+    hipStream_t as = s;
+    if (side) {
+      ACMI_REQUIRE(hipEventRecord(side->fork, s) == hipSuccess &&
+                       hipStreamWaitEvent(side->s, side->fork, 0) == hipSuccess,
+                   ACMI_ERR_HIP, "acmi_backward: side-stream fork failed");
+      as = side->s;
+    }
+    prof_begin(ACMI_PROF_CONV1_AFACTOR, as);
+    const int rc0 = conv1_afactor_u8(obs, img_stride, B, astat + L.stat_off[0],
+                                     reinterpret_cast<int*>(ws + pcap), afactor_ws_floats(B), as);
+    prof_end(ACMI_PROF_CONV1_AFACTOR, as);
+    if (rc0) return rc0;
+  }
   int rc = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s);
   if (rc) return rc;
-  const bool st = astat != nullptr;
   float* part = ws;
   // heads: X = a4 (512), dY = dhead (A+1 columns: pi | v)
   rc = wgrad_layer(DenseRows{a->a4, 512, B, 512}, 512, B, bw->dhead, bw->ldh, L.A + 1, st,
@@ -854,11 +900,12 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
                    400LL * B, bw->d1, 32, 32, false, part, ws_cap, grads + L.off[0], 32, nullptr,
                    nullptr, s, ACMI_PROF_CONV1_WGRAD, 1.0f / 255.0f);  // raw u8 patches
   if (rc || !st) return rc;
-  prof_begin(ACMI_PROF_CONV1_AFACTOR, s);
-  rc = conv1_afactor_u8(obs, img_stride, B, astat + L.stat_off[0], reinterpret_cast<int*>(ws),
-                        ws_cap, s);
-  prof_end(ACMI_PROF_CONV1_AFACTOR, s);
-  return rc;
+  if (side) {  // join the conv1 A factor
+    ACMI_REQUIRE(hipEventRecord(side->join, side->s) == hipSuccess &&
+                     hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
+                 ACMI_ERR_HIP, "acmi_backward: side-stream join failed");
+  }
+  return ACMI_OK;
 }
 
 // sampled-loss output gradients at the heads (kfac "gradients" mode):
@@ -1031,7 +1078,7 @@ int64_t acmi_backward_ws_floats(int B, int A, int C3) {
   Layout L;
   if (!make_layout(A, C3, &L) || B < 0) return -1;
   const int ldg = roundup4(A + 1) < 8 ? 8 : roundup4(A + 1);
-  return bwd_partial_cap(B, A, C3) + (long long)B * ldg + 64;
+  return bwd_partial_cap(B, A, C3) + afactor_ws_floats(B) + (long long)B * ldg + 64;
 }
 
 int acmi_backward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,
