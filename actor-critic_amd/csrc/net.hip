@@ -295,9 +295,11 @@ static int convf_lds() {
 
 // split factor for fc4 at small batch (64 x 128 tiles over 512 columns)
 static void fc4_plan(int B, int K, int* nz, int* chunk) {
+  static const int maxsp = getenv("ACMI_FC4_SPLIT") ? atoi(getenv("ACMI_FC4_SPLIT")) : 8;
   const int blocks = cdiv(B, 64) * 4;
-  int sp = blocks >= 256 ? 1 : std::min(8, cdiv(256, blocks));
-  int ch = (cdiv(K, sp) + 31) / 32 * 32;
+  int sp = blocks >= 256 ? 1 : std::min(maxsp, cdiv(256 * maxsp / 8, blocks));
+  const int q = g_gemm_mode == ACMI_GEMM_X3 ? 16 : 32;  // the split GEMM's K-tile
+  int ch = (cdiv(K, sp) + q - 1) / q * q;
   *chunk = ch;
   *nz = cdiv(K, ch);
 }
@@ -389,6 +391,14 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     case 6: ACMI_HEADS(6); break;
     case 7: ACMI_HEADS(7); break;
     case 8: ACMI_HEADS(8); break;
+    case 9: ACMI_HEADS(9); break;
+    case 10: ACMI_HEADS(10); break;
+    case 11: ACMI_HEADS(11); break;
+    case 12: ACMI_HEADS(12); break;
+    case 13: ACMI_HEADS(13); break;
+    case 14: ACMI_HEADS(14); break;
+    case 15: ACMI_HEADS(15); break;
+    case 16: ACMI_HEADS(16); break;
     default: ACMI_REQUIRE(false, ACMI_ERR_ARG, "fc4 split factor %d out of range", nz);
   }
 #undef ACMI_HEADS
