@@ -100,6 +100,9 @@ _SIGS = {
     'acmi_env_reset': (c_int, [ctypes.POINTER(EnvState), c_int, c_int, c_u32, c_vp, c_i64, c_vp]),
     'acmi_env_step': (c_int, [ctypes.POINTER(EnvState), c_int, c_int, c_u32, c_vp, c_vp, c_i64, c_vp, c_i64,
                               c_vp, c_vp, c_vp, c_i64, c_vp]),
+    'acmi_atari_preprocess': (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_int, c_vp, c_i64, c_vp]),
+    'acmi_atari_stack': (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp,
+                                 c_i64, c_vp]),
     'acmi_selftest_plans': (c_int, [c_int]),
     'acmi_gemm_f32': (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     'acmi_prof_enable': (c_int, [c_int, c_int]),

@@ -311,6 +311,34 @@ int acmi_env_step(const acmi_env_state_t* st, int N, int env_offset,
                   float* rewards, uint8_t* terminals, float* episode_rewards,
                   int64_t ld, acmi_stream_t stream);
 
+/* ------------------------------------------------------------------------
+ * Atari frame preprocessing for real (raw RGB) frames, batched over envs:
+ * replaces the frame half of the reference's per-env wrapper chain
+ *   AtariFrameskipWrapper  (envs/atari/wrappers.py:54-67: np.amax of the last
+ *                           two raw frames),
+ *   AtariPreprocessFrameWrapper (wrappers.py:30-33: cv2 RGB2GRAY + INTER_AREA
+ *                           resize to 84x84),
+ *   FrameStackWrapper      (wrappers.py:224-235: roll, zero on terminal,
+ *                           insert; reset repeats the frame 4 times).
+ * Env n's frames: raw + n*env_stride is its LAST frame [H][W][3] u8, and, when
+ * frame_stride != 0 and (nframes null or nframes[n] >= 2), the frame before
+ * it is at + frame_stride (max-pooled with it).  H, W in [84, 504],
+ * H*W <= 40960, W a multiple of 4, not both multiples of 84 (cv2's
+ * integer-ratio fast path is not restated); raw/strides 4-byte aligned.
+ * ---------------------------------------------------------------------- */
+/* gray [84][84] u8 of env n at gray_out + n*out_stride */
+int acmi_atari_preprocess(const uint8_t* raw, int64_t env_stride,
+                          int64_t frame_stride, const uint8_t* nframes, int N,
+                          int H, int W, uint8_t* gray_out, int64_t out_stride,
+                          acmi_stream_t stream);
+/* 4-frame stacks [84][84][4] u8 at stack + n*stack_stride: reset != 0 ->
+ * [f,f,f,f]; else [s1,s2,s3,f], or [0,0,0,f] where terminals[n] != 0
+ * (terminals nullable).  stack_in == stack_out is allowed. */
+int acmi_atari_stack(const uint8_t* raw, int64_t env_stride, int64_t frame_stride,
+                     const uint8_t* nframes, int N, int H, int W,
+                     const uint8_t* terminals, int reset, const uint8_t* stack_in,
+                     uint8_t* stack_out, int64_t stack_stride, acmi_stream_t stream);
+
 /* Rollout variant of acmi_forward: batch row b reads image b of `obs` and
  * writes activation row b*act_img_stride (env-major [N][T] buffers, the
  * pointers in *acts pre-offset by step t), so step t of a T-step rollout

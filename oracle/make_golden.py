@@ -241,11 +241,73 @@ def golden_framestack(seed=7, envs=(0, 5), steps=700):
         json.dump(record, f)
 
 
+def _atari_chain_reference(env, wsrc, wtree):
+    """The make_atari_env chain (a2c_acktr.py:190-213) from the reference's method
+    bodies, minus AtariPreprocessFrameWrapper (cv2 is absent: the frames stay raw RGB)
+    and RenderWrapper.  gym.RewardWrapper.step (apply `reward` to the inner step's
+    reward) is the one piece of glue written here."""
+    def m(cls, name):
+        return _compile(_find(wtree, name, cls), wsrc, {'np': np})
+
+    noop = _bind(_Obj(), {'reset': m('AtariNoopResetWrapper', 'reset'), 'step': m('AtariNoopResetWrapper', 'step')})
+    noop.env, noop.unwrapped, noop.noop_max = env, env, 30
+    skip = _bind(_Obj(), {'step': m('AtariFrameskipWrapper', 'step'), 'reset': m('AtariFrameskipWrapper', 'reset')})
+    skip.env, skip._frameskip = noop, 4
+    info = _bind(_Obj(), {'step': m('EpisodeInfoWrapper', 'step'), 'reset': m('EpisodeInfoWrapper', 'reset')})
+    info.env, info.total_reward = skip, 0.0
+    life = _bind(_Obj(), {'step': m('AtariEpisodicLifeWrapper', 'step'),
+                          'reset': m('AtariEpisodicLifeWrapper', 'reset')})
+    life.env, life.lives, life.episode_terminal = info, 0, True
+    fire = _bind(_Obj(), {'step': m('AtariFireResetWrapper', 'step'), 'reset': m('AtariFireResetWrapper', 'reset')})
+    fire.env = life
+    clip = _bind(_Obj(), {'reward': m('AtariClipRewardWrapper', 'reward')})
+
+    def clip_step(self, action):
+        o, r, d, i = self.env.step(action)
+        return o, self.reward(r), d, i
+
+    _bind(clip, {'step': clip_step, 'reset': lambda self, **kw: self.env.reset(**kw)})
+    clip.env = fire
+    clear = _bind(_Obj(), {'step': m('AtariInfoClearWrapper', 'step'), 'reset': m('AtariInfoClearWrapper', 'reset')})
+    clear.env = clip
+    return clear
+
+
+def golden_atari_wrappers(seeds=(3, 11), steps=400):
+    """Trace of the reference's Atari wrapper chain over oracle.FakeALE: per step the
+    CRC32 of the (max-pooled raw) observation, clipped reward, terminal, episode
+    total from info; plus every action the game itself received (noop/fire resets)."""
+    wsrc = _source('envs/atari/wrappers.py')
+    wtree = ast.parse(wsrc)
+    rng = np.random.default_rng(5)
+    record = {}
+    for seed in seeds:
+        game = oracle.FakeALE(seed)
+        env = _atari_chain_reference(game, wsrc, wtree)
+        obs = env.reset()
+        crcs, rews, terms, eps, acts = [zlib.crc32(np.ascontiguousarray(obs).tobytes())], [], [], [], []
+        for t in range(steps):
+            a = int(rng.integers(0, 4))
+            obs, r, d, info = env.step(a)
+            crcs.append(zlib.crc32(np.ascontiguousarray(obs).tobytes()))
+            rews.append(float(r))
+            terms.append(bool(d))
+            eps.append(info['episode']['total_reward'] if 'episode' in info else None)
+            acts.append(a)
+            if d:  # the training loop's auto-reset (multi_env.py:127-132)
+                crcs.append(zlib.crc32(np.ascontiguousarray(env.reset()).tobytes()))
+        record['seed{}'.format(seed)] = dict(crc=crcs, rewards=rews, terminals=terms, episode=eps, actions=acts,
+                                            game_actions=game.actions)
+    with open(os.path.join(OUT, 'atari_wrappers.json'), 'w') as f:
+        json.dump(record, f)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     n = golden_returns()
     golden_agent_layout()
     golden_framestack()
+    golden_atari_wrappers()
     print('wrote {} returns cases, agent layout, frame-stack/auto-reset trace to {}'.format(n, OUT))
 
 
