@@ -356,61 +356,67 @@ static void af_plan_tri(long long rows, int* nchunk, int* chunk) {
   *nchunk = (int)((rows + *chunk - 1) / *chunk);
 }
 
-// A (257 x 257, f32) from the exact integer sums; element (a, b), a,b <= 256
-__global__ void conv1_afactor_finalize(const int* part, const int* colsum, int nchunk, int rows,
-                                       float* astat) {
-  // upper triangle only (consecutive threads read consecutive partials),
-  // written to both halves
+// A (257 x 257, f32) from the exact integer partials, in two passes:
+//  1. conv1_afactor_reduce: int64 sums over the chunks -- blocks of 64 consecutive
+//     elements x 4 chunk groups (every chunk's partial row read coalesced, 8 loads
+//     in flight per thread, 4x the waves of one thread per element); elements of
+//     the 32x32 tiles below the diagonal (never written) are skipped; the last 4
+//     blocks sum the column sums.  Integer sums: the order is immaterial.
+//  2. conv1_afactor_finalize: A = (sum u u^T) / (255^2 R) with u = x + 128,
+//     mirrored into both halves.
+__global__ __launch_bounds__(256) void conv1_afactor_reduce(const int* part, const int* colsum,
+                                                            int nchunk, long long* sums) {
+  __shared__ long long red[4][64];
+  const int t = threadIdx.x, e0 = blockIdx.x * 64, el = t & 63, g = t >> 6;
+  const bool cs = e0 >= 65536;  // column-sum blocks
+  const int e = (cs ? e0 - 65536 : e0) + el;
+  const int row = e >> 8, col = e & 255;
+  long long acc = 0;
+  if (cs ? e < 256 : (row >> 5) <= (col >> 5)) {
+    const int* src = cs ? colsum + e : part + e;
+    const long long stride = cs ? 256 : 65536;
+    for (int c0 = g; c0 < nchunk; c0 += 32) {
+      int v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = c0 + 4 * u;
+        v[u] = src[(long long)(c < nchunk ? c : 0) * stride];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += (c0 + 4 * u < nchunk) ? v[u] : 0;
+    }
+  }
+  red[g][el] = acc;
+  __syncthreads();
+  if (g == 0) sums[(cs ? 65536 : 0) + e] = red[0][el] + red[1][el] + red[2][el] + red[3][el];
+}
+
+__global__ void conv1_afactor_finalize(const long long* sums, int rows, float* astat) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= 257 * 257) return;
-  const int a = idx / 257, b = idx - a * 257;
-  if (a > b) return;
-  const int lo = a, hi = b;
+  const int lo = idx / 257, hi = idx - lo * 257;
+  if (lo > hi) return;
   const long long R = rows;
+  const long long* sx = sums + 65536;
   double v;
   if (hi == 256 && lo == 256) {
     v = 1.0;
+  } else if (hi == 256) {
+    v = (double)(sx[lo] + 128 * R) / (255.0 * (double)R);
   } else {
-    // int32 partials are exact; summed in int64 (the order is immaterial)
-    long long sx_lo = 0;
-    for (int c0 = 0; c0 < nchunk; c0 += 8) {
-      int v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = colsum[(long long)(c0 + u < nchunk ? c0 + u : 0) * 256 + lo];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) sx_lo += (c0 + u < nchunk) ? v[u] : 0;
-    }
-    if (hi == 256) {
-      v = (double)(sx_lo + 128 * R) / (255.0 * (double)R);
-    } else {
-      long long sx_hi = 0, cx = 0;
-      for (int c0 = 0; c0 < nchunk; c0 += 8) {
-        int vh[8], vc[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const long long c = c0 + u < nchunk ? c0 + u : 0;
-          vh[u] = colsum[c * 256 + hi];
-          vc[u] = part[c * 65536 + lo * 256 + hi];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          sx_hi += (c0 + u < nchunk) ? vh[u] : 0;
-          cx += (c0 + u < nchunk) ? vc[u] : 0;
-        }
-      }
-      const long long uu = cx + 128 * (sx_lo + sx_hi) + 16384 * R;
-      v = (double)uu / (65025.0 * (double)R);
-    }
+    const long long uu = sums[lo * 256 + hi] + 128 * (sx[lo] + sx[hi]) + 16384 * R;
+    v = (double)uu / (65025.0 * (double)R);
   }
   astat[lo * 257 + hi] = (float)v;
   astat[hi * 257 + lo] = (float)v;
 }
 
+// partials + column sums (ints), then the int64 sums (8-byte aligned, 2 ints of slack)
 long long conv1_afactor_ws_ints(long long rows) {
   int nchunk, chunk, nt, ct;
   af_plan(rows, &nchunk, &chunk);
   af_plan_tri(rows, &nt, &ct);
-  return (long long)std::max(nchunk, nt) * (65536 + 256);
+  return (long long)std::max(nchunk, nt) * (65536 + 256) + 2 * (65536 + 256) + 2;
 }
 
 int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* astat, int* ws,
@@ -435,8 +441,12 @@ int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* ast
   else
     hipLaunchKernelGGL(conv1_afactor_i8_kernel, dim3(3 * nchunk), dim3(256), 0, s, obs, img_stride,
                        (int)rows, chunk, part, colsum);
-  hipLaunchKernelGGL(conv1_afactor_finalize, dim3(cdiv(257 * 257, 256)), dim3(256), 0, s, part,
-                     colsum, nchunk, (int)rows, astat);
+  long long* sums = reinterpret_cast<long long*>(
+      ((uintptr_t)(colsum + (long long)nchunk * 256) + 7) & ~(uintptr_t)7);
+  hipLaunchKernelGGL(conv1_afactor_reduce, dim3(65536 / 64 + 4), dim3(256), 0, s, part, colsum, nchunk,
+                     sums);
+  hipLaunchKernelGGL(conv1_afactor_finalize, dim3(cdiv(257 * 257, 256)), dim3(256), 0, s, sums,
+                     (int)rows, astat);
   ACMI_LAUNCH_CHECK("conv1_afactor_u8");
   return ACMI_OK;
 }
