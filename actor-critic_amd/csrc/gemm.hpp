@@ -192,50 +192,13 @@ __device__ __forceinline__ void store_tile_lds(const Epi& epi, const Acc& acc, i
 // DEPTH: K-tiles of staging loads in flight (register sets): 1 = the next
 // tile's loads overlap the current tile's MFMAs; 2 = two tiles ahead, for
 // latency-bound shapes (short per-tile MFMA work, L2-missing gathers).
-template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM,
-          class OpA, class OpB, class Epi, int DEPTH = 1>
-// waves_per_eu = the blocks per CU the LDS allows (one wave per SIMD each),
-// which plan_rounds counts on for the split-K reductions: for the 128x128x16
-// tiles that is 4, and without the hint the compiler parks the accumulators in
-// AGPRs next to ~85 VGPRs so only 3 fit.  (The conv2 input gradient spills a
-// little at 4 and is still faster than at 3; shapes whose registers cannot
-// reach the LDS bound get the compiler's best, -Wno-pass-failed.)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    gemm_blocks_per_cu<BM, BN, BK, OpA::KCONTIG, OpB::KCONTIG>())))
-void gemm_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, int sym_cols) {
+// The work of one output tile (bx, by) of split-K chunk bz: gemm_kernel maps its
+// grid onto tiles, gemm_group_kernel maps one grid over several problems.
+template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM, class OpA, class OpB,
+          class Epi, int DEPTH>
+__device__ __forceinline__ void gemm_block(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk,
+                                           int sym_cols, int bx, int by, int bz) {
   using TL = Tile<BM, BN, BK, WTM, WTN>;
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if constexpr (SPLITK) {
-    // live tiles only: row x skips its first skip(x) column tiles (those
-    // strictly below the diagonal of the symmetric block, see sym_cols)
-    const int tx = (I + BM - 1) / BM, ty = (J + BN - 1) / BN;
-    const int ssym = sym_cols > 0 ? sym_cols / BN : 0;
-    int live = 0;
-    for (int x = 0; x < tx; ++x) live += ty - min(x * BM / BN, ssym);
-    const int total = gridDim.x;
-    const int b = blockIdx.x;
-#ifndef ACMI_NO_XCD_REMAP
-    const int xcd = b & 7, base = total >> 3, rem = total & 7;
-    const int l = xcd * base + min(xcd, rem) + (b >> 3);
-#else
-    const int l = b + 0 * total;
-#endif
-    bz = l / live;
-    int t = l - bz * live;
-    bx = 0;
-    for (int x = 0; x < tx; ++x) {
-      const int n = ty - min(x * BM / BN, ssym);
-      if (t >= n) {
-        t -= n;
-        bx = x + 1;
-      } else {
-        break;
-      }
-    }
-    by = min(bx * BM / BN, ssym) + t;
-  } else if (sym_cols > 0 && (by + 1) * BN <= bx * BM && (by + 1) * BN <= sym_cols) {
-    return;
-  }
   set_z(opA, bz);
   set_z(opB, bz);
   set_z(epi, bz);
@@ -493,6 +456,53 @@ void gemm_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, in
   }
 }
 
+template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM,
+          class OpA, class OpB, class Epi, int DEPTH = 1>
+// waves_per_eu = the blocks per CU the LDS allows (one wave per SIMD each),
+// which plan_rounds counts on for the split-K reductions: for the 128x128x16
+// tiles that is 4, and without the hint the compiler parks the accumulators in
+// AGPRs next to ~85 VGPRs so only 3 fit.  (The conv2 input gradient spills a
+// little at 4 and is still faster than at 3; shapes whose registers cannot
+// reach the LDS bound get the compiler's best, -Wno-pass-failed.)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    gemm_blocks_per_cu<BM, BN, BK, OpA::KCONTIG, OpB::KCONTIG>())))
+void gemm_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, int sym_cols) {
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if constexpr (SPLITK) {
+    // live tiles only: row x skips its first skip(x) column tiles (those
+    // strictly below the diagonal of the symmetric block, see sym_cols)
+    const int tx = (I + BM - 1) / BM, ty = (J + BN - 1) / BN;
+    const int ssym = sym_cols > 0 ? sym_cols / BN : 0;
+    int live = 0;
+    for (int x = 0; x < tx; ++x) live += ty - min(x * BM / BN, ssym);
+    const int total = gridDim.x;
+    const int b = blockIdx.x;
+#ifndef ACMI_NO_XCD_REMAP
+    const int xcd = b & 7, base = total >> 3, rem = total & 7;
+    const int l = xcd * base + min(xcd, rem) + (b >> 3);
+#else
+    const int l = b + 0 * total;
+#endif
+    bz = l / live;
+    int t = l - bz * live;
+    bx = 0;
+    for (int x = 0; x < tx; ++x) {
+      const int n = ty - min(x * BM / BN, ssym);
+      if (t >= n) {
+        t -= n;
+        bx = x + 1;
+      } else {
+        break;
+      }
+    }
+    by = min(bx * BM / BN, ssym) + t;
+  } else if (sym_cols > 0 && (by + 1) * BN <= bx * BM && (by + 1) * BN <= sym_cols) {
+    return;
+  }
+  gemm_block<BM, BN, BK, WTM, WTN, SPLITK, COLSUM, OpA, OpB, Epi, DEPTH>(opA, opB, epi, I, J, K, k_chunk,
+                                                                       sym_cols, bx, by, bz);
+}
+
 // ---------------------------------------------------------------------------
 // Epilogues.  Two phases per element so no load sits under the tile-edge
 // branch (the .s trap (c) again: a load under `if (i < I && j < J)` waits
@@ -633,6 +643,46 @@ inline void launch_gemm(const OpA& a, const OpB& b, const Epi& e, int I, int J,
   if (SPLITK) grid = dim3(live_tiles<BM, BN>(I, J, sym_cols) * zdim);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, BK, WTM, WTN, SPLITK, COLSUM, OpA, OpB, Epi, DEPTH>),
                      grid, dim3(256), 0, s, a, b, e, I, J, K, k_chunk, sym_cols);
+}
+
+// Several independent problems (same operand types and tile shape, no split-K)
+// in one launch: block b runs tile b - tile0[p] of problem p.  For chains of
+// small GEMMs whose launches would otherwise each cost a latency.
+constexpr int kGemmGroupMax = 6;
+template <class OpA, class OpB, class Epi>
+struct GemmGroup {
+  int n;
+  int tile0[kGemmGroupMax + 1];
+  int tiles_x[kGemmGroupMax];
+  int I[kGemmGroupMax], J[kGemmGroupMax], K[kGemmGroupMax];
+  OpA a[kGemmGroupMax];
+  OpB b[kGemmGroupMax];
+  Epi e[kGemmGroupMax];
+};
+
+template <int BM, int BN, int BK, int WTM, int WTN, class OpA, class OpB, class Epi>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    gemm_blocks_per_cu<BM, BN, BK, OpA::KCONTIG, OpB::KCONTIG>())))
+void gemm_group_kernel(GemmGroup<OpA, OpB, Epi> g) {
+  const int b = blockIdx.x;
+  int p = 0;
+  while (p + 1 < g.n && b >= g.tile0[p + 1]) ++p;
+  p = __builtin_amdgcn_readfirstlane(p);
+  const int t = b - g.tile0[p];
+  const int bx = t % g.tiles_x[p], by = t / g.tiles_x[p];
+  gemm_block<BM, BN, BK, WTM, WTN, false, false, OpA, OpB, Epi, 1>(g.a[p], g.b[p], g.e[p], g.I[p], g.J[p],
+                                                                    g.K[p], 0, 0, bx, by, 0);
+}
+
+template <int BM, int BN, int BK, int WTM, int WTN, class OpA, class OpB, class Epi>
+inline void launch_gemm_group(GemmGroup<OpA, OpB, Epi>& g, hipStream_t s) {
+  g.tile0[0] = 0;
+  for (int p = 0; p < g.n; ++p) {
+    g.tiles_x[p] = cdiv(g.I[p], BM);
+    g.tile0[p + 1] = g.tile0[p] + g.tiles_x[p] * cdiv(g.J[p], BN);
+  }
+  hipLaunchKernelGGL((gemm_group_kernel<BM, BN, BK, WTM, WTN, OpA, OpB, Epi>), dim3(g.tile0[g.n]), dim3(256),
+                     0, s, g);
 }
 
 }  // namespace acmi

@@ -664,12 +664,20 @@ int acmi_kfac_eigvals(int A, int C3, const float* factors, double* eigvals, doub
   return ACMI_OK;
 }
 
+// per-layer t1 = Ainv g blocks (rows padded to ldg, offsets rounded to 4 floats)
+static long long kfac_t1_floats(const KLayout& K, long long* off = nullptr) {
+  long long o = 0;
+  for (int l = 0; l < 6; ++l) {
+    if (off) off[l] = o;
+    o += (K.din[l] * K.inv_ld[2 * l + 1] + 3) / 4 * 4;
+  }
+  return o;
+}
+
 int64_t acmi_kfac_step_ws_floats(int A, int C3) {
   KLayout K;
   if (!klayout(A, C3, &K)) return -1;
-  long long m = 0;
-  for (int l = 0; l < 6; ++l) m = std::max(m, K.din[l] * K.inv_ld[2 * l + 1]);
-  return m + KRED + 16;
+  return kfac_t1_floats(K) + KRED + 16;
 }
 
 int acmi_kfac_step(int A, int C3, float* params, float* velocity, const float* grads,
@@ -679,45 +687,44 @@ int acmi_kfac_step(int A, int C3, float* params, float* velocity, const float* g
   ACMI_REQUIRE(params && velocity && grads && inv && precon && ws && klayout(A, C3, &K),
                ACMI_ERR_ARG, "acmi_kfac_step: bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  long long tmax = 0;
-  for (int l = 0; l < 6; ++l) tmax = std::max(tmax, K.din[l] * K.inv_ld[2 * l + 1]);
-  float* t1 = ws;
-  float* part = ws + tmax;
+  long long t1off[6];
+  const long long t1n = kfac_t1_floats(K, t1off);
+  float* part = ws + t1n;
   float* coeff = part + KRED;
+  // Delta_l = Ainv_l g_l Ginv_l for the six layers as two grouped launches (all
+  // first products, then all second products) instead of twelve dependent ones;
+  // t1_l = Ainv_l g_l (Ainv symmetric: A(k, i) = Ainv[k][i]), rows padded to ldg.
+  // The value head (dout = 1, unaligned rows of g) has its own first launch.
+  GemmGroup<MatI<true>, MatI<true>, EpiStore> g1;
+  GemmGroup<MatTK<true>, MatI<true>, EpiStore> g2;
+  g1.n = g2.n = 0;
   for (int l = 0; l < 6; ++l) {
     const int din = (int)K.din[l], dout = (int)K.dout[l];
     const int lda = (int)K.inv_ld[2 * l], ldg = (int)K.inv_ld[2 * l + 1];
     const float* ainv = inv + K.inv_off[2 * l];
     const float* ginv = inv + K.inv_off[2 * l + 1];
     const float* g = grads + K.poff[2 * l];  // [W; b] contiguous, din x dout
-    float* out = precon + K.poff[2 * l];
-    // t1 = Ainv g  (Ainv symmetric: A(k,i) = Ainv[k][i]); t1 rows padded to ldg
-    MatI<true> a1{ainv, lda, din, din};
-    EpiStore e1{t1, ldg};
-    // out = t1 Ginv
-    MatTK<true> a2{t1, ldg, dout, din};
-    MatI<true> b2{ginv, ldg, dout, dout};
-    EpiStore e2{out, dout};
+    float* t1 = ws + t1off[l];
     if (dout % 4 == 0) {
-      MatI<true> b1{g, dout, din, dout};
-      // 64x64 tiles: fc4 (1569 x 512) gives 200 blocks instead of 52
-      if (dout >= 128)
-        launch_gemm<64, 64, 32, 1, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
-      else if (dout > 32)
-        launch_gemm<128, 64, 32, 2, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
-      else
-        launch_gemm<128, 32, 32, 1, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
-    } else {  // the value head (dout = 1): unaligned rows of g
-      MatI<false> b1{g, dout, din, dout};
-      launch_gemm<128, 32, 32, 1, 1, false, false>(a1, b1, e1, din, dout, din, 1, 0, s);
+      const int q = g1.n++;
+      g1.a[q] = MatI<true>{ainv, lda, din, din};
+      g1.b[q] = MatI<true>{g, dout, din, dout};
+      g1.e[q] = EpiStore{t1, ldg};
+      g1.I[q] = din, g1.J[q] = dout, g1.K[q] = din;
+    } else {
+      launch_gemm<128, 32, 32, 1, 1, false, false>(MatI<true>{ainv, lda, din, din},
+                                                   MatI<false>{g, dout, din, dout}, EpiStore{t1, ldg},
+                                                   din, dout, din, 1, 0, s);
     }
-    if (dout >= 128)
-      launch_gemm<64, 64, 32, 1, 1, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
-    else if (dout > 32)
-      launch_gemm<128, 64, 32, 2, 1, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
-    else
-      launch_gemm<128, 32, 32, 1, 1, false, false>(a2, b2, e2, din, dout, dout, 1, 0, s);
+    const int q = g2.n++;
+    g2.a[q] = MatTK<true>{t1, ldg, dout, din};
+    g2.b[q] = MatI<true>{ginv, ldg, dout, dout};
+    g2.e[q] = EpiStore{precon + K.poff[2 * l], dout};
+    g2.I[q] = din, g2.J[q] = dout, g2.K[q] = dout;
   }
+  // 64x64 tiles: fc4 (1569 x 512) alone is 200 blocks; the other layers ride along
+  launch_gemm_group<64, 64, 32, 1, 1>(g1, s);
+  launch_gemm_group<64, 64, 32, 1, 1>(g2, s);
   const long long n = K.nparams;
   hipLaunchKernelGGL(kdot_partial_kernel, dim3(KRED), dim3(256), 0, s, grads, precon, n, part);
   hipLaunchKernelGGL(kcoeff_kernel, dim3(1), dim3(256), 0, s, part, KRED, lr, norm_constraint,
