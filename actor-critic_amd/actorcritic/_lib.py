@@ -103,6 +103,7 @@ _SIGS = {
     'acmi_atari_preprocess': (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_int, c_vp, c_i64, c_vp]),
     'acmi_atari_stack': (c_int, [c_vp, c_i64, c_i64, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp,
                                  c_i64, c_vp]),
+    'acmi_stream_wait_backward_dx': (c_int, [c_vp]),
     'acmi_selftest_plans': (c_int, [c_int]),
     'acmi_gemm_f32': (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp]),
     'acmi_prof_enable': (c_int, [c_int, c_int]),

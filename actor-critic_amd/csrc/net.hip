@@ -804,6 +804,27 @@ static SideStream* side_stream() {
 }
 static long long afactor_ws_floats(int B) { return conv1_afactor_ws_ints(400LL * B); }
 
+// Recorded on the backward's stream right after its input-gradient chain (per
+// device): acmi_stream_wait_backward_dx lets the sampled-loss chain on another
+// stream start there, next to the weight-gradient reductions instead of next to
+// the (memory-bound) input gradients.
+static hipEvent_t* dx_done_event() {
+  static hipEvent_t ev[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!ev[dev] && hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming) != hipSuccess) {
+    ev[dev] = nullptr;
+    return nullptr;
+  }
+  return &ev[dev];
+}
+// the conv1 A factor after the dX chain (default), so that it too runs next to
+// the sampled-loss chain started at the dX event; ACMI_AF_FIRST=1: before it
+static bool afactor_first() {
+  static const bool v = getenv("ACMI_AF_FIRST") && atoi(getenv("ACMI_AF_FIRST")) != 0;
+  return v;
+}
+
 // ---------------------------------------------------------------------------
 // backward (dX chain) shared by the loss backward and the sampled backward
 // ---------------------------------------------------------------------------
@@ -865,6 +886,16 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // conv1 A factor first, on the side stream (its int partials after the shared
   // split-K partials); falls back to this stream when no side stream exists
   SideStream* side = st ? side_stream() : nullptr;
+  auto dx = [&]() -> int {
+    const int r = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s);
+    if (r) return r;
+    hipEvent_t* ev = dx_done_event();
+    ACMI_REQUIRE(ev && hipEventRecord(*ev, s) == hipSuccess, ACMI_ERR_HIP,
+                 "acmi_backward: dX event record failed");
+    return ACMI_OK;
+  };
+  int rc = ACMI_OK;
+  if (!afactor_first() && (rc = dx())) return rc;
   if (st) {
     const long long pcap = bwd_partial_cap(B, L.A, L.C3);
     hipStream_t as = s;
@@ -880,8 +911,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
     prof_end(ACMI_PROF_CONV1_AFACTOR, as);
     if (rc0) return rc0;
   }
-  int rc = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s);
-  if (rc) return rc;
+  if (afactor_first() && (rc = dx())) return rc;
   float* part = ws;
   // heads: X = a4 (512), dY = dhead (A+1 columns: pi | v)
   rc = wgrad_layer(DenseRows{a->a4, 512, B, 512}, 512, B, bw->dhead, bw->ldh, L.A + 1, st,
@@ -1112,6 +1142,13 @@ int acmi_backward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride,
                              cap, s);
   return backward_impl<64>(L, net->params, obs, img_stride, B, acts, bwd, grads, a_stats, ws,
                            cap, s);
+}
+
+int acmi_stream_wait_backward_dx(acmi_stream_t stream) {
+  hipEvent_t* ev = dx_done_event();
+  ACMI_REQUIRE(ev && hipStreamWaitEvent((hipStream_t)stream, *ev, 0) == hipSuccess, ACMI_ERR_HIP,
+               "acmi_stream_wait_backward_dx failed");
+  return ACMI_OK;
 }
 
 int acmi_kfac_output_stats(const acmi_net_t* net, int B, const acmi_acts_t* acts,

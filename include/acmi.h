@@ -214,6 +214,11 @@ int acmi_kfac_output_stats(const acmi_net_t* net, int B,
                            const acmi_acts_t* acts, const acmi_bwd_t* bwd,
                            uint32_t seed, uint32_t stream_id, uint32_t counter,
                            float* g_stats, float* ws, acmi_stream_t stream);
+/* Makes `stream` wait (stream-ordered, no host sync) for the point right after
+ * the input-gradient chain of the most recent acmi_backward on this device, so
+ * a sampled-loss chain (acmi_kfac_output_stats on its own buffers) enqueued on
+ * `stream` afterwards runs next to that backward's weight-gradient reductions. */
+int acmi_stream_wait_backward_dx(acmi_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * K-FAC running factors: zero-initialised EMA with zero-debias (kfac
