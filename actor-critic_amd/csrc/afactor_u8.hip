@@ -19,6 +19,7 @@
 #include <algorithm>
 
 #include "common.hpp"
+#include "symred3.hpp"  // split3, pk_bf16, ds_tr16, cat8, stage_f4 (fused conv1 wgrad)
 
 namespace acmi {
 
@@ -216,20 +217,37 @@ __constant__ int8_t kTri[8][5][2] = {
     {{2, 2}, {2, 3}, {2, 4}, {2, 5}, {2, 6}}, {{2, 7}, {5, 5}, {5, 6}, {5, 7}, {-1, -1}},
     {{3, 3}, {3, 4}, {3, 5}, {3, 6}, {3, 7}}, {{4, 4}, {4, 5}, {4, 6}, {4, 7}, {-1, -1}}};
 
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv1_afactor_i8_tri_kernel(const uint8_t* obs,
+// WG: also the conv1 weight gradient [P;1]^T d1 from the same staged patch bytes
+// (fused with the A factor: the u8 patch gather is shared).  d1 rows are staged
+// next to them, split three ways into a [part][row][32] bf16 image (as
+// conv1_wgrad_x3_kernel's), the patch bytes enter the bf16 MFMAs exactly
+// (u = x ^ 0x80); wave w owns patch columns 32w..32w+31 x all 32 channels.
+// Per-chunk partials [chunk][257][32] (row 256: the bias gradient), reduced by
+// finalize_wgrad_kernel like the separate kernel's.  24 KB more LDS; two waves
+// per SIMD (one block per CU) for the extra registers.
+template <bool WG>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WG ? 2 : 4))) void conv1_afactor_i8_tri_kernel(const uint8_t* obs,
                                                                    long long img_stride, int rows,
                                                                    int chunk_rows, int* part,
-                                                                   int* colsum) {
+                                                                   int* colsum, const float* d1,
+                                                                   float* wpart) {
   const int total = gridDim.x, b = blockIdx.x;
   const int xcd = b & 7, base_l = total >> 3, rem = total & 7;
   const int chunk = xcd * base_l + min(xcd, rem) + (b >> 3);
   const int r_begin = chunk * chunk_rows;
   const int r_end = min(rows, r_begin + chunk_rows);
   __shared__ __attribute__((aligned(16))) uint8_t lds[2][256 * AF_LINE];
+  constexpr int DRA = 64;              // d1 image row bytes: 32 channels x bf16
+  constexpr int DPART = AF_BK * DRA;   // 4 KB per split part
+  __shared__ __attribute__((aligned(16))) char dimg[WG ? 2 : 1][WG ? 3 * DPART : 16];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
+  // d1 staging (WG): 8 threads per row (one float4 each), 64 rows
+  const int drow = tid >> 3, dcol = (tid & 7) * 4;
+  StF4 rd = make_float4(0.f, 0.f, 0.f, 0.f);
+  float dsum[4] = {0.f, 0.f, 0.f, 0.f};
   // staging map: 4 rows (4*q4 .. +3) x 8 columns (8*cg .. +7) per thread, cg < 32
   const int q4 = tid & 15;
   const int cg = tid >> 4;
@@ -251,6 +269,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       ra[q] = *reinterpret_cast<const uint2*>(ok ? obs + (off + (uint32_t)(coff + 16 * q)) : x0);
+    if constexpr (WG) {
+      const int k = r0 + drow;
+      const bool dok = k < r_end;
+      rd = stage_f4(d1 + (long long)(dok ? k : 0) * 32 + dcol, dok);
+    }
   };
   auto transpose4 = [](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t* out) {
     const uint32_t p01l = __builtin_amdgcn_perm(w1, w0, 0x05010400u);
@@ -270,6 +293,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       *reinterpret_cast<uint32_t*>(lds[buf] + (c + j) * AF_LINE + 4 * q4) = cols[j];
+    if constexpr (WG) {
+      dsum[0] += rd.x;
+      dsum[1] += rd.y;
+      dsum[2] += rd.z;
+      dsum[3] += rd.w;
+      uint2 h, m, l;
+      split3(rd.x, rd.y, h.x, m.x, l.x);
+      split3(rd.z, rd.w, h.y, m.y, l.y);
+      char* ds = dimg[buf] + drow * DRA + 2 * dcol;
+      *reinterpret_cast<uint2*>(ds) = h;
+      *reinterpret_cast<uint2*>(ds + DPART) = m;
+      *reinterpret_cast<uint2*>(ds + 2 * DPART) = l;
+    }
   };
 
   int ti[5], tj[5];
@@ -292,6 +328,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0;
   int csum = 0;
+  f32x16 wacc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) wacc[r] = 0.f;
+  // d1 fragment offset in the [k][32] image (conv1_wgrad_x3_kernel's map)
+  const int daoff = (8 * (lane >> 5) + ((lane >> 2) & 3)) * DRA + 8 * (4 * ((lane >> 4) & 1) + (lane & 3));
 
   const int nst = r_end > r_begin ? (r_end - r_begin + AF_BK - 1) / AF_BK : 0;
   if (nst > 0) {
@@ -314,6 +355,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
       for (int t = 0; t < NT; ++t) {
         const v4i bb = *reinterpret_cast<const v4i*>(S + tj[t] * 32 * AF_LINE + 32 * s);
         acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ti[t] == row0 ? a0 : a1, bb, acc[t], 0, 0, 0);
+      }
+    }
+    if constexpr (WG) {
+      // weight gradient: C^T[channel][patch column] over this stage's 64 rows
+      const char* dsb = dimg[cur];
+      const uint8_t* pc = lds[cur] + (32 * wave + (lane & 31)) * AF_LINE + 8 * (lane >> 5);
+#pragma unroll
+      for (int ks = 0; ks < AF_BK / 16; ++ks) {
+        bf16x8 a[3];
+#pragma unroll
+        for (int pt = 0; pt < 3; ++pt) {
+          const char* ap = dsb + pt * DPART + 16 * ks * DRA + daoff;
+          a[pt] = cat8(ds_tr16(ap), ds_tr16(ap + 4 * DRA));
+        }
+        const uint2 xb = *reinterpret_cast<const uint2*>(pc + 16 * ks);
+        const uint32_t u0 = xb.x ^ 0x80808080u, u1 = xb.y ^ 0x80808080u;  // back to u
+        const uint4 pb = make_uint4(pk_bf16((float)(u0 & 255u), (float)((u0 >> 8) & 255u)),
+                                    pk_bf16((float)((u0 >> 16) & 255u), (float)(u0 >> 24)),
+                                    pk_bf16((float)(u1 & 255u), (float)((u1 >> 8) & 255u)),
+                                    pk_bf16((float)((u1 >> 16) & 255u), (float)(u1 >> 24)));
+        const bf16x8 bb = __builtin_bit_cast(bf16x8, pb);
+        wacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bb, wacc, 0, 0, 0);
+        wacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb, wacc, 0, 0, 0);
+        wacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb, wacc, 0, 0, 0);
       }
     }
     if (tid < 256) {  // column sums of x over the staged rows
@@ -342,6 +407,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
     }
   }
   if (tid < 256) colsum[(long long)chunk * 256 + tid] = csum;
+  if constexpr (WG) {
+    // wacc[r]: channel (r&3) + 8(r>>2) + 4(lane>>5), patch column 32w + (lane&31)
+    float* wout = wpart + (long long)chunk * 257 * 32;
+    const int i = 32 * wave + (lane & 31);
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq)
+      *reinterpret_cast<float4*>(wout + i * 32 + 8 * gq + 4 * (lane >> 5)) =
+          make_float4(wacc[4 * gq], wacc[4 * gq + 1], wacc[4 * gq + 2], wacc[4 * gq + 3]);
+    // bias gradient (row 256): the 64 row-threads of each channel group through LDS
+    float* cs = reinterpret_cast<float*>(&lds[0][0]);  // free after the last stage's barrier
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cs[drow * 32 + dcol + e] = dsum[e];
+    __syncthreads();
+    if (tid < 32) {
+      float t = 0.f;
+      for (int r = 0; r < AF_BK; ++r) t += cs[r * 32 + tid];
+      wout[256 * 32 + tid] = t;
+    }
+  }
 }
 
 // chunks for the one-block-per-chunk kernel: 2 blocks per CU resident
@@ -416,13 +500,22 @@ long long conv1_afactor_ws_ints(long long rows) {
   int nchunk, chunk, nt, ct;
   af_plan(rows, &nchunk, &chunk);
   af_plan_tri(rows, &nt, &ct);
-  return (long long)std::max(nchunk, nt) * (65536 + 256) + 2 * (65536 + 256) + 2;
+  return (long long)std::max(nchunk, nt) * (65536 + 256) + 2 * (65536 + 256) + 2 +
+         (long long)nt * 257 * 32 + 4;  // + the fused weight-gradient partials (floats)
+}
+
+// chunks of the one-block-per-chunk (fused) kernel, for the weight-gradient finalize
+int conv1_afactor_fused_chunks(long long rows) {
+  int nt, ct;
+  af_plan_tri(rows, &nt, &ct);
+  return nt;
 }
 
 int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* astat, int* ws,
-                     long long ws_ints, hipStream_t s) {
+                     long long ws_ints, hipStream_t s, const float* d1, float** wpart_out) {
   const long long rows = 400LL * B;
   const bool tri = g_gemm_mode == ACMI_GEMM_X3;
+  ACMI_REQUIRE(!d1 || tri, ACMI_ERR_ARG, "fused conv1 weight gradient needs the bf16x3 mode");
   int nchunk, chunk;
   if (tri)
     af_plan_tri(rows, &nchunk, &chunk);
@@ -435,14 +528,20 @@ int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* ast
                "conv1 A factor: frames must span < 2^32 bytes");
   int* part = ws;
   int* colsum = ws + (long long)nchunk * 65536;
-  if (tri)
-    hipLaunchKernelGGL(conv1_afactor_i8_tri_kernel, dim3(nchunk), dim3(512), 0, s, obs, img_stride,
-                       (int)rows, chunk, part, colsum);
+  long long* sums = reinterpret_cast<long long*>(
+      ((uintptr_t)(colsum + (long long)nchunk * 256) + 7) & ~(uintptr_t)7);
+  // fused weight-gradient partials after the int64 sums (16-byte aligned)
+  float* wpart = reinterpret_cast<float*>(((uintptr_t)(sums + 65536 + 256) + 15) & ~(uintptr_t)15);
+  if (wpart_out) *wpart_out = d1 ? wpart : nullptr;
+  if (tri && d1)
+    hipLaunchKernelGGL(conv1_afactor_i8_tri_kernel<true>, dim3(nchunk), dim3(512), 0, s, obs, img_stride,
+                       (int)rows, chunk, part, colsum, d1, wpart);
+  else if (tri)
+    hipLaunchKernelGGL(conv1_afactor_i8_tri_kernel<false>, dim3(nchunk), dim3(512), 0, s, obs,
+                       img_stride, (int)rows, chunk, part, colsum, nullptr, nullptr);
   else
     hipLaunchKernelGGL(conv1_afactor_i8_kernel, dim3(3 * nchunk), dim3(256), 0, s, obs, img_stride,
                        (int)rows, chunk, part, colsum);
-  long long* sums = reinterpret_cast<long long*>(
-      ((uintptr_t)(colsum + (long long)nchunk * 256) + 7) & ~(uintptr_t)7);
   hipLaunchKernelGGL(conv1_afactor_reduce, dim3(65536 / 64 + 4), dim3(256), 0, s, part, colsum, nchunk,
                      sums);
   hipLaunchKernelGGL(conv1_afactor_finalize, dim3(cdiv(257 * 257, 256)), dim3(256), 0, s, sums,

@@ -108,7 +108,12 @@ inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // afactor_u8.hip: exact-integer conv1 A factor on the i8 matrix cores
 long long conv1_afactor_ws_ints(long long rows);
+// d1 != nullptr (bf16x3 mode): the conv1 weight gradient's per-chunk partials
+// [chunk][257][32] are computed in the same pass (*wpart_out, in ws;
+// conv1_afactor_fused_chunks chunks)
 int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* astat, int* ws,
-                     long long ws_ints, hipStream_t s);
+                     long long ws_ints, hipStream_t s, const float* d1 = nullptr,
+                     float** wpart_out = nullptr);
+int conv1_afactor_fused_chunks(long long rows);
 
 }  // namespace acmi

@@ -820,6 +820,11 @@ static hipEvent_t* dx_done_event() {
 }
 // the conv1 A factor after the dX chain (default), so that it too runs next to
 // the sampled-loss chain started at the dX event; ACMI_AF_FIRST=1: before it
+// ACMI_FUSE_C1=0: the conv1 weight gradient in its own pass (conv1_wgrad_x3_kernel)
+static bool conv1_fused() {
+  static const bool v = !getenv("ACMI_FUSE_C1") || atoi(getenv("ACMI_FUSE_C1")) != 0;
+  return v;
+}
 static bool afactor_first() {
   static const bool v = getenv("ACMI_AF_FIRST") && atoi(getenv("ACMI_AF_FIRST")) != 0;
   return v;
@@ -886,6 +891,8 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // conv1 A factor first, on the side stream (its int partials after the shared
   // split-K partials); falls back to this stream when no side stream exists
   SideStream* side = st ? side_stream() : nullptr;
+  // conv1's weight gradient fused into the A-factor pass (needs d1: after the dX chain)
+  const bool fuse_c1 = st && g_gemm_mode == ACMI_GEMM_X3 && !afactor_first() && conv1_fused();
   auto dx = [&]() -> int {
     const int r = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s);
     if (r) return r;
@@ -906,10 +913,19 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
       as = side->s;
     }
     prof_begin(ACMI_PROF_CONV1_AFACTOR, as);
+    float* wpart = nullptr;
     const int rc0 = conv1_afactor_u8(obs, img_stride, B, astat + L.stat_off[0],
-                                     reinterpret_cast<int*>(ws + pcap), afactor_ws_floats(B), as);
+                                     reinterpret_cast<int*>(ws + pcap), afactor_ws_floats(B), as,
+                                     fuse_c1 ? bw->d1 : nullptr, &wpart);
     prof_end(ACMI_PROF_CONV1_AFACTOR, as);
     if (rc0) return rc0;
+    if (fuse_c1) {  // the conv1 weight gradient came with the A factor: reduce its chunks
+      const long long rows = 400LL * B;
+      WgradDesc d{wpart, conv1_afactor_fused_chunks(rows), 256, 32, 0, 32, grads + L.off[0], 32,
+                  nullptr, nullptr, (int)rows, 1.0f / 255.0f};
+      hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(257 * 32, 256)), dim3(256), 0, as, d);
+      ACMI_LAUNCH_CHECK("conv1 fused weight gradient");
+    }
   }
   if (afactor_first() && (rc = dx())) return rc;
   float* part = ws;
@@ -936,9 +952,10 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // conv1: patches of the u8 observations
   // conv1: weight gradient on the f32 engine; its A factor from the u8 frames on
   // the i8 matrix cores (exact integer sums, afactor_u8.hip)
-  rc = wgrad_layer(ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>{obs, (uint32_t)img_stride, B * 400}, 256,
-                   400LL * B, bw->d1, 32, 32, false, part, ws_cap, grads + L.off[0], 32, nullptr,
-                   nullptr, s, ACMI_PROF_CONV1_WGRAD, 1.0f / 255.0f);  // raw u8 patches
+  if (!fuse_c1)
+    rc = wgrad_layer(ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>{obs, (uint32_t)img_stride, B * 400}, 256,
+                     400LL * B, bw->d1, 32, 32, false, part, ws_cap, grads + L.off[0], 32, nullptr,
+                     nullptr, s, ACMI_PROF_CONV1_WGRAD, 1.0f / 255.0f);  // raw u8 patches
   if (rc || !st) return rc;
   if (side) {  // join the conv1 A factor
     ACMI_REQUIRE(hipEventRecord(side->join, side->s) == hipSuccess &&
