@@ -247,7 +247,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WG ? 2 : 4)
   // d1 staging (WG): 8 threads per row (one float4 each), 64 rows
   const int drow = tid >> 3, dcol = (tid & 7) * 4;
   StF4 rd = make_float4(0.f, 0.f, 0.f, 0.f);
-  float dsum[4] = {0.f, 0.f, 0.f, 0.f};
+  double dsum[4] = {0.0, 0.0, 0.0, 0.0};  // bias gradient: ~8000 rows per thread column
   // staging map: 4 rows (4*q4 .. +3) x 8 columns (8*cg .. +7) per thread, cg < 32
   const int q4 = tid & 15;
   const int cg = tid >> 4;
@@ -294,10 +294,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WG ? 2 : 4)
     for (int j = 0; j < 8; ++j)
       *reinterpret_cast<uint32_t*>(lds[buf] + (c + j) * AF_LINE + 4 * q4) = cols[j];
     if constexpr (WG) {
-      dsum[0] += rd.x;
-      dsum[1] += rd.y;
-      dsum[2] += rd.z;
-      dsum[3] += rd.w;
+      dsum[0] += (double)rd.x;
+      dsum[1] += (double)rd.y;
+      dsum[2] += (double)rd.z;
+      dsum[3] += (double)rd.w;
       uint2 h, m, l;
       split3(rd.x, rd.y, h.x, m.x, l.x);
       split3(rd.z, rd.w, h.y, m.y, l.y);
@@ -416,14 +416,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WG ? 2 : 4)
       *reinterpret_cast<float4*>(wout + i * 32 + 8 * gq + 4 * (lane >> 5)) =
           make_float4(wacc[4 * gq], wacc[4 * gq + 1], wacc[4 * gq + 2], wacc[4 * gq + 3]);
     // bias gradient (row 256): the 64 row-threads of each channel group through LDS
-    float* cs = reinterpret_cast<float*>(&lds[0][0]);  // free after the last stage's barrier
+    double* cs = reinterpret_cast<double*>(&lds[0][0]);  // free after the last stage's barrier
 #pragma unroll
     for (int e = 0; e < 4; ++e) cs[drow * 32 + dcol + e] = dsum[e];
     __syncthreads();
     if (tid < 32) {
-      float t = 0.f;
+      double t = 0.0;
       for (int r = 0; r < AF_BK; ++r) t += cs[r * 32 + tid];
-      wout[256 * 32 + tid] = t;
+      wout[256 * 32 + tid] = (float)t;
     }
   }
 }

@@ -427,36 +427,63 @@ struct WgradDesc {
   float wscale;  // applied to the weight rows (a < K) of the gradient
 };
 
-__global__ void finalize_wgrad_kernel(WgradDesc d) {
+// One block = 32 consecutive outputs x 8 chunk groups: group g sums chunks
+// g, g+8, ... in order (4 loads in flight), then the 8 group sums are added in
+// group order -- a fixed order (deterministic) with 8x the loads in flight of one
+// thread per output.  Outputs: the gradient rows (K+1) x cout, then the upper
+// triangle of the A factor (written to both halves).
+constexpr int kFinGroups = 8;
+__device__ __forceinline__ float chunk_sum_group(const float* p, int n, long long cs, int g) {
+  float s = 0.f;
+  for (int c0 = g; c0 < n; c0 += 4 * kFinGroups) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + u * kFinGroups;
+      v[u] = p[(long long)(c < n ? c : g) * cs];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s += (c0 + u * kFinGroups < n) ? v[u] : 0.f;
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(256) void finalize_wgrad_kernel(WgradDesc d) {
+  __shared__ float red[kFinGroups][32];
   const int K = d.I;
   const long long ngrad = (long long)(K + 1) * d.cout;
   const long long nstat = d.astat ? (long long)(K + 1) * (K + 1) : 0;
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= ngrad + nstat) return;
+  const int el = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const long long idx = (long long)blockIdx.x * 32 + el;
   const long long cs = (long long)(d.I + 1) * d.J;  // chunk stride
+  // the partial this output sums (nullptr: nothing to sum)
+  const float* p = nullptr;
+  int a = 0, b = 0, n = 0;
   if (idx < ngrad) {
-    const int a = (int)(idx / d.cout);
-    const int n = (int)(idx - (long long)a * d.cout);
+    a = (int)(idx / d.cout);
+    n = (int)(idx - (long long)a * d.cout);
     const int row = a < K ? a : d.I;
-    const float* p = d.part + (long long)row * d.J + d.kp + n;
-    const float s = a < K ? chunk_sum(p, d.nchunk, cs) * d.wscale : chunk_sum(p, d.nchunk, cs);
+    p = d.part + (long long)row * d.J + d.kp + n;
+  } else if (idx < ngrad + nstat) {
+    const long long e = idx - ngrad;
+    a = (int)(e / (K + 1));
+    b = (int)(e - (long long)a * (K + 1));
+    // column K (the homogeneous coordinate) = sum of P = column-sum row
+    if (a <= b && a != K) p = b < K ? d.part + (long long)a * d.J + b : d.part + (long long)d.I * d.J + a;
+  }
+  red[g][el] = p ? chunk_sum_group(p, d.nchunk, cs, g) : 0.f;
+  __syncthreads();
+  if (g != 0 || idx >= ngrad + nstat) return;
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < kFinGroups; ++q) s += red[q][el];
+  if (idx < ngrad) {
+    if (a < K) s *= d.wscale;
     if (n < d.nsplit) d.gradA[(long long)a * d.nsplit + n] = s;
     else d.gradB[(long long)a * (d.cout - d.nsplit) + (n - d.nsplit)] = s;
   } else {
-    // upper triangle only (a <= b: consecutive b read consecutive partials),
-    // written to both halves
-    const long long e = idx - ngrad;
-    const int a = (int)(e / (K + 1));
-    const int b = (int)(e - (long long)a * (K + 1));
     if (a > b) return;
-    float s;
-    if (a == K) {
-      s = (float)d.rows;
-    } else {
-      // column K (the homogeneous coordinate) = sum of P = column-sum row
-      const float* p = b < K ? d.part + (long long)a * d.J + b : d.part + (long long)d.I * d.J + a;
-      s = chunk_sum(p, d.nchunk, cs);
-    }
+    if (a == K) s = (float)d.rows;
     s *= 1.0f / (float)d.rows;
     d.astat[(long long)a * (K + 1) + b] = s;
     d.astat[(long long)b * (K + 1) + a] = s;
@@ -708,7 +735,7 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
   prof_end(site, s);
   WgradDesc d{part, nc, I, J, kp, cout, gradA, nsplit, gradB, astat, (int)rows, wscale};
   const long long total = (long long)(K + 1) * cout + (astat ? (long long)(K + 1) * (K + 1) : 0);
-  hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(total, 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(total, 32)), dim3(256), 0, s, d);
   ACMI_LAUNCH_CHECK("wgrad_layer");
   return ACMI_OK;
 }
@@ -923,7 +950,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
       const long long rows = 400LL * B;
       WgradDesc d{wpart, conv1_afactor_fused_chunks(rows), 256, 32, 0, 32, grads + L.off[0], 32,
                   nullptr, nullptr, (int)rows, 1.0f / 255.0f};
-      hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(257 * 32, 256)), dim3(256), 0, as, d);
+      hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(257 * 32, 32)), dim3(256), 0, as, d);
       ACMI_LAUNCH_CHECK("conv1 fused weight gradient");
     }
   }
