@@ -226,6 +226,9 @@ def test_concurrent_g_stats_bit_identical(lib, cuda, monkeypatch):
     monkeypatch.setattr(NetEngine, 'concurrent_stats', False)
     serial = _run_two_updates()
     monkeypatch.setattr(NetEngine, 'concurrent_stats', True)
-    conc = _run_two_updates()
-    for i, (a, b) in enumerate(zip(serial[:4], conc[:4])):
-        assert torch.equal(a, b), i
+    # side chain started with the backward, and at its dX event (acmi_stream_wait_backward_dx)
+    for after_dx in (False, True):
+        monkeypatch.setattr(NetEngine, 'stats_after_dx', after_dx)
+        conc = _run_two_updates()
+        for i, (a, b) in enumerate(zip(serial[:4], conc[:4])):
+            assert torch.equal(a, b), (after_dx, i)
