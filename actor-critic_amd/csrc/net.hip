@@ -638,11 +638,17 @@ struct WgradPlan {
   int I, J, kp, cout_pad, nc, ch;
   bool slabs;  // symred_kernel (slab groups) instead of 128x128 live tiles
   bool six;    // bf16x3 six-slab groups (symred6_kernel)
+  bool six_greedy = false;  // ... with the greedy plan for any K (fc4)
   SymPlan sp;
   SymPlan6 sp6;
   long long floats;
 };
 
+// ACMI_SIX_GREEDY=0: fc4's wgrad + A factor on gemm3 128x128 live tiles instead
+static bool six_greedy_on() {
+  static const bool v = !getenv("ACMI_SIX_GREEDY") || atoi(getenv("ACMI_SIX_GREEDY")) != 0;
+  return v;
+}
 static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows, bool u8 = false,
                             int mode = g_gemm_mode) {
   WgradPlan p;
@@ -654,8 +660,14 @@ static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows, bo
   p.J = p.kp + p.cout_pad;
   p.slabs = with_stats && sym_plan(K, p.cout_pad, &p.sp);  // (f32 patch sources only)
   p.six = p.slabs && mode == ACMI_GEMM_X3 && (symred_variant() == 0 || symred_variant() == 5) && sym_plan6(K, p.cout_pad, &p.sp6);
+  // fc4 (K = 1568, no four-slab plan): greedy six-slab groups instead of 128x128 tiles
+  p.six_greedy = !p.slabs && !u8 && with_stats && mode == ACMI_GEMM_X3 && K % 4 == 0 && six_greedy_on() &&
+                 sym_plan6_greedy(K, p.cout_pad, &p.sp6);
+  if (p.six_greedy) p.six = true;
   if (u8)  // conv1 weight gradient: conv1_wgrad_u8/x3_kernel, one 256x32 block per chunk
     conv1_wgrad_u8_plan(rows, &p.nc, &p.ch, mode);
+  else if (p.six_greedy)  // many groups: one round of blocks, few chunks (partials stay small)
+    plan_rounds(rows, p.sp6.ngroups, kCUs, &p.nc, &p.ch, 2048);
   else if (p.six)  // one 512-thread block per CU (2 x 64 accumulators per wave)
     plan_rounds(rows, p.sp6.ngroups, kCUs, &p.nc, &p.ch);
   else if (p.slabs && mode == ACMI_GEMM_X3)
@@ -1313,6 +1325,43 @@ int acmi_selftest_plans(int max_k) {
           if (cov[(size_t)a * (nb + 1) + b] != 1) return -(K + cp);
       for (int b = 0; b <= nb; ++b)
         if (cs[b] != 1) return -(K + cp);
+    }
+  // greedy six-slab groups (fc4 and the other K): every needed sub-tile exactly once,
+  // at most 16 per group, a half-width tile never in slot 0 under a full one, each
+  // column slab's sum by exactly one (0, b) tile
+  for (int K : {1568, 512, 576})
+    for (int cp : {512, 64, 8}) {
+      SymPlan6 p;
+      if (!sym_plan6_greedy(K, cp, &p)) return -(K + cp + 1);
+      const int J = K + cp, ns = (J + 63) / 64, nbp = (K + 63) / 64;
+      std::vector<int> cov((size_t)ns * ns, 0), cs(ns, 0);
+      for (int g = 0; g < p.ngroups; ++g) {
+        int n = 0;
+        for (int w = 0; w < 8; ++w) {
+          bool half0 = false;
+          for (int t = 0; t < 2; ++t) {
+            const int ra = p.g[g].ra[w][t], cb = p.g[g].cb[w][t];
+            if (ra < 0) {
+              if (t == 0 && p.g[g].ra[w][1] >= 0) return -(K + cp + 1);
+              continue;
+            }
+            ++n;
+            const int a = p.g[g].base[ra], b = p.g[g].base[cb];
+            const bool half = b + 32 >= J;
+            if (t == 0) half0 = half;
+            else if (half0 && !half) return -(K + cp + 1);
+            if (a % 64 || b % 64 || a >= K || b < a || b >= J) return -(K + cp + 1);
+            cov[(size_t)(a / 64) * ns + b / 64]++;
+            if (a == 0) cs[b / 64]++;
+          }
+        }
+        if (n > 16) return -(K + cp + 1);
+      }
+      for (int a = 0; a < nbp; ++a)
+        for (int b = a; b < ns; ++b)
+          if (cov[(size_t)a * ns + b] != 1) return -(K + cp + 1);
+      for (int b = 0; b < ns; ++b)
+        if (cs[b] != 1) return -(K + cp + 1);
     }
   for (long long rows : {1000LL, 4096000LL, 829440LL, 501760LL, 10240LL}) {
     for (int live : {1, 3, 11, 14, 90}) {

@@ -35,7 +35,12 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
 #include <functional>
+#include <map>
+#include <mutex>
+#include <random>
+#include <vector>
 
 #include "symred.hpp"
 
@@ -733,7 +738,7 @@ struct SymGroup6 {
   int8_t ra[8][2];          // per wave and tile: staged slab of the rows (-1: no tile)
   int8_t cb[8][2];          // per wave and tile: staged slab of the columns
 };
-constexpr int kSym6MaxGroups = 8;
+constexpr int kSym6MaxGroups = 48;
 struct SymPlan6 {
   int ngroups;
   SymGroup6 g[kSym6MaxGroups];
@@ -802,6 +807,122 @@ inline bool sym_plan6(int K, int cout_pad, SymPlan6* p) {
     return true;
   }
   return false;
+}
+
+// Six-slab groups for any K (fc4: K = 1568, dY 512 wide): the [P | dY] column
+// space is cut into 64-column slabs at multiples of 64 (a slab may straddle the
+// P/dY boundary; rows >= K of a row slab are computed and dropped by the store
+// mask).  Needed sub-tiles: (a, b), b >= a, a a slab holding P rows.  Groups are
+// built greedily: every slab seeds a candidate six-set grown by the slab adding
+// the most uncovered sub-tiles; the candidate with the most (capped at 16) wins
+// and takes its 16 hardest sub-tiles (those whose slabs have the fewest other
+// uncovered ones), full-width first so a half-width tile never sits in slot 0
+// under a full one.  Five seeded restarts (shuffled tie order), the fewest
+// groups kept: fc4 (1568 | 512) gets ~43 groups for its 525 sub-tiles.  Coverage
+// is checked by acmi_selftest_plans; plans are cached per (K, cout_pad).
+inline bool sym_plan6_greedy_build(int K, int cout_pad, SymPlan6* out) {
+  const int J = K + cout_pad;
+  const int ns = (J + 63) / 64, nbp = (K + 63) / 64;
+  if (ns > 64 || nbp < 1) return false;
+  bool found = false;
+  for (int rs = 0; rs < 5; ++rs) {
+    std::mt19937 rng(12345u + rs);
+    std::vector<char> need((size_t)ns * ns, 0);
+    int remaining = 0;
+    for (int a = 0; a < nbp; ++a)
+      for (int b = a; b < ns; ++b) need[(size_t)a * ns + b] = 1, ++remaining;
+    auto nd = [&](int x, int y) -> int {
+      return x <= y ? need[(size_t)x * ns + y] : need[(size_t)y * ns + x];
+    };
+    SymPlan6 p;
+    int ng = 0;
+    bool ok = true;
+    std::vector<int> order(ns), xs(ns);
+    while (remaining > 0) {
+      if (ng == kSym6MaxGroups) {
+        ok = false;
+        break;
+      }
+      int best_set[6] = {0, 0, 0, 0, 0, 0}, best_key = -1, best_tot = -1;
+      for (int i = 0; i < ns; ++i) order[i] = i;
+      std::shuffle(order.begin(), order.end(), rng);
+      for (int s0 : order) {
+        int set[6] = {s0, 0, 0, 0, 0, 0}, n = 1;
+        while (n < 6) {
+          int bx = -1, bg = -1;
+          xs = order;
+          std::shuffle(xs.begin(), xs.end(), rng);
+          for (int x : xs) {
+            bool in = false;
+            for (int i = 0; i < n; ++i) in |= set[i] == x;
+            if (in) continue;
+            int g = nd(x, x);
+            for (int i = 0; i < n; ++i) g += nd(x, set[i]);
+            if (g > bg) bg = g, bx = x;
+          }
+          set[n++] = bx;
+        }
+        int tot = 0;
+        for (int i = 0; i < 6; ++i)
+          for (int j = i; j < 6; ++j) tot += nd(set[i], set[j]);
+        const int key = std::min(16, tot);
+        if (key > best_key || (key == best_key && tot < best_tot)) {
+          best_key = key, best_tot = tot;
+          for (int i = 0; i < 6; ++i) best_set[i] = set[i];
+        }
+      }
+      std::sort(best_set, best_set + 6);
+      // the set's uncovered sub-tiles, hardest first (fewest other uncovered tiles on their slabs)
+      int deg[6];
+      for (int i = 0; i < 6; ++i) {
+        deg[i] = 0;
+        for (int y = 0; y < ns; ++y) deg[i] += nd(best_set[i], y);
+      }
+      struct T {
+        int i, j, key;
+        bool half;
+      };
+      std::vector<T> tiles;
+      for (int i = 0; i < 6; ++i)
+        for (int j = i; j < 6; ++j)
+          if (nd(best_set[i], best_set[j]))
+            tiles.push_back({i, j, deg[i] + deg[j], 64 * best_set[j] + 32 >= J});
+      std::stable_sort(tiles.begin(), tiles.end(), [](const T& x, const T& y) { return x.key < y.key; });
+      if (tiles.size() > 16) tiles.resize(16);
+      std::stable_sort(tiles.begin(), tiles.end(), [](const T& x, const T& y) { return !x.half && y.half; });
+      SymGroup6& G = p.g[ng];
+      for (int i = 0; i < 6; ++i) G.base[i] = (int16_t)(64 * best_set[i]);
+      for (int w = 0; w < 8; ++w) G.ra[w][0] = G.ra[w][1] = G.cb[w][0] = G.cb[w][1] = -1;
+      for (int m = 0; m < (int)tiles.size(); ++m) {
+        need[(size_t)best_set[tiles[m].i] * ns + best_set[tiles[m].j]] = 0;
+        --remaining;
+        G.ra[m % 8][m / 8] = (int8_t)tiles[m].i;
+        G.cb[m % 8][m / 8] = (int8_t)tiles[m].j;
+      }
+      ++ng;
+    }
+    if (ok && (!found || ng < out->ngroups)) {
+      p.ngroups = ng;
+      *out = p;
+      found = true;
+    }
+  }
+  return found;
+}
+
+inline bool sym_plan6_greedy(int K, int cout_pad, SymPlan6* p) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, std::pair<bool, SymPlan6>> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  const auto key = std::make_pair(K, cout_pad);
+  auto it = cache.find(key);
+  if (it == cache.end()) {
+    SymPlan6 q;
+    const bool ok = sym_plan6_greedy_build(K, cout_pad, &q);
+    it = cache.emplace(key, std::make_pair(ok, q)).first;
+  }
+  if (it->second.first) *p = it->second.second;
+  return it->second.first;
 }
 
 // PIPE: the K-tile loads run two tiles ahead, and tile kt+1's split + LDS
