@@ -129,6 +129,37 @@ __global__ void heads_dx_kernel(const float* dhead, int ldh, int B, const float*
   *reinterpret_cast<float4*>(d4 + q * 4) = o;
 }
 
+// Breakout's A = 4 (16-byte aligned W_pi rows, dhead rows of ldh % 4 == 0): the
+// four W_pi rows and the dhead row as float4 loads (7 loads a thread instead of 26),
+// the same k-ordered fmaf chain per output
+__global__ void heads_dx4_kernel(const float* dhead, int ldh, int B, const float* wpi,
+                                 const float* wv, const float* a4, float* d4) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long long)B * 128) return;
+  const int m = (int)(q >> 7), j0 = (int)(q & 127) * 4;
+  const float* g = dhead + (long long)m * ldh;
+  const float4 g4 = *reinterpret_cast<const float4*>(g);
+  const float gv = g[4];
+  const float4* w4 = reinterpret_cast<const float4*>(wpi + j0 * 4);
+  const float4 x = *reinterpret_cast<const float4*>(a4 + q * 4);
+  float o[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float4 w = w4[e];
+    float acc = __builtin_fmaf(g4.x, w.x, 0.f);
+    acc = __builtin_fmaf(g4.y, w.y, acc);
+    acc = __builtin_fmaf(g4.z, w.z, acc);
+    acc = __builtin_fmaf(g4.w, w.w, acc);
+    o[e] = __builtin_fmaf(gv, wv[j0 + e], acc);
+  }
+  float4 r;
+  r.x = o[0] * (float)(x.x > 0.f);
+  r.y = o[1] * (float)(x.y > 0.f);
+  r.z = o[2] * (float)(x.z > 0.f);
+  r.w = o[3] * (float)(x.w > 0.f);
+  *reinterpret_cast<float4*>(d4 + q * 4) = r;
+}
+
 // conv/fc epilogue with an image remap so the rollout can write step t of an
 // env-major [N][T][rows] activation buffer in place.
 struct EpiAct {
@@ -877,8 +908,12 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
                     const acmi_bwd_t* bw, const float* dhead, int ldh,
                     hipStream_t s) {
   // heads -> d4 = (dhead W_h^T) * relu'(a4)
-  hipLaunchKernelGGL(heads_dx_kernel, dim3(cdiv((long long)B * 128, 256)), dim3(256), 0, s, dhead,
-                     ldh, B, P + L.off[8], P + L.off[10], L.A, a->a4, bw->d4);
+  if (L.A == 4 && ldh % 4 == 0 && (uintptr_t)(P + L.off[8]) % 16 == 0 && (uintptr_t)dhead % 16 == 0)
+    hipLaunchKernelGGL(heads_dx4_kernel, dim3(cdiv((long long)B * 128, 256)), dim3(256), 0, s, dhead,
+                       ldh, B, P + L.off[8], P + L.off[10], a->a4, bw->d4);
+  else
+    hipLaunchKernelGGL(heads_dx_kernel, dim3(cdiv((long long)B * 128, 256)), dim3(256), 0, s, dhead,
+                       ldh, B, P + L.off[8], P + L.off[10], L.A, a->a4, bw->d4);
   {  // fc4 -> d3 = (d4 W4^T) * relu'(a3)
     const int K3 = 49 * C3;
     RowsAsK<DenseRows> opA{DenseRows{bw->d4, 512, B, 512}};
