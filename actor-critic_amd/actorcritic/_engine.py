@@ -144,6 +144,7 @@ class UpdateState(object):
                             self.dhead.data_ptr(), eng.ldh)
         self.actions = None
         self.fwd = None
+        self.loss_reduced = True  # loss slots hold global means (see objectives._Loss)
         self._side = None
 
     def side(self, eng):
@@ -224,7 +225,7 @@ class NetEngine(object):
         net = self.net()
         bwd, ws = (side.bwd, side.ws) if side is not None else (st.bwd, st.bwd_ws)
         _lib.call('acmi_kfac_output_stats', ctypes.byref(net), fwd.M, ctypes.byref(fwd.acts.struct),
-                  ctypes.byref(bwd), seed, self.rank, counter, _lib.ptr(st.gstat), _lib.ptr(ws),
+                  ctypes.byref(bwd), seed, self.rank * fwd.M, counter, _lib.ptr(st.gstat), _lib.ptr(ws),
                   self.stream())
 
     concurrent_stats = os.environ.get('ACMI_CONCURRENT_STATS', '1') != '0'
@@ -268,6 +269,7 @@ class NetEngine(object):
             from actorcritic import parallel
             k = st.red.numel() if with_stats else st.n_grad_red
             parallel.allreduce_sum_(st.red[:k])
+            st.loss_reduced = True
 
     def allreduce_begin(self, st, with_stats):
         """Starts summing what acmi_backward produced -- [grads | losses (| A factor
@@ -279,6 +281,7 @@ class NetEngine(object):
             return None
         from actorcritic import parallel
         k = st.n_grad_red + (self.layout.stat_off[5] if with_stats else 0)
+        st.loss_reduced = True
         return parallel.allreduce_sum_async(st.red[:k])
 
     def allreduce_end(self, st, with_stats, pending):

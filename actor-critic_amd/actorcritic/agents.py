@@ -92,17 +92,26 @@ class _RolloutBuffers(object):
 class MultiEnvAgent(Agent):
     """Multiple envs (MultiEnv), multiple steps (agents.py:134-228)."""
 
-    def __init__(self, multi_env, model, num_steps):
+    def __init__(self, multi_env, model, num_steps, copy_batches=False):
         self._env = multi_env
         self._model = model
         self._num_steps = num_steps
         self._observations = None
         self._bufs = None
+        self._copy = bool(copy_batches)
 
     def _fast(self):
         return getattr(self._env, 'batched', None) is not None and hasattr(self._model, 'engine')
 
     def interact(self, session):
+        """One T-step rollout -> (observations [N,T,...], actions [N,T], rewards [N,T],
+        terminals [N,T], next_observations [N,...], infos) (agents.py:157-228).
+
+        Device rollout aliasing: the returned tensors are the agent's persistent
+        rollout buffers and the NEXT interact() overwrites them in place (the
+        reference returns fresh lists every call).  A caller that keeps a batch
+        across calls (logging, replay, comparing rollouts) clones it, or constructs
+        the agent with ``copy_batches=True`` to receive fresh tensors every call."""
         if self._fast():
             return self._interact_device()
         return self._interact_lists(session)
@@ -199,8 +208,8 @@ class MultiEnvAgent(Agent):
                 src = obs0 + t * OBS_BYTES
                 eng.forward(src, N, rb.acts.view(t, T), want_value=True, img_stride=T * OBS_BYTES, act_stride=T)
                 act_t = rb.actions_tn[t]
-                _lib.call('acmi_sample_actions', _lib.c_vp(rb.acts.logits.data_ptr() + 4 * t * A), T * A, N, A,
-                          seed, eng.rank, eng.sample_counter, None, 0, _lib.c_vp(act_t.data_ptr()),
+                _lib.call('acmi_sample_actions_at', _lib.c_vp(rb.acts.logits.data_ptr() + 4 * t * A), T * A, N,
+                          A, seed, 0, eng.sample_counter, eng.rank * N, None, 0, _lib.c_vp(act_t.data_ptr()),
                           _lib.c_vp(eng._bad_rows.data_ptr()), stream)
                 eng.sample_counter += 1
                 if t + 1 < T:
@@ -213,11 +222,15 @@ class MultiEnvAgent(Agent):
         rb.bad_host.copy_(eng._bad_rows, non_blocking=True)
         rb.bad_event = torch.cuda.Event()
         rb.bad_event.record()
-        fwd = ForwardOut(eng, rb.acts, N, T, rb.obs.view(N * T, 84, 84, 4))
-        eng.register_rollout(rb.obs, fwd)
         self._observations = rb.next_obs
-        return (rb.obs, rb.actions, rb.rewards, rb.terminals.view(torch.bool), rb.next_obs,
-                EpisodeInfoBatch(rb.episode_rewards))
+        out = (rb.obs, rb.actions, rb.rewards, rb.terminals.view(torch.bool), rb.next_obs, rb.episode_rewards)
+        if self._copy:
+            out = tuple(x.clone() for x in out)
+        obs = out[0]
+        # the update re-uses the rollout activations for exactly these observations
+        fwd = ForwardOut(eng, rb.acts, N, T, obs.view(N * T, 84, 84, 4))
+        eng.register_rollout(obs, fwd)
+        return out[:5] + (EpisodeInfoBatch(out[5]),)
 
 
 def _half_step(eng, env, rb, h, N2, T, A, t, seed, dev_ctr=False):
@@ -232,6 +245,9 @@ def _half_step(eng, env, rb, h, N2, T, A, t, seed, dev_ctr=False):
     acts.ws = rb.ws[h].data_ptr()
     acts.ws_floats = rb.ws[h].numel()
     act_t = rb.actions_tn[t].data_ptr() + 4 * n0
+    # the sampler's RNG is keyed by the global env row (stream 0): env shards over
+    # ranks draw exactly what one process stepping all envs would
+    row0 = eng.rank * rb.N + n0
     if dev_ctr:
         ctr_dev, ctr = _lib.c_vp(rb.ctr_dev.data_ptr()), t
     else:
@@ -243,14 +259,14 @@ def _half_step(eng, env, rb, h, N2, T, A, t, seed, dev_ctr=False):
     rew, term, ep = rb.rewards.data_ptr() + 4 * row, rb.terminals.data_ptr() + row, \
         rb.episode_rewards.data_ptr() + 4 * row
     if rb.fused:  # tower + fused heads/sample/env-step tail (acmi_rollout_step)
-        io = _lib.RolloutIO(seed, eng.rank, ctr, ctr_dev, n0, act_t, eng._bad_rows.data_ptr(), env.range_state(n0),
+        io = _lib.RolloutIO(seed, 0, ctr, ctr_dev, row0, act_t, eng._bad_rows.data_ptr(), env.range_state(n0),
                             env.env_offset + n0, env.seed, dst, dstride, rew, term, ep, T)
         _lib.call('acmi_rollout_step', ctypes.byref(eng.net()), ctypes.c_void_p(src), T * OBS_BYTES, N2,
                   ctypes.byref(acts), T, ctypes.byref(io), eng.stream())
         return
     eng.forward(src, N2, acts, want_value=True, img_stride=T * OBS_BYTES, act_stride=T)
     _lib.call('acmi_sample_actions_dev', _lib.c_vp(rb.acts.logits.data_ptr() + 4 * row * A), T * A, N2, A,
-              seed, eng.rank, ctr_dev, ctr, n0, None, 0, _lib.c_vp(act_t),
+              seed, 0, ctr_dev, ctr, row0, None, 0, _lib.c_vp(act_t),
               _lib.c_vp(eng._bad_rows.data_ptr()), eng.stream())
     env.step_range_into(n0, N2, act_t, src, T * OBS_BYTES, dst, dstride, rew, term, ep, T)
 

@@ -14,6 +14,16 @@ import os
 import torch
 
 
+def _first_order(optimizer):
+    """The optimizer whose slot variables a checkpoint carries: the optimizer itself
+    (A2C: clip-wrapped RMSProp) or, for ACKTR, its cold-start optimizer (clip-wrapped
+    Momentum); the K-FAC state is saved separately under kfac/."""
+    if optimizer is None:
+        return None
+    cold = getattr(optimizer, '_cold_optimizer', None)
+    return cold if cold is not None else optimizer
+
+
 def _optimizer_state(optimizer):
     out = {}
     if optimizer is None:
@@ -25,14 +35,8 @@ def _optimizer_state(optimizer):
     for attr in ('cov_updates', 'inverse_updates'):
         if hasattr(optimizer, attr):
             out['kfac_meta/' + attr] = torch.tensor(getattr(optimizer, attr))
-    inner = getattr(optimizer, '_cold_optimizer', None) or getattr(optimizer, '_optimizer', None)
-    inner = getattr(inner, '_optimizer', inner)
-    for name in ('_accum', '_ms', '_mom'):
-        v = getattr(inner, name, None) if inner is not None else None
-        if v is None:
-            v = getattr(optimizer, name, None)
-        if isinstance(v, torch.Tensor):
-            out['opt/' + name] = v.detach().cpu()
+    for name, v in _first_order(optimizer).slots().items():
+        out['opt/' + name] = v.detach().cpu()
     return out
 
 
@@ -69,6 +73,10 @@ def load(path, model, optimizer=None, global_step=None):
         global_step.assign(int(blob['global_step']))
     if optimizer is not None:
         eng = model.engine
+        slots = {k[4:]: v for k, v in blob.items() if k.startswith('opt/')}
+        if slots:
+            # tf.train.Saver restores the slot variables too (a2c_acktr.py:101-102)
+            _first_order(optimizer).restore_slots(eng, slots)
         if any(k.startswith('kfac/') for k in blob) and hasattr(optimizer, '_init_state'):
             st = optimizer._init_state(eng)
             for k, v in blob.items():

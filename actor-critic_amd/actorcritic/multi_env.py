@@ -104,12 +104,12 @@ class MultiEnv(object):
         self._executor.shutdown()
 
 
-def create_subprocess_envs(env_fns):
+def create_subprocess_envs(env_fns, context='spawn'):
     """Creates one :class:`SubprocessEnv` per function, starts them all, then
     initialises them in parallel (multi_env.py:92-118)."""
     envs = []
     for env_fn in env_fns:
-        env = SubprocessEnv(env_fn)
+        env = SubprocessEnv(env_fn, context=context)
         env.start()
         envs.append(env)
     with concurrent.futures.ThreadPoolExecutor(max(1, len(envs))) as executor:
@@ -136,9 +136,14 @@ class SubprocessEnv(object):
     class _Command:
         INIT, STEP, RESET, RENDER, CLOSE = range(5)
 
-    def __init__(self, env_fn, context=None):
+    def __init__(self, env_fn, context='spawn'):
+        # 'spawn' by default: every child -- including one the restart path starts
+        # mid-training, after this process has initialised HIP -- is a fresh
+        # interpreter, never a fork of a GPU-initialised address space.  env_fn must
+        # therefore be picklable (a module-level function or functools.partial);
+        # context='fork' restores the reference's behaviour for CPU-only parents.
         self._env_fn = env_fn
-        self._ctx = multiprocessing.get_context(context) if context else multiprocessing
+        self._ctx = multiprocessing.get_context(context)
         self._parent_connection = self._child_connection = self._process = None
         self._started = False
         self._initialized = False

@@ -85,6 +85,35 @@ class Optimizer(object):
     def _apply_dense(self, ctx, eng, grads, clip_norm):  # pragma: no cover - abstract
         raise NotImplementedError
 
+    # -- slot variables (tf.train.Optimizer slots: saved and restored by checkpoint) --
+    _slot_names = ()
+
+    def _ensure_slots(self, eng):
+        """Allocates the slot variables with their TF initial values (first
+        _apply_dense, or a checkpoint restore before it)."""
+
+    def slots(self):
+        """{name: tensor} of the allocated slot variables."""
+        out = {}
+        for name in self._slot_names:
+            v = getattr(self, name, None)
+            if v is not None:
+                out[name] = v
+        return out
+
+    def restore_slots(self, eng, values):
+        """Copies checkpointed slot values in, allocating the slots first."""
+        unknown = set(values) - set(self._slot_names)
+        if unknown:
+            raise ValueError('{} has no slots {}'.format(type(self).__name__, sorted(unknown)))
+        self._ensure_slots(eng)
+        for name, v in values.items():
+            dst = getattr(self, name)
+            if tuple(dst.shape) != tuple(v.shape):
+                raise ValueError('slot {} has shape {} in the checkpoint, {} here'.format(
+                    name, tuple(v.shape), tuple(dst.shape)))
+            dst.copy_(v.to(dst.device))
+
 
 class MomentumOptimizer(Optimizer):
     """TF1 MomentumOptimizer: accum = m*accum + g;  var -= lr*accum."""
@@ -98,12 +127,17 @@ class MomentumOptimizer(Optimizer):
         self._ws = None
         self.last_norm = None
 
-    def _apply_dense(self, ctx, eng, grads, clip_norm):
+    _slot_names = ('_accum',)
+
+    def _ensure_slots(self, eng):
         import torch
         if self._accum is None:
-            self._accum = torch.zeros_like(eng.params)
+            self._accum = torch.zeros_like(eng.params)  # TF 'momentum' slot: zeros
             self._ws = torch.zeros(int(eng.lib.acmi_opt_ws_floats(eng.params.numel())), device=eng.device)
             self.last_norm = torch.zeros(1, device=eng.device)
+
+    def _apply_dense(self, ctx, eng, grads, clip_norm):
+        self._ensure_slots(eng)
         _lib.call('acmi_momentum_apply', _lib.ptr(eng.params), _lib.ptr(self._accum), _lib.ptr(grads),
                   eng.params.numel(), self._lr(ctx), self._momentum, float(clip_norm), _lib.ptr(self._ws),
                   _lib.ptr(self.last_norm), eng.stream())
@@ -122,13 +156,18 @@ class RMSPropOptimizer(Optimizer):
         self._ms = self._mom = self._ws = None
         self.last_norm = None
 
-    def _apply_dense(self, ctx, eng, grads, clip_norm):
+    _slot_names = ('_ms', '_mom')
+
+    def _ensure_slots(self, eng):
         import torch
         if self._ms is None:
-            self._ms = torch.ones_like(eng.params)
+            self._ms = torch.ones_like(eng.params)  # TF1 RMSProp 'rms' slot starts at 1
             self._mom = torch.zeros_like(eng.params)
             self._ws = torch.zeros(int(eng.lib.acmi_opt_ws_floats(eng.params.numel())), device=eng.device)
             self.last_norm = torch.zeros(1, device=eng.device)
+
+    def _apply_dense(self, ctx, eng, grads, clip_norm):
+        self._ensure_slots(eng)
         _lib.call('acmi_rmsprop_apply', _lib.ptr(eng.params), _lib.ptr(self._ms), _lib.ptr(self._mom),
                   _lib.ptr(grads), eng.params.numel(), self._lr(ctx), self._decay, self._momentum, self._eps,
                   float(clip_norm), _lib.ptr(self._ws), _lib.ptr(self.last_norm), eng.stream())
@@ -156,3 +195,12 @@ class ClipGlobalNormOptimizer(Optimizer):
 
     def _apply_dense(self, ctx, eng, grads, clip_norm):
         self._optimizer._apply_dense(ctx, eng, grads, self._clip_norm)
+
+    def _ensure_slots(self, eng):
+        self._optimizer._ensure_slots(eng)
+
+    def slots(self):
+        return self._optimizer.slots()
+
+    def restore_slots(self, eng, values):
+        self._optimizer.restore_slots(eng, values)

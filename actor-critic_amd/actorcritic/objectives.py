@@ -65,6 +65,10 @@ class SharedLoss(Node):
         loss = ctx.eval(self.objective._loss_node)
         return loss[0] + self.weight * loss[1]
 
+    def _finalize(self, ctx, value):
+        loss = self.objective._loss_node.scalars(ctx)
+        return loss[0] + self.weight * loss[1]
+
 
 class _Targets(Node):
     name = 'target_values'
@@ -111,12 +115,25 @@ class _Loss(Node):
         if actions.numel() != M:
             raise ValueError('actions must have the shape of the observations batch [env, step]')
         st.actions = actions
+        # the kernel scales the loss scalars by 1/world like dhead; they hold the
+        # global means once the update's all-reduce has summed them (loss_reduced)
+        st.loss_reduced = eng.world_size == 1
         _lib.call('acmi_a2c_loss', _lib.ptr(fwd.flat_logits), eng.A, _lib.ptr(fwd.flat_value), _lib.ptr(actions),
                   _lib.ptr(st.targets), _lib.ptr(st.adv), M, eng.A, float(obj._beta), float(obj._vcoef),
                   1.0 / eng.world_size, _lib.ptr(st.dhead), eng.ldh, _lib.ptr(st.loss_ws), _lib.ptr(st.loss),
                   eng.stream())
         st.fwd = fwd
         return st.loss
+
+    def scalars(self, ctx):
+        """[policy, baseline, entropy] of this run as fetched: the global means when
+        the run's optimize op all-reduced them, else (no update in the run) this
+        rank's means -- the kernel's 1/world scale undone."""
+        loss = ctx.eval(self)
+        st = ctx.eval(self.objective._targets_node)
+        if getattr(st, 'loss_reduced', True):
+            return loss[:3]
+        return loss[:3] * float(self.objective._model.engine.world_size)
 
 
 class _LossScalar(Node):
@@ -125,6 +142,9 @@ class _LossScalar(Node):
 
     def _eval(self, ctx):
         return ctx.eval(self.loss_node)[self.index]
+
+    def _finalize(self, ctx, value):
+        return self.loss_node.scalars(ctx)[self.index]
 
 
 class A2CObjective(ActorCriticObjective):

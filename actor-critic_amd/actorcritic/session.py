@@ -22,6 +22,12 @@ class Node(object):
     def _eval(self, ctx):  # pragma: no cover - abstract
         raise NotImplementedError
 
+    def _finalize(self, ctx, value):
+        """The fetched value once every node of the run is enqueued (Session.run calls
+        it for each fetch); nodes whose value depends on later ops of the same run --
+        the loss scalars, reduced over ranks only if the optimize op ran -- override it."""
+        return value
+
     def __add__(self, other):
         return _Sum(self, other)
 
@@ -85,6 +91,9 @@ class _Sum(Node):
     def _eval(self, ctx):
         return ctx.eval(self.a) + ctx.eval(self.b)
 
+    def _finalize(self, ctx, value):
+        return self.a._finalize(ctx, ctx.eval(self.a)) + self.b._finalize(ctx, ctx.eval(self.b))
+
 
 class _Scale(Node):
     def __init__(self, a, k):
@@ -92,6 +101,9 @@ class _Scale(Node):
 
     def _eval(self, ctx):
         return ctx.eval(self.a) * ctx.eval(self.k)
+
+    def _finalize(self, ctx, value):
+        return self.a._finalize(ctx, ctx.eval(self.a)) * self.k._finalize(ctx, ctx.eval(self.k))
 
 
 class Variable(Node):
@@ -175,6 +187,7 @@ class Session(object):
         single = not isinstance(fetches, (list, tuple))
         items = [fetches] if single else list(fetches)
         out = [ctx.eval(f) if f is not None else None for f in items]
+        out = [f._finalize(ctx, v) if isinstance(f, Node) else v for f, v in zip(items, out)]
         if host:
             out = [_to_host(v) for v in out]
         return out[0] if single else out

@@ -1042,7 +1042,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
 // sampled-loss output gradients at the heads (kfac "gradients" mode):
 // g_pi = softmax(z) - onehot(y), y ~ Cat(z);  g_v = V - y_v = -eps, eps~N(0,1)
 __global__ void sampled_head_grad_kernel(const float* logits, int ld, int B, int A,
-                                         uint32_t seed, uint32_t sid, uint32_t ctr,
+                                         uint32_t seed, uint32_t row0, uint32_t ctr,
                                          float* g, int ldg) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= B) return;
@@ -1051,7 +1051,8 @@ __global__ void sampled_head_grad_kernel(const float* logits, int ld, int B, int
   for (int a = 0; a < A; ++a) mx = fmaxf(mx, z[a]);
   float se = 0.f;
   for (int a = 0; a < A; ++a) se += expf(z[a] - mx);
-  const uint32_t h = key4(seed, sid, ctr, (uint32_t)m);
+  // keyed by the global row: a data-parallel shard draws what the full batch would
+  const uint32_t h = key4(seed, 0u, ctr, row0 + (uint32_t)m);
   const float u = u01(h);
   // inverse CDF draw
   const float target = u * se;
@@ -1074,7 +1075,7 @@ __global__ void sampled_head_grad_kernel(const float* logits, int ld, int B, int
 template <int C3>
 static int output_stats_impl(const Layout& L, const float* P, int B,
                              const acmi_acts_t* a, const acmi_bwd_t* bw,
-                             uint32_t seed, uint32_t sid, uint32_t ctr,
+                             uint32_t seed, uint32_t row0, uint32_t ctr,
                              float* gstat, float* ws, long long ws_cap,
                              hipStream_t s) {
   const int ldg = roundup4(L.A + 1) < 8 ? 8 : roundup4(L.A + 1);
@@ -1082,7 +1083,7 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
   float* part = ws + (long long)B * ldg;
   const long long cap = ws_cap - (long long)B * ldg;
   hipLaunchKernelGGL(sampled_head_grad_kernel, dim3(cdiv(B, 128)), dim3(128), 0, s,
-                     a->logits, a->ld_logits, B, L.A, seed, sid, ctr, ghead, ldg);
+                     a->logits, a->ld_logits, B, L.A, seed, row0, ctr, ghead, ldg);
   int rc = dx_chain<C3>(L, P, B, a, bw, ghead, ldg, s);
   if (rc) return rc;
   // heads: G_pi (A x A) from the first A columns, G_v = element (A, A)
@@ -1243,7 +1244,7 @@ int acmi_stream_wait_backward_dx(acmi_stream_t stream) {
 }
 
 int acmi_kfac_output_stats(const acmi_net_t* net, int B, const acmi_acts_t* acts,
-                           const acmi_bwd_t* bwd, uint32_t seed, uint32_t stream_id,
+                           const acmi_bwd_t* bwd, uint32_t seed, uint32_t row_offset,
                            uint32_t counter, float* g_stats, float* ws, acmi_stream_t stream) {
   Layout L;
   ACMI_REQUIRE(net && acts && bwd && g_stats && ws, ACMI_ERR_ARG,
@@ -1253,9 +1254,9 @@ int acmi_kfac_output_stats(const acmi_net_t* net, int B, const acmi_acts_t* acts
   const long long cap = acmi_backward_ws_floats(B, net->num_actions, net->conv3_filters);
   hipStream_t s = (hipStream_t)stream;
   if (L.C3 == 32)
-    return output_stats_impl<32>(L, net->params, B, acts, bwd, seed, stream_id, counter,
+    return output_stats_impl<32>(L, net->params, B, acts, bwd, seed, row_offset, counter,
                                  g_stats, ws, cap, s);
-  return output_stats_impl<64>(L, net->params, B, acts, bwd, seed, stream_id, counter, g_stats,
+  return output_stats_impl<64>(L, net->params, B, acts, bwd, seed, row_offset, counter, g_stats,
                                ws, cap, s);
 }
 

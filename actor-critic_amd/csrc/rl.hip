@@ -144,7 +144,7 @@ __global__ void a2c_loss_kernel(const float* logits, int ld, const float* values
 }
 
 __global__ void a2c_loss_final_kernel(const float* part, int nb, int M, float beta,
-                                      float* out) {
+                                      float scale, float* out) {
   // one wave: deterministic fixed-order sums
   float a = 0.f, b = 0.f, c = 0.f;
   for (int i = threadIdx.x; i < nb; i += 64) {
@@ -156,11 +156,13 @@ __global__ void a2c_loss_final_kernel(const float* part, int nb, int M, float be
   b = wave_sum(b);
   c = wave_sum(c);
   if (threadIdx.x == 0) {
+    // scale = 1/world_size: the SUM all-reduce of the update buffer then leaves
+    // the global means (every rank holds M rows)
     const float mean_pl = a / (float)M;
     const float mean_h = b / (float)M;
-    out[0] = -(mean_pl + beta * mean_h);
-    out[1] = c / (float)M;
-    out[2] = mean_h;
+    out[0] = scale * -(mean_pl + beta * mean_h);
+    out[1] = scale * (c / (float)M);
+    out[2] = scale * mean_h;
   }
 }
 
@@ -347,7 +349,7 @@ int acmi_a2c_loss(const float* logits, int ld, const float* values, const int32_
   hipLaunchKernelGGL(a2c_loss_kernel, dim3(nb), dim3(LOSS_BLOCK), 0, s, logits, ld, values,
                      actions, targets, adv, M, A, beta, vcoef, grad_scale, dhead, ldh, ws);
   hipLaunchKernelGGL(a2c_loss_final_kernel, dim3(1), dim3(64), 0, s, ws, nb, M, beta,
-                     loss_out);
+                     grad_scale, loss_out);
   ACMI_LAUNCH_CHECK("acmi_a2c_loss");
   return ACMI_OK;
 }

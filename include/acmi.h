@@ -165,7 +165,9 @@ int acmi_returns(const float* rewards, const uint8_t* terminals,
  *   L_pi = -(mean(adv*logpi(a)) + beta*mean(H)),  L_v = mean((target-V)^2/2)
  * dhead[m][0..A-1] = dL/dlogits, dhead[m][A] = dL/dV, row stride ldh >= A+1,
  * each scaled by grad_scale (1/world_size for data-parallel means).
- * loss_out[0..2] = (L_pi, L_v, mean entropy) — deterministic two-pass sums.
+ * loss_out[0..2] = grad_scale * (L_pi, L_v, mean entropy) — deterministic
+ * two-pass sums; scaled like dhead so that a SUM all-reduce over the ranks
+ * (the update buffer's loss slots) yields the global means.
  * ws: >= acmi_a2c_loss_ws_floats(M) floats.
  * ---------------------------------------------------------------------- */
 int64_t acmi_a2c_loss_ws_floats(int M);
@@ -205,14 +207,16 @@ int acmi_backward(const acmi_net_t* net, const uint8_t* obs,
  * K-FAC output-factor statistics (kfac "gradients" estimation mode over the
  * predictive distributions registered at policies.py:146-158 and
  * baselines.py:55-69): y_pi ~ Categorical(logits) and y_v ~ N(V, 1) are
- * sampled with the counter RNG (seed, stream_id, counter); the per-example
+ * sampled with the counter RNG keyed (seed, 0, counter, row_offset + b) --
+ * row_offset = the global row of batch row 0 (rank * B for an env shard), so
+ * a data-parallel shard draws exactly the full batch's samples; the per-example
  * gradients of -log p(y) w.r.t. each registered layer output are
  * back-propagated (dX only) and G_l = mean over rows of g g^T is written to
  * g_stats (layout of acmi_kfac_layout, G part).  Reuses bwd->d1..d4 and ws.
  * ---------------------------------------------------------------------- */
 int acmi_kfac_output_stats(const acmi_net_t* net, int B,
                            const acmi_acts_t* acts, const acmi_bwd_t* bwd,
-                           uint32_t seed, uint32_t stream_id, uint32_t counter,
+                           uint32_t seed, uint32_t row_offset, uint32_t counter,
                            float* g_stats, float* ws, acmi_stream_t stream);
 /* Makes `stream` wait (stream-ordered, no host sync) for the point right after
  * the input-gradient chain of the most recent acmi_backward on this device, so

@@ -45,7 +45,17 @@ def _worker(rank, world, port, out_dir):
     g, _, af = oracle.backward(params, acts, dl_full[mine] * world / world, dv_full[mine] * world / world, A, C3,
                                with_a_factors=True)
     stats = np.concatenate([f.ravel() for f in af])
-    red = torch.from_numpy(np.concatenate([g, [1.0, 2.0, 3.0, 0.0], stats]))
+    # loss slots as acmi_a2c_loss writes them: this rank's means scaled by 1/world
+    # (grad_scale), so the SUM all-reduce leaves the global means
+    act_full = rng.integers(0, A, M)
+    tg_full = rng.standard_normal(M)
+    full_pre = oracle.forward(params, obs, A, C3)
+    mine_l = oracle.a2c_loss_and_head_grads(full_pre['logits'][mine], full_pre['value'][mine], act_full[mine],
+                                            tg_full[mine])
+    full_l = oracle.a2c_loss_and_head_grads(full_pre['logits'], full_pre['value'], act_full, tg_full)
+    names = ('policy_loss', 'baseline_loss', 'mean_entropy')
+    loss_slots = [mine_l[k] / world for k in names] + [0.0]
+    red = torch.from_numpy(np.concatenate([g, loss_slots, stats]))
     # the split path of a K-FAC update (engine.allreduce_begin/_end): the prefix
     # [grads | losses | A stats] asynchronously, the G tail synchronously, then wait
     red2 = red.clone()
@@ -63,7 +73,7 @@ def _worker(rank, world, port, out_dir):
     g_full, _, af_full = oracle.backward(params, full, dl_full, dv_full, A, C3, with_a_factors=True)
     np.testing.assert_allclose(grads, g_full, rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(stats_mean, np.concatenate([f.ravel() for f in af_full]), rtol=1e-9, atol=1e-12)
-    assert red[n:n + 3].tolist() == [world * 1.0, world * 2.0, world * 3.0]
+    np.testing.assert_allclose(red[n:n + 3].numpy(), [full_l[k] for k in names], rtol=1e-12)
     # every rank holds bit-identical reduced buffers
     digest = torch.tensor([float(np.frombuffer(red.numpy().tobytes(), np.uint8).astype(np.int64).sum())],
                           dtype=torch.float64)

@@ -334,3 +334,51 @@ def test_losses_and_fetches_through_session(lib, cuda):
     assert me == pytest.approx(ref['mean_entropy'], rel=1e-5)
     assert ent.shape == (N, T) and lp.shape == (N, T)
     np.testing.assert_allclose(ent.reshape(-1), oracle.entropy(full['logits']), rtol=1e-5)
+
+
+@pytest.mark.parametrize('acktr', [False, True])
+def test_resumed_update_is_bit_identical(lib, cuda, tmp_path, acktr):
+    """A checkpoint written between two updates and restored into a fresh graph gives
+    the uninterrupted run's second update bit for bit: the RMSProp ms/mom slots (A2C)
+    and the cold-start Momentum accumulator + K-FAC velocity (ACKTR, gs < 30) come
+    back with the parameters and the global step (a2c_acktr.py:101-102)."""
+    from actorcritic import checkpoint
+    from actorcritic import session as sess
+    C3 = 32 if acktr else 64
+    env, model, agent, obj, gs, opt, op, params = _build(3, 4, C3=C3)
+    with sess.Session() as s:
+        s.run(op, feed_dict=_feed(model, agent.interact(s)))
+        # a fresh copy of the second batch: both runs below take the same inputs
+        # (and the same batched forward -- no rollout-cache hit on a copy)
+        data = tuple(x.clone() if isinstance(x, torch.Tensor) else x for x in agent.interact(s))
+        path = checkpoint.save(str(tmp_path / 'Atari'), gs.value, model, opt)
+        s.run(op, feed_dict=_feed(model, data))
+    torch.cuda.synchronize()
+    uninterrupted, gs_after = model.params.clone(), gs.value
+
+    env, model2, agent2, obj2, gs2, opt2, op2, _ = _build(3, 4, C3=C3)
+    checkpoint.load(path, model2, opt2, gs2)
+    with sess.Session() as s:
+        s.run(op2, feed_dict=_feed(model2, data))
+    torch.cuda.synchronize()
+    assert gs2.value == gs_after
+    assert not torch.equal(model2.params, torch.from_numpy(params).cuda())
+    assert torch.equal(model2.params, uninterrupted)
+
+
+def test_copy_batches_returns_fresh_tensors(lib, cuda):
+    """copy_batches=True: a kept batch survives the next interact(); its update still
+    re-uses the rollout activations (same result as the aliased buffers)."""
+    from actorcritic import session as sess
+    from actorcritic.agents import MultiEnvAgent
+    env, model, agent, obj, gs, opt, op, params = _build(3, 4)
+    agent = MultiEnvAgent(env, model, 4, copy_batches=True)
+    with sess.Session() as s:
+        first = agent.interact(s)
+        assert model.engine.lookup_rollout(first[0]) is not None
+        kept = [x.clone() for x in first[:5]]
+        second = agent.interact(s)
+        for a, b in zip(first[:5], kept):
+            assert torch.equal(a, b)
+        assert first[0].data_ptr() != second[0].data_ptr()
+        assert model.engine.lookup_rollout(first[0]) is None  # superseded: recomputed if fed

@@ -67,6 +67,9 @@ def test_protocol_and_errors():
 
 def test_child_crash_restarts_transparently():
     env = SubprocessEnv(make_env)
+    # children (restarts included) are fresh interpreters, never forks of a parent
+    # that may have initialised HIP
+    assert env._ctx.get_start_method() == 'spawn'
     env.start()
     env.initialize()
     env.reset()
