@@ -57,6 +57,9 @@ _SIGS = {
     'acmi_abi_version': (c_int, []),
     'acmi_set_gemm_mode': (c_int, [c_int]),
     'acmi_get_gemm_mode': (c_int, []),
+    'acmi_set_conv_stats_mode': (c_int, [c_int]),
+    'acmi_get_conv_stats_mode': (c_int, []),
+    'acmi_band_info': (c_int, [c_int, c_int, c_i64, ctypes.POINTER(c_i64)]),
     'acmi_param_count': (c_i64, [c_int, c_int]),
     'acmi_param_offsets': (c_int, [c_int, c_int, ctypes.POINTER(c_i64)]),
     'acmi_kfac_layout': (c_int, [c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
@@ -112,6 +115,9 @@ _SIGS = {
 
 GEMM_F32 = 0  # acmi_set_gemm_mode: v_mfma_f32_32x32x2_f32
 GEMM_X3 = 1   # bf16x3 split operands on the bf16 matrix cores (default)
+
+CONV_STATS_PATCHES = 0  # acmi_set_conv_stats_mode: im2col patch rows
+CONV_STATS_BAND = 1     # pixel-pair band reduction (default)
 
 PROF_CONV1_WGRAD = 1
 PROF_CONV2_WGRAD = 2

@@ -18,6 +18,7 @@
 #include "conv1u8.hpp"
 #include "convt3.hpp"
 #include "convfwd3.hpp"
+#include "band.hpp"
 #include "stepper.hpp"
 
 namespace acmi {
@@ -665,6 +666,17 @@ int g_gemm_mode = [] {
   return (e && e[0] == 'f') ? ACMI_GEMM_F32 : ACMI_GEMM_X3;
 }();
 
+// conv2 / conv3 weight gradient + A factor (acmi_set_conv_stats_mode): pixel-pair
+// band reduction (band.hpp, bf16x3 only) or the patch-row symmetric reduction.
+// Initial value from ACMI_BAND ("0": patch rows), default band.
+int g_conv_stats_mode = [] {
+  const char* e = getenv("ACMI_BAND");
+  return (e && e[0] == '0') ? ACMI_CONV_STATS_PATCHES : ACMI_CONV_STATS_BAND;
+}();
+static bool band_on(bool with_stats) {
+  return with_stats && g_gemm_mode == ACMI_GEMM_X3 && g_conv_stats_mode == ACMI_CONV_STATS_BAND;
+}
+
 struct WgradPlan {
   int I, J, kp, cout_pad, nc, ch;
   bool slabs;  // symred_kernel (slab groups) instead of 128x128 live tiles
@@ -842,6 +854,9 @@ static long long bwd_partial_cap(int B, int A, int C3) {
       m = std::max(m, gcov_plan(co[l], rowsL[l]).floats);
     }
   }
+  // band reductions of conv2 / conv3 (rows = images)
+  m = std::max(m, band_ws_floats(band_host_plan(20, 20, 32, 4, 4, 2, 64), B));
+  m = std::max(m, band_ws_floats(band_host_plan(9, 9, 64, 3, 3, 1, C3), B));
   return m;
 }
 
@@ -1013,15 +1028,23 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
                    part, ws_cap, grads + L.off[6], 512, nullptr,
                    st ? astat + L.stat_off[3] : nullptr, s);
   if (rc) return rc;
-  // conv3: patches of a2
-  rc = wgrad_layer(ConvRows<float, 9, 9, 64, 3, 3, 1>{a->a2, 81 * 64, B * 49}, 576, 49LL * B,
-                   bw->d3, C3, C3, st, part, ws_cap, grads + L.off[4], C3, nullptr,
-                   st ? astat + L.stat_off[2] : nullptr, s);
+  // conv3 / conv2: pixel-pair band reductions over the dense activation rows
+  // (band.hpp), or the patches of a2 / a1
+  if (band_on(st))
+    rc = band_layer(a->a2, 9, 9, 64, 3, 3, 1, bw->d3, C3, B, part, ws_cap, grads + L.off[4],
+                    astat + L.stat_off[2], 1.f, s);
+  else
+    rc = wgrad_layer(ConvRows<float, 9, 9, 64, 3, 3, 1>{a->a2, 81 * 64, B * 49}, 576, 49LL * B,
+                     bw->d3, C3, C3, st, part, ws_cap, grads + L.off[4], C3, nullptr,
+                     st ? astat + L.stat_off[2] : nullptr, s);
   if (rc) return rc;
-  // conv2: patches of a1
-  rc = wgrad_layer(ConvRows<float, 20, 20, 32, 4, 4, 2>{a->a1, 400 * 32, B * 81}, 512,
-                   81LL * B, bw->d2, 64, 64, st, part, ws_cap, grads + L.off[2], 64, nullptr,
-                   st ? astat + L.stat_off[1] : nullptr, s, ACMI_PROF_CONV2_WGRAD);
+  if (band_on(st))
+    rc = band_layer(a->a1, 20, 20, 32, 4, 4, 2, bw->d2, 64, B, part, ws_cap, grads + L.off[2],
+                    astat + L.stat_off[1], 1.f, s, ACMI_PROF_CONV2_WGRAD);
+  else
+    rc = wgrad_layer(ConvRows<float, 20, 20, 32, 4, 4, 2>{a->a1, 400 * 32, B * 81}, 512,
+                     81LL * B, bw->d2, 64, 64, st, part, ws_cap, grads + L.off[2], 64, nullptr,
+                     st ? astat + L.stat_off[1] : nullptr, s, ACMI_PROF_CONV2_WGRAD);
   if (rc) return rc;
   // conv1: patches of the u8 observations
   // conv1: weight gradient on the f32 engine; its A factor from the u8 frames on
@@ -1116,6 +1139,35 @@ int acmi_set_gemm_mode(int mode) {
   return ACMI_OK;
 }
 int acmi_get_gemm_mode(void) { return g_gemm_mode; }
+
+int acmi_set_conv_stats_mode(int mode) {
+  ACMI_REQUIRE(mode == ACMI_CONV_STATS_PATCHES || mode == ACMI_CONV_STATS_BAND, ACMI_ERR_ARG,
+               "acmi_set_conv_stats_mode: unknown mode %d", mode);
+  g_conv_stats_mode = mode;
+  return ACMI_OK;
+}
+int acmi_get_conv_stats_mode(void) { return g_conv_stats_mode; }
+
+int acmi_band_info(int layer, int C3, int64_t rows, int64_t* info) {
+  ACMI_REQUIRE(info && (layer == 1 || layer == 2) && (C3 == 32 || C3 == 64) && rows > 0, ACMI_ERR_ARG,
+               "acmi_band_info: bad arguments");
+  const BandPlan* p = layer == 1 ? band_host_plan(20, 20, 32, 4, 4, 2, 64) : band_host_plan(9, 9, 64, 3, 3, 1, C3);
+  ACMI_REQUIRE(p, ACMI_ERR_ARG, "acmi_band_info: no plan");
+  int nc, ch;
+  band_chunks(rows, (int)p->groups.size(), &nc, &ch);
+  info[0] = p->ntiles;
+  info[1] = (int64_t)p->groups.size();
+  info[2] = nc;
+  info[3] = ch;
+  int units = 0;
+  for (const BandGroup& G : p->groups) {
+    int t = 0;
+    for (int w = 0; w < 8; ++w) t += (G.ra[w][0] >= 0) + (G.ra[w][1] >= 0);
+    units += (t + 3) / 4;
+  }
+  info[4] = units;  // sum over groups of the busiest SIMD's sub-tiles
+  return ACMI_OK;
+}
 
 int64_t acmi_param_count(int A, int C3) {
   Layout L;
@@ -1404,6 +1456,19 @@ int acmi_selftest_plans(int max_k) {
       int nc, ch;
       plan_rounds(rows, live, 1024, &nc, &ch);
       if (ch % 32 != 0 || (long long)nc * ch < rows || (long long)(nc - 1) * ch >= rows) return -1;
+    }
+  }
+  // band plans (conv2, conv3 at C3 = 32 / 64): exact cover, column-sum owners,
+  // and the fold tables reproduce the patch-row sums (host emulation in double)
+  const int bshape[3][7] = {{20, 20, 32, 4, 4, 2, 64}, {9, 9, 64, 3, 3, 1, 32}, {9, 9, 64, 3, 3, 1, 64}};
+  for (int i = 0; i < 3; ++i) {
+    const int* b = bshape[i];
+    const BandPlan* p = band_host_plan(b[0], b[1], b[2], b[3], b[4], b[5], b[6]);
+    if (!p || band_plan_check(*p) != 0 || band_plan_emulate(*p) > 1e-12) return -(1000 + i);
+    for (long long rows : {1LL, 37LL, 10240LL, 20480LL}) {
+      int nc, ch;
+      band_chunks(rows, (int)p->groups.size(), &nc, &ch);
+      if (ch % 16 != 0 || (long long)nc * ch < rows || (long long)(nc - 1) * ch >= rows) return -(1010 + i);
     }
   }
   return 0;

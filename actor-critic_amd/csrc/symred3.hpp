@@ -930,19 +930,27 @@ inline bool sym_plan6_greedy(int K, int cout_pad, SymPlan6* p) {
 // instead of after both sub-tiles.  With one 512-thread block per CU the two
 // waves of a SIMD share the block's barrier phase, so without this a SIMD's
 // MFMA pipe idles through every commit.
-template <class Op, class Epi, bool PIPE = false>
+// Plan = SymPlan6 (by value: groups over the upper triangle, dense partials
+// [chunk][I+1][J] through store_tile) or BandPlanDev (band.hpp: groups in device
+// memory, each sub-tile stored to its compact slot [chunk][tile][64][64] and
+// each slab's column sums by its owning group, EpiBand).
+template <class Op, class Epi, bool PIPE = false, class Plan = SymPlan6>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_chunk) {
+void symred6_kernel(Op op, Epi epi, Plan plan, int I, int J, int K, int k_chunk) {
+  constexpr bool kBand = !std::is_same<Plan, SymPlan6>::value;
   constexpr int BK = kX3Rows;
   __shared__ __attribute__((aligned(16))) char lds[2 * kSixBuf];
 
   const int total = gridDim.x;
   const int b = blockIdx.x;
   const int xcd = b & 7, base8 = total >> 3, rem = total & 7;
-  const int l = xcd * base8 + min(xcd, rem) + (b >> 3);
+  int l = xcd * base8 + min(xcd, rem) + (b >> 3);
+  if constexpr (kBand) {
+    if (!plan.xcd_remap) l = b;  // dispatch order: every XCD on the same chunk of rows
+  }
   const int ng = plan.ngroups;
   const int bz = l / ng;
-  const SymGroup6& G = plan.g[l - bz * ng];
+  const auto& G = plan.g[l - bz * ng];
   set_z(epi, bz);
   const int kbeg = bz * k_chunk;
   const int kend = min(K, kbeg + k_chunk);
@@ -1115,16 +1123,40 @@ void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_ch
 #pragma unroll
   for (int e = 0; e < 12; ++e) cs[srow * 384 + scol + e] = csum[e];
   __syncthreads();
+  if constexpr (kBand) {
+    const int khalf = lane >> 5;
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    if (t >= ntile) break;
-    store_tile<2, 2>(epi, acc[t], ib[t], jb[t], lane, I, J);
-    if (ib[t] == 0) {  // the (0, b) sub-tile is unique: its wave writes slab b's column sums
-      const int col = 64 * G.cb[wave][t] + lane;
+    for (int t = 0; t < 2; ++t) {
+      if (t >= ntile) break;
+      float* dst = epi.part + ((long long)bz * epi.ntiles + G.tile[wave][t]) * 4096;
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            dst[(32 * tm + (r & 3) + 8 * (r >> 2) + 4 * khalf) * 64 + 32 * tn + (lane & 31)] =
+                acc[t][tm][tn][r];
+    }
+    if (wave < 6 && ((G.csown >> wave) & 1)) {  // this group owns staged slab `wave`'s sums
+      const int col = 64 * wave + lane;
       float v = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) v += cs[r * 384 + col];
-      if (jb[t] + lane < J) epi.colsum(jb[t] + lane, v);
+      epi.cs[(long long)bz * epi.ncols + G.base[wave] + lane] = v;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (t >= ntile) break;
+      store_tile<2, 2>(epi, acc[t], ib[t], jb[t], lane, I, J);
+      if (ib[t] == 0) {  // the (0, b) sub-tile is unique: its wave writes slab b's column sums
+        const int col = 64 * G.cb[wave][t] + lane;
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v += cs[r * 384 + col];
+        if (jb[t] + lane < J) epi.colsum(jb[t] + lane, v);
+      }
     }
   }
 }

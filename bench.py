@@ -153,9 +153,21 @@ def main():
     # 64x64 sub-tiles per pixel (2*44*64*64 FLOP), reported as executed_tflops.
     M = N * T
     rows = 81 * M
-    x3 = acktr and _lib.load().acmi_get_gemm_mode() == _lib.GEMM_X3
-    if acktr:
-        kern_flops = 2.0 * (513 * 514 / 2 + 513 * 64) * rows
+    lib = _lib.load()
+    x3 = acktr and lib.acmi_get_gemm_mode() == _lib.GEMM_X3
+    band = x3 and lib.acmi_get_conv_stats_mode() == _lib.CONV_STATS_BAND
+    patch_flops = 2.0 * (513 * 514 / 2 + 513 * 64) * rows  # the patch-row sums it replaces
+    if band:
+        # pixel-pair band reduction (band.hpp): the needed 64x64 sub-tiles of
+        # [X | dY]^T [X | dY] over the M images' dense rows, 2*64*64 FLOP per
+        # sub-tile and image; every executed sub-tile is needed
+        info = (ctypes.c_int64 * 5)()
+        _lib.call('acmi_band_info', 1, C3, M, info)
+        kern_flops = exec_flops = 2.0 * 64 * 64 * info[0] * M
+        kern_name = ('conv2 band reduction: wgrad + K-FAC A factor over pixel-pair sub-tiles '
+                     '(bf16x3 split-operand MFMA, f32-accurate)')
+    elif acktr:
+        kern_flops = patch_flops
         exec_flops = 2.0 * 44 * 64 * 64 * rows
         kern_name = ('conv2 wgrad + K-FAC A-factor reduction GEMM (bf16x3 split-operand MFMA, f32-accurate)'
                      if x3 else 'conv2 wgrad + K-FAC A-factor reduction GEMM (f32 MFMA)')
@@ -173,6 +185,13 @@ def main():
                 'frac': (achieved / peak) if achieved else None, 'traffic': traffic,
                 'launches': cnt.value, 'avg_ms': kern_ms, 'flops_per_launch': kern_flops,
                 'executed_tflops': executed}
+    if band and achieved:
+        roofline['sub_tiles'] = int(info[0])
+        roofline['groups'] = int(info[1])
+        roofline['chunks'] = int(info[2])
+        # the patch-row formulation's unique FLOPs over the same time: the rate
+        # the replaced kernel would have needed to match
+        roofline['patch_equivalent_tflops'] = patch_flops / (kern_ms * 1e-3) / 1e12
     if x3 and achieved:
         # peak = bf16 dense peak / 6 (f32-equivalent); the same rate against the
         # f32-input MFMA peak, and the bf16 MFMA work actually issued

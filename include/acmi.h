@@ -48,6 +48,27 @@ int acmi_abi_version(void);
 int acmi_set_gemm_mode(int mode);
 int acmi_get_gemm_mode(void);
 
+/* How conv2 / conv3 form their weight gradient + A factor in ACMI_GEMM_X3 mode
+ * (both fp32-accurate, same sums reassociated):
+ *   ACMI_CONV_STATS_BAND    pixel-pair band reduction (default): each pair of
+ *                           input pixels sharing a patch is multiplied once over
+ *                           the images' dense activation rows, the patch sums
+ *                           folded afterwards (2.5x / 1.6x fewer MACs for conv3 /
+ *                           conv2 than patch rows, no im2col gather)
+ *   ACMI_CONV_STATS_PATCHES [P;1]^T [P | dY] over the im2col patch rows
+ * Initial mode from ACMI_BAND ("0" = patches).  The band plans (sub-tile
+ * groups, fold tables) are built on the first backward of each device and
+ * kept for the process: that first acmi_backward allocates and synchronises
+ * once (do not capture it in a graph).  Not stream-ordered. */
+#define ACMI_CONV_STATS_PATCHES 0
+#define ACMI_CONV_STATS_BAND 1
+int acmi_set_conv_stats_mode(int mode);
+int acmi_get_conv_stats_mode(void);
+/* plan facts of the band reduction of conv2 (layer 1) or conv3 (layer 2) at
+ * `rows` images: info[0] sub-tiles, [1] groups (blocks per chunk), [2] chunks,
+ * [3] rows per chunk, [4] sum over groups of the busiest SIMD's sub-tiles */
+int acmi_band_info(int layer, int C3, int64_t rows, int64_t* info);
+
 /* ------------------------------------------------------------------------
  * Model layout.  Replaces AtariModel._build_params
  * (actorcritic/envs/atari/model.py:129-170, nn.py:8-84).

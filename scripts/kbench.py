@@ -82,8 +82,23 @@ def inverse(A=4, C3=32, reps=10):
     print('kfac inverse (all 12 damped inverses): {:.3f} ms'.format(ms))
 
 
+def band_scaling(sizes=(1024, 2048, 4096, 10240)):
+    """conv2 band kernel time vs images: against its MFMA-bound time (sum over
+    groups of the busiest SIMD's sub-tiles x 4 x 6 MFMAs of 32 cycles per 16
+    image rows, over 256 CUs at 2.4 GHz) -- memory effects show as a growing ratio"""
+    for M in sizes:
+        info = (ctypes.c_int64 * 5)()
+        _lib.call('acmi_band_info', 1, 32, M, info)
+        bound_ms = info[4] * 4 * 6 * 32 * (M / 16.0) / 256 / 2.4e9 * 1e3
+        _lib.call('acmi_prof_enable', 2, 64)
+        backward(M, True, 2, reps=6)
+        print('   M={} plan {} -> MFMA-bound {:.3f} ms'.format(M, list(info), bound_ms))
+
+
 if __name__ == '__main__':
     what = sys.argv[1]
+    if what == 'band':
+        band_scaling()
     if what == 'inverse':
         inverse()
     elif what == 'gemm':

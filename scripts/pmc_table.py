@@ -21,6 +21,9 @@ def main(d):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = short(row['Kernel_Name'])
+                g = row.get('Grid_Size') or row.get('Grid_Size_X')
+                if g:  # one kernel at several shapes (the band reductions of conv2 / conv3)
+                    k = '{} [grid {}]'.format(k, g)
                 vals[k][row['Counter_Name']].append((row['Dispatch_Id'], float(row['Counter_Value'])))
     for k, cs in sorted(vals.items()):
         print(k)

@@ -3,7 +3,11 @@ FETCH_SIZE and WRITE_SIZE passes (separate rocprofv3 runs), with the gfx950
 correction of MI355X_MICROARCH.md (FETCH_SIZE x2, WRITE_SIZE as reported; both
 in KB), written as the profiles/<round>/pmc_traffic.json that bench.py reads.
 
-  python scripts/pmc_traffic.py gpurun_out/pmc_bench3 profiles/r01/pmc_traffic.json
+  python scripts/pmc_traffic.py gpurun_out/pmc_bench3 profiles/r01/pmc_traffic.json [band GRID]
+
+With `band GRID` the kernel is the conv2 band reduction (symred6_kernel with
+EpiBand; the conv3 one has another grid size, GRID = groups x chunks x 512 of
+conv2, acmi_band_info).
 """
 import collections
 import csv
@@ -18,12 +22,20 @@ WORKLOAD = 'Breakout ACKTR 512 envs/GPU x 20 steps'
 ALGO_INPUT_BYTES = 736624640  # a1 patches source + d2 read once (DESIGN.md Roofline)
 
 
+BAND_KERNEL = ('conv2 band reduction: wgrad + K-FAC A factor over pixel-pair sub-tiles '
+               '(bf16x3 split-operand MFMA, f32-accurate)')
+BAND_MATCH = 'EpiBand'
+GRID = None
+
+
 def per_dispatch(d, counter):
     vals = collections.defaultdict(float)
     for f in glob.glob(os.path.join(d, '*', '*_counter_collection.csv')):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if row['Counter_Name'] == counter and MATCH in row['Kernel_Name']:
+                    if GRID is not None and int(row.get('Grid_Size') or row.get('Grid_Size_X')) != GRID:
+                        continue
                     vals[row['Dispatch_Id']] += float(row['Counter_Value'])
     return list(vals.values())
 
@@ -55,4 +67,6 @@ def main(d, out):
 
 
 if __name__ == '__main__':
+    if len(sys.argv) > 4 and sys.argv[3] == 'band':
+        KERNEL, MATCH, GRID = BAND_KERNEL, BAND_MATCH, int(sys.argv[4])
     main(sys.argv[1], sys.argv[2])

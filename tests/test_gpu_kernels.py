@@ -204,6 +204,92 @@ def test_x3_gemms_are_f32_class(lib, cuda):
     assert ratios[len(ratios) // 2] <= 3.0, ratios
 
 
+def _with_conv_stats(lib, mode, fn, *a, **k):
+    prev = lib.acmi_get_conv_stats_mode()
+    _lib.call('acmi_set_conv_stats_mode', mode)
+    try:
+        return fn(*a, **k)
+    finally:
+        _lib.call('acmi_set_conv_stats_mode', prev)
+
+
+def test_band_conv_stats_match_float64(lib, cuda):
+    """conv2 / conv3 weight gradients and A factors from the pixel-pair band
+    reduction (band.hpp) vs float64 and vs the patch-row reduction: the same
+    sums reassociated, so f32-class (<= 5e-6 relative) and within 10x of the
+    patch path's error (floored at 5e-7)."""
+    eb = _with_conv_stats(lib, _lib.CONV_STATS_BAND, _backward_errors, lib, cuda, B=24, seed=5)
+    ep = _with_conv_stats(lib, _lib.CONV_STATS_PATCHES, _backward_errors, lib, cuda, B=24, seed=5)
+    for key in ep:
+        print(key, 'band %.3g  patches %.3g' % (eb[key], ep[key]))
+    for key in ep:
+        assert eb[key] <= 5e-6 and eb[key] <= 10 * max(ep[key], 5e-7), (key, eb[key], ep[key])
+
+
+def _band_backward(lib, cuda, B, mode, reps=1, seed=8):
+    """(grads, A-factor stats) of acmi_backward in conv-stats `mode`, `reps` times"""
+    A, C3 = 4, 32
+    params = rand_params(A, C3, cuda, seed=seed)
+    g = torch.Generator().manual_seed(seed + 1)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
+    t, acts = alloc_acts(B, A, C3, cuda)
+    net = _net(params, A, C3)
+    _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+              _lib.stream_handle())
+    ldh = 8
+    dhead = torch.zeros(B, ldh)
+    dhead[:, :A + 1] = torch.randn(B, A + 1, generator=g) / B
+    dhead = dhead.to(cuda)
+    z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=cuda)
+    d = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
+    bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
+    din = (ctypes.c_int64 * 6)()
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, din, None, so, ctypes.byref(tot))
+    ws = z(lib.acmi_backward_ws_floats(B, A, C3))
+    outs = []
+    for _ in range(reps):
+        grads, astat = z(params.numel()), z(tot.value)
+        _with_conv_stats(lib, mode, _lib.call, 'acmi_backward', ctypes.byref(net), _lib.ptr(obs),
+                         84 * 84 * 4, B, ctypes.byref(acts), ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat),
+                         _lib.ptr(ws), _lib.stream_handle())
+        torch.cuda.synchronize()
+        outs.append((grads.cpu(), astat.cpu()))
+    return outs, list(din), list(so), _layout(A, C3)[0]
+
+
+def test_band_chunked_matches_patch_rows(lib, cuda):
+    """At B = 1100 images the band reduction splits the images into chunks
+    (per-chunk partials, in-order chunk reduction): conv2 / conv3 gradient blocks
+    and A factors agree with the patch-row reduction to f32 accuracy."""
+    B = 1100
+    info = (ctypes.c_int64 * 5)()
+    _lib.call('acmi_band_info', 1, 32, B, info)
+    assert info[2] >= 2, list(info)
+    (ob,), din, so, off = _band_backward(lib, cuda, B, _lib.CONV_STATS_BAND)
+    (op,), _, _, _ = _band_backward(lib, cuda, B, _lib.CONV_STATS_PATCHES)
+    for blk in (2, 3, 4, 5):  # conv2 W, b, conv3 W, b
+        a, b = ob[0][off[blk]:off[blk + 1]].double(), op[0][off[blk]:off[blk + 1]].double()
+        rel = (a - b).abs().max().item() / b.abs().max().item()
+        assert rel < 1e-5, (blk, rel)
+    for f in (1, 2):
+        a = ob[1][so[f]:so[f] + din[f] * din[f]].double()
+        b = op[1][so[f]:so[f] + din[f] * din[f]].double()
+        rel = (a - b).abs().max().item() / b.abs().max().item()
+        assert rel < 1e-5, (f, rel)
+
+
+def test_band_backward_deterministic_and_symmetric(lib, cuda):
+    """Two band backwards on the same inputs are bit-identical, and the band A
+    factors are exactly symmetric (the upper triangle is mirrored)."""
+    outs, din, so, _ = _band_backward(lib, cuda, 1100, _lib.CONV_STATS_BAND, reps=2)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for f in (1, 2):
+        F = outs[0][1][so[f]:so[f] + din[f] * din[f]].reshape(din[f], din[f])
+        assert torch.equal(F, F.t()), f
+
+
 def test_kfac_inverse_matches_numpy(lib, cuda):
     A, C3 = 4, 32
     din = (ctypes.c_int64 * 6)()
