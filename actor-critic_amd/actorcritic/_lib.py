@@ -78,6 +78,10 @@ _SIGS = {
                                   ctypes.POINTER(RolloutIO), c_vp]),
     'acmi_categorical': (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     'acmi_returns': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    'acmi_gae': (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_float, c_vp, c_vp, c_vp]),
+    'acmi_adv_moments_ws_doubles': (c_i64, [c_i64]),
+    'acmi_adv_moments': (c_int, [c_vp, c_i64, c_vp, c_vp, c_vp]),
+    'acmi_adv_normalize': (c_int, [c_vp, c_i64, c_vp, ctypes.c_double, ctypes.c_double, c_vp]),
     'acmi_a2c_loss_ws_floats': (c_i64, [c_int]),
     'acmi_a2c_loss': (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_float, c_float, c_float,
                               c_vp, c_int, c_vp, c_vp, c_vp]),

@@ -7,6 +7,14 @@ stop-gradient advantage (:128-130), no advantage normalisation, policy loss
 ``mean((target-V)^2/2)`` (:151-154) — evaluated by libacmi (acmi_returns,
 acmi_a2c_loss).  The py_func discount-matrix closures become one reverse scan per
 env whose gamma tables are the exact float32 values the closures produce.
+
+Two options go beyond the reference (BASELINE.json's north_star names them; both
+off by default, so the defaults are the reference's objective): ``gae_lambda``
+(GAE(lambda) targets/advantages, acmi_gae; lambda = 1 is the n-step target in
+exact arithmetic) and ``normalize_advantages`` (batch-normalised advantages for
+the policy loss, acmi_adv_moments / acmi_adv_normalize; under data parallelism
+the moments are summed over ranks, so every rank normalises with the global
+batch's mean and std).
 """
 
 from abc import ABCMeta, abstractmethod
@@ -89,12 +97,36 @@ class _Targets(Node):
         rewards = _device(ctx.eval(model.rewards_placeholder), torch.float32, eng.device).reshape(N, T)
         terminals = _device_bool_u8(ctx.eval(model.terminals_placeholder), eng.device).reshape(N, T)
         st = eng.update_state(N * T)
-        gp, bp = obj._tables(T, eng.device)
-        _lib.call('acmi_returns', _lib.ptr(rewards), _lib.ptr(terminals), _lib.ptr(fwd.flat_value),
-                  _lib.ptr(boot.flat_value), N, T, _lib.ptr(gp), _lib.ptr(bp), _lib.ptr(st.targets),
-                  _lib.ptr(st.adv), eng.stream())
+        if obj._gae_lambda is None:
+            gp, bp = obj._tables(T, eng.device)
+            _lib.call('acmi_returns', _lib.ptr(rewards), _lib.ptr(terminals), _lib.ptr(fwd.flat_value),
+                      _lib.ptr(boot.flat_value), N, T, _lib.ptr(gp), _lib.ptr(bp), _lib.ptr(st.targets),
+                      _lib.ptr(st.adv), eng.stream())
+        else:
+            _lib.call('acmi_gae', _lib.ptr(rewards), _lib.ptr(terminals), _lib.ptr(fwd.flat_value),
+                      _lib.ptr(boot.flat_value), N, T, obj._gamma, obj._gae_lambda, _lib.ptr(st.targets),
+                      _lib.ptr(st.adv), eng.stream())
+        if obj._normalize:
+            _normalize_advantages(eng, st.adv, N * T, obj._adv_eps)
         st.fwd = fwd
         return st
+
+
+def _normalize_advantages(eng, adv, M, eps):
+    """adv <- (adv - mean) / (std + eps) over the global batch (all ranks)."""
+    ws = getattr(eng, '_adv_ws', None)
+    need = int(eng.lib.acmi_adv_moments_ws_doubles(M))
+    if ws is None or ws.numel() < need:
+        ws = torch.zeros(need, dtype=torch.float64, device=eng.device)
+        eng._adv_ws = ws
+        eng._adv_moments = torch.zeros(2, dtype=torch.float64, device=eng.device)
+    mom = eng._adv_moments
+    _lib.call('acmi_adv_moments', _lib.ptr(adv), M, _lib.ptr(ws), _lib.ptr(mom), eng.stream())
+    if eng.world_size > 1:
+        from actorcritic import parallel
+        parallel.allreduce_sum_(mom)
+    _lib.call('acmi_adv_normalize', _lib.ptr(adv), M, _lib.ptr(mom), float(M * eng.world_size), float(eps),
+              eng.stream())
 
 
 class _Loss(Node):
@@ -150,9 +182,18 @@ class _LossScalar(Node):
 class A2CObjective(ActorCriticObjective):
     """A2C/ACKTR objective (objectives.py:82-175)."""
 
-    def __init__(self, model, discount_factor=0.99, entropy_regularization_strength=0.01, name=None):
+    def __init__(self, model, discount_factor=0.99, entropy_regularization_strength=0.01, name=None,
+                 gae_lambda=None, normalize_advantages=False, advantage_epsilon=1e-8):
+        """The reference's arguments (objectives.py:100); ``gae_lambda`` (None: the
+        reference's n-step targets; a float in [0, 1]: GAE(lambda)) and
+        ``normalize_advantages`` are extensions beyond it (module docstring)."""
+        if gae_lambda is not None and not 0.0 <= float(gae_lambda) <= 1.0:
+            raise ValueError('gae_lambda must be in [0, 1] or None, got {}'.format(gae_lambda))
         self._model = model
         self._gamma = float(discount_factor)
+        self._gae_lambda = None if gae_lambda is None else float(gae_lambda)
+        self._normalize = bool(normalize_advantages)
+        self._adv_eps = float(advantage_epsilon)
         self._beta = float(entropy_regularization_strength)
         self._vcoef = 0.5
         self._name = name or 'A2CObjective'

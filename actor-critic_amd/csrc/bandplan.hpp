@@ -118,6 +118,8 @@ inline std::vector<char> band_needed(const BandGeom& g) {
 // fewest groups kept.  Groups are emitted in order of their first slab.
 inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 2) {
   const int ns = g.ns;
+  // ACMI_BAND_CAP: sub-tiles per group (default 16 = two per wave)
+  static const int cap = std::max(1, std::min(16, getenv("ACMI_BAND_CAP") ? atoi(getenv("ACMI_BAND_CAP")) : 16));
   const std::vector<char> need0 = band_needed(g);
   bool found = false;
   for (int rs = 0; rs < restarts; ++rs) {
@@ -188,7 +190,7 @@ inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 2) 
         if (deg[s0] == 0 || tried++ == kSeeds) break;
         int cs[6];
         const int tot = grow(s0, cs);
-        const int key = std::min(16, tot);
+        const int key = std::min(cap, tot);
         if (key > best_key || (key == best_key && tot < best_tot)) {
           best_key = key, best_tot = tot;
           for (int i = 0; i < 6; ++i) set[i] = cs[i];
@@ -205,7 +207,7 @@ inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 2) 
           if (nd(set[i], set[j]))
             tiles.push_back({i, j, deg[set[i]] + deg[set[j]], 64 * set[j] + 32 >= g.J});
       std::stable_sort(tiles.begin(), tiles.end(), [](const T& x, const T& y) { return x.key < y.key; });
-      if (tiles.size() > 16) tiles.resize(16);
+      if ((int)tiles.size() > cap) tiles.resize(cap);
       std::stable_sort(tiles.begin(), tiles.end(), [](const T& x, const T& y) { return !x.half && y.half; });
       BandGroup G;
       for (int i = 0; i < 6; ++i) G.base[i] = 64 * set[i];

@@ -77,6 +77,74 @@ __global__ void returns_kernel(const float* r, const uint8_t* d, const float* v,
 }
 
 // ---------------------------------------------------------------------------
+// GAE(lambda) targets (Schulman et al. 2016; an option beyond the reference,
+// whose targets are the n-step returns above): one thread per env, reverse scan
+//   delta_t = r_t + gamma V_{t+1} (1 - d_t) - V_t,   V_T = V_boot
+//   A_t = delta_t + gamma lambda (1 - d_t) A_{t+1},  target_t = A_t + V_t
+// with the operation order fixed (__f*_rn: no contraction) so the numpy float32
+// restatement (oracle.gae_f32) is bit-exact.  lambda = 1 equals the n-step
+// target in exact arithmetic.
+// ---------------------------------------------------------------------------
+__global__ void gae_kernel(const float* r, const uint8_t* d, const float* v, const float* vb, int N,
+                           int T, float gamma, float gl, float* tgt, float* adv) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float next_v = vb[n], last = 0.f;
+  for (int t = T - 1; t >= 0; --t) {
+    const long long i = (long long)n * T + t;
+    const bool live = d[i] == 0;
+    const float vi = v[i];
+    const float delta = __fsub_rn(__fadd_rn(r[i], live ? __fmul_rn(gamma, next_v) : 0.f), vi);
+    last = __fadd_rn(delta, live ? __fmul_rn(gl, last) : 0.f);
+    adv[i] = last;
+    tgt[i] = __fadd_rn(last, vi);
+    next_v = vi;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// advantage normalisation (an option beyond the reference): batch moments in
+// double, two fixed-order passes; normalise with the (all-reduced) moments
+// ---------------------------------------------------------------------------
+constexpr int MOM_BLOCKS = 256;
+
+__global__ void adv_moments_partial_kernel(const float* a, long long M, double* part) {
+  __shared__ double red[2][4];
+  double s = 0.0, q = 0.0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < M;
+       i += (long long)gridDim.x * blockDim.x) {
+    const double x = a[i];
+    s += x;
+    q += x * x;
+  }
+  s = wave_sum_d(s);
+  q = wave_sum_d(q);
+  if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = s, red[1][threadIdx.x >> 6] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    part[2 * blockIdx.x + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
+
+__global__ void adv_moments_final_kernel(const double* part, int nb, double* out) {
+  double s = 0.0, q = 0.0;  // one wave, lane-strided then butterfly
+  for (int i = threadIdx.x; i < nb; i += 64) s += part[2 * i], q += part[2 * i + 1];
+  s = wave_sum_d(s);
+  q = wave_sum_d(q);
+  if (threadIdx.x == 0) out[0] = s, out[1] = q;
+}
+
+__global__ void adv_normalize_kernel(float* a, long long M, const double* mom, double count, double eps) {
+  const double mean = mom[0] / count;
+  const double var = fmax(mom[1] / count - mean * mean, 0.0);
+  const double inv = 1.0 / (sqrt(var) + eps);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < M;
+       i += (long long)gridDim.x * blockDim.x)
+    a[i] = (float)(((double)a[i] - mean) * inv);
+}
+
+// ---------------------------------------------------------------------------
 // A2C loss + head gradients (objectives.py:123-154, :78)
 // ---------------------------------------------------------------------------
 constexpr int LOSS_BLOCK = 256;
@@ -332,6 +400,39 @@ int acmi_returns(const float* rewards, const uint8_t* terminals, const float* va
                      rewards, terminals, values, v_boot, N, T, gamma_pow, boot_pow, targets,
                      adv);
   ACMI_LAUNCH_CHECK("acmi_returns");
+  return ACMI_OK;
+}
+
+int acmi_gae(const float* rewards, const uint8_t* terminals, const float* values, const float* v_boot,
+             int N, int T, float gamma, float lambda, float* targets, float* adv, acmi_stream_t stream) {
+  ACMI_REQUIRE(rewards && terminals && values && v_boot && targets && adv && N >= 0 && T >= 1 &&
+                   lambda >= 0.f && lambda <= 1.f,
+               ACMI_ERR_ARG, "acmi_gae: bad arguments");
+  if (N == 0) return ACMI_OK;
+  hipLaunchKernelGGL(gae_kernel, dim3(cdiv(N, 64)), dim3(64), 0, (hipStream_t)stream, rewards, terminals,
+                     values, v_boot, N, T, gamma, gamma * lambda, targets, adv);
+  ACMI_LAUNCH_CHECK("acmi_gae");
+  return ACMI_OK;
+}
+
+int64_t acmi_adv_moments_ws_doubles(int64_t M) { (void)M; return 2LL * MOM_BLOCKS; }
+
+int acmi_adv_moments(const float* adv, int64_t M, double* ws, double* moments, acmi_stream_t stream) {
+  ACMI_REQUIRE(adv && ws && moments && M >= 1, ACMI_ERR_ARG, "acmi_adv_moments: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(adv_moments_partial_kernel, dim3(MOM_BLOCKS), dim3(256), 0, s, adv, (long long)M, ws);
+  hipLaunchKernelGGL(adv_moments_final_kernel, dim3(1), dim3(64), 0, s, ws, MOM_BLOCKS, moments);
+  ACMI_LAUNCH_CHECK("acmi_adv_moments");
+  return ACMI_OK;
+}
+
+int acmi_adv_normalize(float* adv, int64_t M, const double* moments, double count, double eps,
+                       acmi_stream_t stream) {
+  ACMI_REQUIRE(adv && moments && M >= 1 && count >= 1.0 && eps >= 0.0, ACMI_ERR_ARG,
+               "acmi_adv_normalize: bad arguments");
+  hipLaunchKernelGGL(adv_normalize_kernel, dim3(std::min<long long>(cdiv(M, 256), 1024)), dim3(256), 0,
+                     (hipStream_t)stream, adv, (long long)M, moments, count, eps);
+  ACMI_LAUNCH_CHECK("acmi_adv_normalize");
   return ACMI_OK;
 }
 

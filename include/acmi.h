@@ -179,6 +179,29 @@ int acmi_returns(const float* rewards, const uint8_t* terminals,
                  const float* gamma_pow, const float* boot_pow, float* targets,
                  float* adv, acmi_stream_t stream);
 
+/* GAE(lambda) targets and advantages -- an option BEYOND the reference (whose
+ * A2CObjective uses the n-step targets of acmi_returns, objectives.py:123-130;
+ * BASELINE.json north_star names the GAE scan).  Batch-major [N][T], v_boot[N]
+ * = V(s_T).  delta_t = r_t + gamma*V_{t+1}*(1-d_t) - V_t (V_T = v_boot),
+ * A_t = delta_t + gamma*lambda*(1-d_t)*A_{t+1}, target_t = A_t + V_t; float32,
+ * no contraction, in exactly that order.  lambda = 1 gives the n-step targets
+ * in exact arithmetic.  0 <= lambda <= 1. */
+int acmi_gae(const float* rewards, const uint8_t* terminals, const float* values,
+             const float* v_boot, int N, int T, float gamma, float lambda,
+             float* targets, float* adv, acmi_stream_t stream);
+
+/* Advantage normalisation (an option beyond the reference, which has none,
+ * objectives.py:128-130): moments[0..1] = (sum, sum of squares) of adv[0..M)
+ * in double, fixed order (ws: acmi_adv_moments_ws_doubles(M) doubles).  A
+ * data-parallel caller sums the moments over ranks, then
+ * acmi_adv_normalize: adv = (adv - mean) / (std + eps), mean/std (population)
+ * from moments over `count` rows (the global batch). */
+int64_t acmi_adv_moments_ws_doubles(int64_t M);
+int acmi_adv_moments(const float* adv, int64_t M, double* ws, double* moments,
+                     acmi_stream_t stream);
+int acmi_adv_normalize(float* adv, int64_t M, const double* moments, double count,
+                       double eps, acmi_stream_t stream);
+
 /* ------------------------------------------------------------------------
  * A2C losses and their gradient w.r.t. the head outputs.  Replaces
  * objectives.py:132-154 and the head part of tf.gradients of

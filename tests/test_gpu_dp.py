@@ -37,8 +37,10 @@ def _free_port():
     return p
 
 
-def _iteration(n_envs, rank):
-    """One bench-shaped ACKTR iteration at gs = 40 (steady state, inverse step)."""
+def _iteration(n_envs, rank, gae=None, norm=False):
+    """One bench-shaped ACKTR iteration at gs = 40 (steady state, inverse step);
+    gae / norm: the objective options beyond the reference (GAE(lambda), globally
+    normalised advantages)."""
     from actorcritic import session as sess
     from actorcritic.agents import MultiEnvAgent
     from actorcritic.envs.atari.model import AtariModel
@@ -52,7 +54,8 @@ def _iteration(n_envs, rank):
     env = MultiEnv(SyntheticAtariEnvs(n_envs, num_actions=4, seed=1234, env_offset=rank * n_envs, device=dev))
     model = AtariModel(env.observation_space, env.action_space, 32, random_seed=7, device=dev)
     agent = MultiEnvAgent(env, model, T)
-    obj = A2CObjective(model, discount_factor=0.99, entropy_regularization_strength=0.01)
+    obj = A2CObjective(model, discount_factor=0.99, entropy_regularization_strength=0.01, gae_lambda=gae,
+                       normalize_advantages=norm)
     gs = sess.get_or_create_global_step()
     opt = create_optimizer(True, model, linear_decay(0.25, 0.025, gs, 1e7 / (N_TOTAL * T)))
     op = obj.optimize_shared(opt, baseline_loss_weight=0.5, global_step=gs)
@@ -61,17 +64,18 @@ def _iteration(n_envs, rank):
     with sess.Session(dev) as s:
         obs, act, rew, term, nxt, _ = agent.interact(s)
         rollout = [x.clone() for x in (obs, act, rew, term, nxt)]
-        out = s.run([obj.policy_loss, obj.baseline_loss, obj.mean_entropy, op], feed_dict={
+        out = s.run([obj.policy_loss, obj.baseline_loss, obj.mean_entropy, obj.advantage, op], feed_dict={
             model.observations_placeholder: obs, model.bootstrap_observations_placeholder: nxt,
             model.actions_placeholder: act, model.rewards_placeholder: rew, model.terminals_placeholder: term})
     torch.cuda.synchronize()
     assert opt.last_flags == (False, True, True)
     return dict(rollout=[x.cpu() for x in rollout], losses=torch.tensor(out[:3], dtype=torch.float64),
+                adv=torch.as_tensor(np.asarray(out[3])).reshape(-1).cpu(),
                 step=(model.params - before).cpu(), factors=opt.state['factors'].cpu(), inv=opt.state['inv'].cpu(),
                 params=model.params.cpu())
 
 
-def _worker(rank, port, out_dir):
+def _worker(rank, port, out_dir, gae=None, norm=False):
     import sys
     sys.path.insert(0, os.path.join(ROOT, 'actor-critic_amd'))
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
@@ -79,7 +83,7 @@ def _worker(rank, port, out_dir):
     from actorcritic import parallel
     world, r = parallel.init_from_env()
     assert (world, r) == (WORLD, rank)
-    res = _iteration(N_TOTAL // WORLD, rank)
+    res = _iteration(N_TOTAL // WORLD, rank, gae, norm)
     torch.save(res, os.path.join(out_dir, 'rank{}.pt'.format(rank)))
     parallel.barrier()
     parallel.destroy()
@@ -90,23 +94,30 @@ def _rel(a, b):
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
-def test_sharded_acktr_iteration_matches_full_batch(lib, cuda, tmp_path):
+@pytest.mark.parametrize('gae,norm', [(None, False), (0.95, True)])
+def test_sharded_acktr_iteration_matches_full_batch(lib, cuda, tmp_path, gae, norm):
+    """(None, False) is the reference objective; (0.95, True) adds GAE and the
+    advantage normalisation, whose batch moments are summed over the ranks: each
+    shard's advantages are its slice of the full batch's normalised advantages."""
     ctx = mp.get_context('spawn')
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, str(tmp_path))) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, str(tmp_path), gae, norm)) for r in range(WORLD)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(240)
         assert p.exitcode == 0, 'rank failed with exit code {}'.format(p.exitcode)
     shards = [torch.load(str(tmp_path / 'rank{}.pt'.format(r)), weights_only=True) for r in range(WORLD)]
-    full = _iteration(N_TOTAL, 0)
+    full = _iteration(N_TOTAL, 0, gae, norm)
 
     # rollout: every shard is its slice of the full batch, bit for bit
     n = N_TOTAL // WORLD
     for r, sh in enumerate(shards):
         for i, (a, b) in enumerate(zip(sh['rollout'], full['rollout'])):
             assert torch.equal(a, b[r * n:(r + 1) * n]), ('rollout tensor', i, 'rank', r)
+        # advantages (normalised with the global moments when norm)
+        m = n * T
+        np.testing.assert_allclose(sh['adv'].numpy(), full['adv'][r * m:(r + 1) * m].numpy(), rtol=0, atol=2e-5)
     # replicated state: bit-identical on every rank
     for key in ('params', 'factors', 'inv', 'step'):
         assert torch.equal(shards[0][key], shards[1][key]), key

@@ -55,6 +55,71 @@ def test_returns_kernel_matches_golden(lib, cuda):
         np.testing.assert_array_equal(adv.cpu().numpy(), (got - c['values']).astype(np.float32))
 
 
+@pytest.mark.parametrize('lam', [0.0, 0.95, 1.0])
+def test_gae_kernel_bit_exact_vs_oracle(lib, cuda, lam):
+    """acmi_gae (an option beyond the reference) is bit-exact with the float32
+    restatement: terminals at t = 0 and T-1, an all-terminal row, none."""
+    rng = np.random.default_rng(11)
+    N, T = 37, 20
+    r = rng.choice([-1.0, 0.0, 1.0], size=(N, T)).astype(np.float32)
+    te = rng.random((N, T)) < 0.08
+    te[0, 0] = te[1, T - 1] = True
+    te[2, :] = True
+    te[3, :] = False
+    v = rng.normal(0, 1, size=(N, T)).astype(np.float32)
+    vb = rng.normal(0, 1, size=N).astype(np.float32)
+    tg = torch.zeros(N, T, device=cuda)
+    adv = torch.zeros(N, T, device=cuda)
+    rd, ted, vd, vbd = dev(r), dev(te.astype(np.uint8)), dev(v), dev(vb)
+    _lib.call('acmi_gae', _lib.ptr(rd), _lib.ptr(ted), _lib.ptr(vd), _lib.ptr(vbd), N, T, 0.99, lam,
+              _lib.ptr(tg), _lib.ptr(adv), _lib.stream_handle())
+    t_ref, a_ref = oracle.gae_f32(r, te, v, vb, 0.99, lam)
+    np.testing.assert_array_equal(tg.cpu().numpy(), t_ref)
+    np.testing.assert_array_equal(adv.cpu().numpy(), a_ref)
+
+
+def test_advantage_normalization_matches_oracle(lib, cuda):
+    M = 10240 + 37
+    a = np.random.default_rng(5).normal(0.3, 2.5, size=M).astype(np.float32)
+    ad = dev(a)
+    ws = torch.zeros(int(lib.acmi_adv_moments_ws_doubles(M)), dtype=torch.float64, device=cuda)
+    mom = torch.zeros(2, dtype=torch.float64, device=cuda)
+    _lib.call('acmi_adv_moments', _lib.ptr(ad), M, _lib.ptr(ws), _lib.ptr(mom), _lib.stream_handle())
+    m = mom.cpu().numpy()
+    assert m[0] == pytest.approx(a.astype(np.float64).sum(), rel=1e-12)
+    assert m[1] == pytest.approx((a.astype(np.float64) ** 2).sum(), rel=1e-12)
+    _lib.call('acmi_adv_normalize', _lib.ptr(ad), M, _lib.ptr(mom), float(M), 1e-8, _lib.stream_handle())
+    ref = oracle.normalize_advantages(a)
+    np.testing.assert_allclose(ad.cpu().numpy(), ref, rtol=0, atol=2e-6)
+
+
+def test_gae_and_normalized_advantages_through_objective(lib, cuda):
+    """A2CObjective(gae_lambda=0.95, normalize_advantages=True): targets, advantages
+    and the losses match the float64 oracle of the same options."""
+    from actorcritic import session as sess
+    from actorcritic.objectives import A2CObjective
+    N, T = 4, 5
+    env, model, agent, obj, gs, opt, op, params = _build(N, T)
+    obj2 = A2CObjective(model, gae_lambda=0.95, normalize_advantages=True)
+    with sess.Session() as s:
+        data = agent.interact(s)
+        feed = _feed(model, data)
+        tg, adv, pl, bl = s.run([obj2.target_values, obj2.advantage, obj2.policy_loss, obj2.baseline_loss],
+                                feed_dict=feed)
+    obs, act, rew, term, nxt, _ = data
+    full = oracle.forward(params, obs.cpu().numpy().reshape(-1, 84, 84, 4), 4, 32)
+    vb = oracle.forward(params, nxt.cpu().numpy(), 4, 32)['value']
+    t_ref, a_ref = oracle.gae_f64(rew.cpu().numpy(), term.cpu().numpy(), full['value'].reshape(N, T), vb, 0.99, 0.95)
+    a_ref = oracle.normalize_advantages(a_ref)
+    scale = max(1.0, np.abs(t_ref).max())
+    assert np.abs(tg - t_ref).max() <= 1e-5 * scale
+    assert np.abs(adv - a_ref).max() <= 1e-4
+    ref = oracle.a2c_loss_and_head_grads(full['logits'], full['value'], act.cpu().numpy().reshape(-1),
+                                         t_ref.reshape(-1), adv=a_ref)
+    assert pl == pytest.approx(ref['policy_loss'], rel=1e-4, abs=1e-6)
+    assert bl == pytest.approx(ref['baseline_loss'], rel=1e-4)
+
+
 def test_stepper_matches_reference_wrapper_trace(lib, cuda):
     from actorcritic.envs.atari.wrappers import SyntheticAtariEnvs
     rec = json.load(open(os.path.join(GOLD, 'framestack_autoreset.json')))

@@ -122,3 +122,43 @@ def test_agent_layout_matches_reference(monkeypatch):
     assert json.loads(json.dumps(model.batches)) == gold['sample_batches']
     assert json.loads(json.dumps(first)) == gold['first']
     assert json.loads(json.dumps(second)) == gold['second']
+
+
+def test_gae_lambda1_reduces_to_reference_targets():
+    """GAE(lambda = 1) targets equal the reference's n-step targets (exact
+    arithmetic; float32 differs by rounding of the telescoping V terms): pins the
+    GAE restatement (an option beyond the reference) at lambda = 1."""
+    rng = np.random.default_rng(3)
+    for m, c in _returns_cases():
+        v = rng.normal(0, 1, size=(m['N'], m['T'])).astype(np.float32)
+        tg, adv = oracle.gae_f32(c['rewards'], c['terminals'], v, c['v_boot'], 0.99, 1.0)
+        ref = c['targets_f32']
+        scale = max(1.0, np.abs(ref).max(), np.abs(v).max())
+        assert np.abs(tg - ref).max() <= 4 * m['T'] * np.spacing(np.float32(scale)), m
+        assert np.array_equal(adv, (tg - v).astype(np.float32)) or np.abs(adv - (tg - v)).max() <= 2 * np.spacing(
+            np.float32(scale))
+
+
+@pytest.mark.parametrize('lam', [0.0, 0.5, 0.95])
+def test_gae_f32_matches_float64(lam):
+    rng = np.random.default_rng(7)
+    N, T = 6, 20
+    r = rng.choice([-1.0, 0.0, 1.0], size=(N, T)).astype(np.float32)
+    d = rng.random((N, T)) < 0.1
+    d[0, 0] = d[1, T - 1] = True
+    d[2, :] = True
+    v = rng.normal(0, 1, size=(N, T)).astype(np.float32)
+    vb = rng.normal(0, 1, size=N).astype(np.float32)
+    t32, a32 = oracle.gae_f32(r, d, v, vb, 0.99, lam)
+    t64, a64 = oracle.gae_f64(r, d, v, vb, 0.99, lam)
+    assert np.abs(a32 - a64).max() <= 1e-5 * max(1.0, np.abs(a64).max())
+    assert np.abs(t32 - t64).max() <= 1e-5 * max(1.0, np.abs(t64).max())
+    # lambda = 0: one-step TD error; an all-terminal row is r - V
+    if lam == 0.0:
+        assert np.allclose(a64[2], r[2] - v[2])
+
+
+def test_normalize_advantages_moments():
+    a = np.random.default_rng(1).normal(3.0, 2.0, size=1000)
+    n = oracle.normalize_advantages(a)
+    assert abs(n.mean()) < 1e-12 and abs(n.std() - 1.0) < 1e-6
