@@ -189,6 +189,7 @@ class NetEngine(object):
         self._updates = {}
         self._rollout_cache = None
         self._bad_rows = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._prep, self._prep_version = None, None
         self.sample_counter = 0
 
     # -- update plumbing -------------------------------------------------------
@@ -296,7 +297,16 @@ class NetEngine(object):
 
     # -- plumbing ------------------------------------------------------------
     def net(self):
-        return _lib.Net(self.A, self.C3, self.params.data_ptr())
+        """The C-ABI net: parameters + the conv tower's pre-split weights, re-prepared
+        (acmi_conv_prepare, stream-ordered) at the first use after a parameter update."""
+        if self._prep is None:
+            self._prep = torch.empty(int(self.lib.acmi_conv_prep_bytes(self.C3)), dtype=torch.uint8,
+                                     device=self.device)
+        net = _lib.Net(self.A, self.C3, self.params.data_ptr(), self._prep.data_ptr())
+        if self._prep_version != (self.version, self.params.data_ptr()):
+            _lib.call('acmi_conv_prepare', ctypes.byref(net), ctypes.c_void_p(self._prep.data_ptr()), self.stream())
+            self._prep_version = (self.version, self.params.data_ptr())
+        return net
 
     def activations(self, B, key='default'):
         k = (key, B)

@@ -26,7 +26,7 @@ class AcmiError(RuntimeError):
 
 
 class Net(ctypes.Structure):
-    _fields_ = [('num_actions', c_int), ('conv3_filters', c_int), ('params', c_vp)]
+    _fields_ = [('num_actions', c_int), ('conv3_filters', c_int), ('params', c_vp), ('conv_prep', c_vp)]
 
 
 class Acts(ctypes.Structure):
@@ -61,6 +61,8 @@ _SIGS = {
     'acmi_get_conv_stats_mode': (c_int, []),
     'acmi_band_info': (c_int, [c_int, c_int, c_i64, ctypes.POINTER(c_i64)]),
     'acmi_param_count': (c_i64, [c_int, c_int]),
+    'acmi_conv_prep_bytes': (c_i64, [c_int]),
+    'acmi_conv_prepare': (c_int, [ctypes.POINTER(Net), c_vp, c_vp]),
     'acmi_param_offsets': (c_int, [c_int, c_int, ctypes.POINTER(c_i64)]),
     'acmi_kfac_layout': (c_int, [c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),
                                  ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
@@ -146,7 +148,7 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.acmi_abi_version() != 1:
+        if lib.acmi_abi_version() != 2:
             raise ImportError('libacmi ABI mismatch')
         _lib = lib
     return _lib

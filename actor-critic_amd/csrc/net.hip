@@ -19,6 +19,7 @@
 #include "convt3.hpp"
 #include "convfwd3.hpp"
 #include "band.hpp"
+#include "tower.hpp"
 #include "stepper.hpp"
 
 namespace acmi {
@@ -325,6 +326,13 @@ static int convf_lds() {
   return v;
 }
 
+// conv1 -> conv2 -> conv3 as one fused kernel per image (tower.hpp, bf16x3
+// mode): ACMI_TOWER = 1 (default) or 0 (the per-layer kernels below)
+static int tower_on() {
+  static const int v = getenv("ACMI_TOWER") ? atoi(getenv("ACMI_TOWER")) : 1;
+  return v;
+}
+
 // split factor for fc4 at small batch (64 x 128 tiles over 512 columns)
 static void fc4_plan(int B, int K, int* nz, int* chunk) {
   static const int maxsp = getenv("ACMI_FC4_SPLIT") ? atoi(getenv("ACMI_FC4_SPLIT")) : 8;
@@ -343,10 +351,16 @@ template <int C3>
 static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
                         long long img_stride, int B, const acmi_acts_t* a,
                         int want_value, long long act_img_stride,
-                        hipStream_t s, const TailArgs* tail = nullptr) {
+                        hipStream_t s, const TailArgs* tail = nullptr, const void* prep = nullptr) {
   // act_img_stride: images between consecutive batch rows in the activation
   // buffers (1 = contiguous; T = rollout step t of an env-major buffer).
   const long long st = act_img_stride;
+  if (g_gemm_mode == ACMI_GEMM_X3 && tower_on() && (uintptr_t)obs % 16 == 0 && img_stride % 16 == 0) {
+    // the three convs fused per image (16-byte image loads)
+    prof_begin(ACMI_PROF_CONV1_FWD, s);
+    launch_tower<C3>(obs, img_stride, B, P, L.off, a->a1, a->a2, a->a3, st, prep, s);
+    prof_end(ACMI_PROF_CONV1_FWD, s);
+  } else {
   {  // conv1: [B,84,84,4]u8 -> [B,20,20,32]; the u8 patches stay bytes in LDS
     using Src = ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>;
     MatI<true> w{P + L.off[0], 32, 256, 32};
@@ -384,6 +398,7 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     else
       launch_mm<128, 64, 32, 2, 1, false, false, 16>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
   }
+  }  // per-layer convs
   // fc4: [B,49*C3] -> [B,512]
   const int K4 = 49 * C3;
   // rows are images; with an image stride the dense row stride is st*K4
@@ -1220,8 +1235,24 @@ static int forward_dispatch(const acmi_net_t* net, const uint8_t* obs, int64_t i
   if (B == 0) return ACMI_OK;
   hipStream_t s = (hipStream_t)stream;
   if (L.C3 == 32)
-    return forward_impl<32>(L, net->params, obs, img_stride, B, acts, want_value, act_stride, s, tail);
-  return forward_impl<64>(L, net->params, obs, img_stride, B, acts, want_value, act_stride, s, tail);
+    return forward_impl<32>(L, net->params, obs, img_stride, B, acts, want_value, act_stride, s, tail,
+                            net->conv_prep);
+  return forward_impl<64>(L, net->params, obs, img_stride, B, acts, want_value, act_stride, s, tail,
+                          net->conv_prep);
+}
+
+int64_t acmi_conv_prep_bytes(int C3) {
+  return C3 == 32 ? TowerPrep<32>::BYTES : C3 == 64 ? TowerPrep<64>::BYTES : -1;
+}
+
+int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
+  Layout L;
+  ACMI_REQUIRE(net && net->params && prep && make_layout(net->num_actions, net->conv3_filters, &L),
+               ACMI_ERR_ARG, "acmi_conv_prepare: bad arguments");
+  ACMI_REQUIRE((uintptr_t)prep % 16 == 0, ACMI_ERR_ARG, "acmi_conv_prepare: prep must be 16-byte aligned");
+  launch_tower_prep(net->params, L.off, L.C3, prep, (hipStream_t)stream);
+  ACMI_LAUNCH_CHECK("acmi_conv_prepare");
+  return ACMI_OK;
 }
 
 int acmi_forward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define ACMI_ABI_VERSION 1
+#define ACMI_ABI_VERSION 2
 
 enum {
   ACMI_OK = 0,
@@ -87,7 +87,18 @@ typedef struct acmi_net {
   int num_actions;     /* A  (Breakout 4, full Atari 18); 1 <= A <= 64    */
   int conv3_filters;   /* C3 (32 ACKTR, 64 A2C: a2c_acktr.py:51-53)       */
   const float* params; /* device, acmi_param_count() floats               */
+  const void* conv_prep; /* nullable: device, acmi_conv_prep_bytes(C3) bytes,
+                            filled by acmi_conv_prepare from THESE params (the
+                            caller re-prepares after every parameter change) */
 } acmi_net_t;
+
+/* The forward's conv tower (bf16x3 mode) reads its weights as pre-split
+ * bf16 MFMA fragments when net->conv_prep is set: acmi_conv_prepare writes
+ * them (stream-ordered, one small kernel) -- once per parameter version, not
+ * per rollout step.  With conv_prep == NULL the tower splits the weights
+ * itself (same results, bit for bit). */
+int64_t acmi_conv_prep_bytes(int conv3_filters);
+int acmi_conv_prepare(const acmi_net_t* net, void* conv_prep, acmi_stream_t stream);
 
 int64_t acmi_param_count(int num_actions, int conv3_filters);
 /* off[2*l] = W offset, off[2*l+1] = b offset of layer l (12 entries)       */

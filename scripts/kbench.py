@@ -82,6 +82,21 @@ def inverse(A=4, C3=32, reps=10):
     print('kfac inverse (all 12 damped inverses): {:.3f} ms'.format(ms))
 
 
+def forward(B=512, reps=50):
+    """rollout-batch forward (site 3 = the conv tower / conv1 kernel)"""
+    from actorcritic._engine import NetEngine
+    eng = NetEngine(4, 32)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, device='cuda')
+    acts = eng.activations(B)
+    _lib.call('acmi_prof_enable', 3, 256)
+    ms = timeit(lambda: eng.forward(obs.data_ptr(), B, acts.struct), reps=reps)
+    tot, cnt = ctypes.c_double(), ctypes.c_int()
+    _lib.call('acmi_prof_collect', ctypes.byref(tot), ctypes.byref(cnt))
+    _lib.call('acmi_prof_enable', 0, 0)
+    print('forward B={}: {:.1f} us; site 3 kernel avg {:.1f} us over {}'.format(
+        B, 1e3 * ms, 1e3 * tot.value / max(1, cnt.value), cnt.value))
+
+
 def band_scaling(sizes=(1024, 2048, 4096, 10240)):
     """conv2 band kernel time vs images: against its MFMA-bound time (sum over
     groups of the busiest SIMD's sub-tiles x 4 x 6 MFMAs of 32 cycles per 16
@@ -99,6 +114,8 @@ if __name__ == '__main__':
     what = sys.argv[1]
     if what == 'band':
         band_scaling()
+    elif what == 'forward':
+        forward(int(sys.argv[2]) if len(sys.argv) > 2 else 512)
     if what == 'inverse':
         inverse()
     elif what == 'gemm':

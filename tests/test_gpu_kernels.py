@@ -369,3 +369,26 @@ def test_kfac_eigvals_match_numpy(lib, cuda):
         # north_star: eigenvalues within 1e-4 relative (each eigenvalue)
         assert np.all(np.abs(got[o:o + n] - ref) <= 1e-4 * np.abs(ref) + 1e-12 * np.abs(ref).max())
         o += n
+
+
+@pytest.mark.parametrize('C3', [32, 64])
+def test_conv_prep_forward_bit_identical(lib, cuda, C3):
+    """The conv tower with pre-split weights (acmi_conv_prepare) gives the same
+    activations, bit for bit, as the tower splitting the weights itself."""
+    A, B = 4, 37
+    params = rand_params(A, C3, cuda, seed=4)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=torch.Generator().manual_seed(6),
+                        dtype=torch.uint8).to(cuda)
+    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
+    outs = []
+    for use_prep in (False, True):
+        t, acts = alloc_acts(B, A, C3, cuda)
+        net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr() if use_prep else None)
+        if use_prep:
+            _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), _lib.stream_handle())
+        _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+                  _lib.stream_handle())
+        torch.cuda.synchronize()
+        outs.append({k: v.cpu() for k, v in t.items()})
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
