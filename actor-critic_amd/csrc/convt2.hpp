@@ -1,0 +1,239 @@
+// conv2's input gradient (d1 = conv2^T d2 * relu'(a1)) on bf16x3 with the
+// weights split ONCE per parameter version, and the sampled-loss variant that
+// reduces d1 to the K-FAC G factor of conv1's output without storing it.
+//
+// gemm3_kernel / convt_x3_kernel run this product with every block splitting
+// the 128 x 256 weight matrix into h/m/l again (8000 blocks at the bench shape)
+// and two row tiles per wave: ~10 VALU instructions per MFMA, more issue time
+// than the matrix cores need (rocprofv3: SQ_INSTS_VALU 1.24e8 against 12.3 M
+// MFMAs, 43 % MFMA-busy at 424 us).  Here
+//   * the weights come pre-split from acmi_conv_prepare ([k16 step][phase]
+//     [part h,m,l][lane] x 16 B, the A fragments of v_mfma_f32_32x32x16_bf16),
+//     staged per k-step into LDS by a straight 16-byte copy (12 KB, read back
+//     lane-contiguous: conflict-free ds_read_b128);
+//   * a wave owns 32 super-pixel columns and ALL FOUR stride phases (rows
+//     (phase, ci)): the four phases of a super-pixel gather the same dY pixels
+//     (tap (a, b) of phase (py, px) is kernel position (py + 2a, px + 2b)), so
+//     one B fragment -- 8 channels of one dY pixel, two float4 loads from L2,
+//     one split -- feeds 4 x 6 MFMAs;
+//   * epilogue STORE: the ReLU'-masked d1 as float4 channel runs; epilogue
+//     GRAM: the masked tile goes through LDS ([ci][super-pixel], stride 36:
+//     conflict-free) and its Gram D D^T accumulates on the same bf16x3 MFMAs
+//     across the wave's tiles; blocks write part[block][33][32] for
+//     finalize_cov_kernel (the layout gcov_layer's partials use).
+// Arithmetic per output element is gemm3's (six bf16 MFMAs per 32x32x16, k in
+// the same order: tap-major, channel-minor), so d1 is f32-accurate.
+// Reference: tf.gradients of the conv2d at envs/atari/model.py:184-189
+// (objectives.py:78) and kfac's G factor of conv1's output (registration
+// envs/atari/model.py:227-231) -- the same sums.
+#pragma once
+
+#include "gemm.hpp"
+#include "symred3.hpp"
+
+namespace acmi {
+
+// conv2 geometry: a1 [20][20][32] -> d2 [9][9][64], 4x4 stride 2
+struct CT2 {
+  static constexpr int CIN = 32, COUT = 64, OH = 9, OW = 9, PW = 10, L = 100;
+  static constexpr int NKS = 16;                    // k16 steps: 4 taps x 64 channels
+  static constexpr int STEP_BYTES = 4 * 3 * 1024;   // 4 phases x 3 parts x 64 lanes x 16 B
+  static constexpr int BYTES = NKS * STEP_BYTES;    // 196,608 B of prepared weights
+  static constexpr int TILE = 128;                  // columns per block tile (4 waves x 32)
+};
+
+// prepared weights: fragment (ks, phase) lane l holds W[py+2a][px+2b][ci][co..co+7],
+// ci = l & 31, tap t = ks >> 2 = (a, b), co = 16 (ks & 3) + 8 (l >> 5)
+__global__ void convt2_prep_kernel(const float* w2, char* out) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;  // (ks, phase, lane)
+  if (g >= CT2::NKS * 4 * 64) return;
+  const int lane = g & 63, ph = (g >> 6) & 3, ks = g >> 8;
+  const int py = ph >> 1, px = ph & 1, t = ks >> 2, a = t >> 1, b = t & 1;
+  const int kh = py + 2 * a, kw = px + 2 * b;
+  const int ci = lane & 31, co = 16 * (ks & 3) + 8 * (lane >> 5);
+  const float* p = w2 + ((kh * 4 + kw) * CT2::CIN + ci) * CT2::COUT + co;
+  uint4 h, m, l;
+  split3(p[0], p[1], h.x, m.x, l.x);
+  split3(p[2], p[3], h.y, m.y, l.y);
+  split3(p[4], p[5], h.z, m.z, l.z);
+  split3(p[6], p[7], h.w, m.w, l.w);
+  uint4* d = reinterpret_cast<uint4*>(out + (long long)ks * CT2::STEP_BYTES + ph * 3 * 1024) + lane;
+  d[0] = h;
+  d[64] = m;
+  d[128] = l;
+}
+
+template <bool GRAM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* __restrict__ a1,
+                   float* __restrict__ d1, int B, float* __restrict__ gpart) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * CT2::STEP_BYTES];  // 24 KB ring
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int J = B * CT2::L;
+  const int ntiles = (J + CT2::TILE - 1) / CT2::TILE;
+  const int hl = lane >> 5;  // k half of the fragment; row offset 4 of the accumulator
+  const float* zero = zero_run();
+
+  f32x16 gacc;  // GRAM: this wave's D D^T over its tiles
+#pragma unroll
+  for (int r = 0; r < 16; ++r) gacc[r] = 0.f;
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int j = tile * CT2::TILE + 32 * wave + (lane & 31);
+    const bool jok = j < J;
+    const int jj = jok ? j : 0;
+    const int n = jj / CT2::L, sp = jj - n * CT2::L;
+    const int Y = sp / CT2::PW, X = sp - Y * CT2::PW;
+    const float* dimg = d2 + (long long)n * (CT2::OH * CT2::OW * CT2::COUT);
+    // lane's B fragment for k-step ks: dY pixel (Y - a, X - b), channels co..co+7.
+    // Out-of-image taps load the zero run, selected on the ADDRESS (no branch:
+    // a load under a branch makes the waitcnt pass drain vmcnt at the join)
+    auto bload = [&](int ks, float4 (&x)[2]) {
+      const int t = ks >> 2, a = t >> 1, b = t & 1;
+      const int oy = Y - a, ox = X - b;
+      const bool ok = jok & (oy >= 0) & (oy < CT2::OH) & (ox >= 0) & (ox < CT2::OW);
+      const int oyc = max(oy, 0), oxc = max(ox, 0);  // (in range whenever ok)
+      const float* p = dimg + (oyc * CT2::OW + oxc) * CT2::COUT + 16 * (ks & 3) + 8 * hl;
+      x[0] = *reinterpret_cast<const float4*>(ok ? p : zero);
+      x[1] = *reinterpret_cast<const float4*>(ok ? p + 4 : zero);
+    };
+    // A staging: 12 KB per k-step, three 16-byte runs per thread (named
+    // registers: an array captured by the lambdas below was put in scratch)
+    uint4 ra0, ra1, ra2;
+    auto afetch = [&](int ks) {
+      const uint4* src = reinterpret_cast<const uint4*>(prep + (long long)ks * CT2::STEP_BYTES) + tid;
+      ra0 = src[0];
+      ra1 = src[256];
+      ra2 = src[512];
+    };
+    auto acommit = [&](int buf) {
+      uint4* dst = reinterpret_cast<uint4*>(lds + buf * CT2::STEP_BYTES) + tid;
+      dst[0] = ra0;
+      dst[256] = ra1;
+      dst[512] = ra2;
+    };
+
+    f32x16 acc[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[p][r] = 0.f;
+
+    // two B register sets, alternating by k-step parity (named, never indexed at
+    // run time: a dynamically indexed register array lands in scratch)
+    float4 bx0[2], bx1[2];
+    auto step = [&](int ks, float4 (&cur)[2], float4 (&nxt)[2]) {
+      const int buf = ks & 1;
+      // the last step prefetches step NKS-1 again (harmless): no load under a
+      // run-time branch, whose join would make the waitcnt pass drain vmcnt
+      const int kn = min(ks + 1, CT2::NKS - 1);
+      afetch(kn);
+      bload(kn, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 b[3];
+      {
+        uint4 h, m, l;
+        split3(cur[0].x, cur[0].y, h.x, m.x, l.x);
+        split3(cur[0].z, cur[0].w, h.y, m.y, l.y);
+        split3(cur[1].x, cur[1].y, h.z, m.z, l.z);
+        split3(cur[1].z, cur[1].w, h.w, m.w, l.w);
+        b[0] = __builtin_bit_cast(bf16x8, h);
+        b[1] = __builtin_bit_cast(bf16x8, m);
+        b[2] = __builtin_bit_cast(bf16x8, l);
+      }
+      const char* As = lds + buf * CT2::STEP_BYTES + lane * 16;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        bf16x8 a[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          a[q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(As + (p * 3 + q) * 1024));
+        acc[p] = mfma_x3(a, b, acc[p]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      acommit(buf ^ 1);
+      __syncthreads();
+    };
+    afetch(0);
+    bload(0, bx0);
+    acommit(0);
+    __syncthreads();
+    // two steps per iteration, not unrolled further (a full unroll keeps every
+    // step's addresses live and spills)
+    for (int ks = 0; ks < CT2::NKS; ks += 2) {
+      step(ks, bx0, bx1);
+      step(ks + 1, bx1, bx0);
+    }
+
+    // epilogue: rows (phase p, ci) x this wave's 32 super-pixel columns
+    float* scr = reinterpret_cast<float*>(lds) + wave * 32 * 36;  // [32][36] per wave
+    if constexpr (!GRAM) {
+      // ReLU'-masked d1 through the LDS transpose: each store instruction writes
+      // 8 whole 128-byte pixel rows (gemm.hpp store_tile_lds, EpiConvT addressing)
+      store_tile_lds<4, 1>(EpiConvT<20, 20, 2, 32>{d1, a1}, reinterpret_cast<const f32x16(&)[4][1]>(acc), 0,
+                           tile * CT2::TILE + 32 * wave, lane, scr, 4 * CT2::CIN, J);
+    } else {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int py = p >> 1, px = p & 1;
+        const long long pix = ((long long)n * 20 + 2 * Y + py) * 20 + 2 * X + px;
+        // masked tile as [ci][super-pixel] (rows ci = (r & 3) + 8 (r >> 2) + 4 hl)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int ci = 8 * g + 4 * hl;
+          const float4 x = *reinterpret_cast<const float4*>(jok ? a1 + pix * CT2::CIN + ci : zero);
+          const int c = lane & 31;
+          scr[(ci + 0) * 36 + c] = x.x > 0.f ? acc[p][4 * g + 0] : 0.f;
+          scr[(ci + 1) * 36 + c] = x.y > 0.f ? acc[p][4 * g + 1] : 0.f;
+          scr[(ci + 2) * 36 + c] = x.z > 0.f ? acc[p][4 * g + 2] : 0.f;
+          scr[(ci + 3) * 36 + c] = x.w > 0.f ? acc[p][4 * g + 3] : 0.f;
+        }
+        // G += D D^T, k = the 32 super-pixels (two k16 steps); the lane's fragment
+        // D[ci = lane & 31][k = 16 h + 8 hl .. +7] serves as A and as B.  (LDS ops
+        // of one wave execute in issue order: the reads see all lanes' stores.)
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float* rp = scr + (lane & 31) * 36 + 16 * h + 8 * hl;
+          const float4 x0 = *reinterpret_cast<const float4*>(rp);
+          const float4 x1 = *reinterpret_cast<const float4*>(rp + 4);
+          uint4 hh, mm, ll;
+          split3(x0.x, x0.y, hh.x, mm.x, ll.x);
+          split3(x0.z, x0.w, hh.y, mm.y, ll.y);
+          split3(x1.x, x1.y, hh.z, mm.z, ll.z);
+          split3(x1.z, x1.w, hh.w, mm.w, ll.w);
+          const bf16x8 f[3] = {__builtin_bit_cast(bf16x8, hh), __builtin_bit_cast(bf16x8, mm),
+                               __builtin_bit_cast(bf16x8, ll)};
+          gacc = mfma_x3(f, f, gacc);
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    __syncthreads();  // the ring / scratch is reused by the next tile
+  }
+
+  if constexpr (GRAM) {
+    // the 4 waves' Grams summed in wave order through LDS, then part[block][33][32]
+    float* red = reinterpret_cast<float*>(lds);  // [32][32]
+    for (int w = 0; w < 4; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int i = (r & 3) + 8 * (r >> 2) + 4 * hl, jc = lane & 31;
+          red[i * 32 + jc] = (w ? red[i * 32 + jc] : 0.f) + gacc[r];
+        }
+      }
+      __syncthreads();
+    }
+    float* out = gpart + (long long)blockIdx.x * 33 * 32;
+    for (int e = tid; e < 32 * 32; e += 256) out[e] = red[e];
+  }
+}
+
+// blocks of the Gram variant (per-block partials, finalize_cov_kernel sums them)
+inline int convt2_gram_blocks(int B) {
+  const int ntiles = (B * CT2::L + CT2::TILE - 1) / CT2::TILE;
+  return std::max(1, std::min(ntiles, 768));
+}
+
+}  // namespace acmi

@@ -20,6 +20,7 @@
 #include "convfwd3.hpp"
 #include "band.hpp"
 #include "tower.hpp"
+#include "convt2.hpp"
 #include "stepper.hpp"
 
 namespace acmi {
@@ -313,6 +314,13 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* part, int nz, c
 // here -- its f32 dY image (3-4 images x 81 px x 64 ch) leaves one block per CU.
 static int convt_lds() {
   static const int v = getenv("ACMI_CONVT") ? atoi(getenv("ACMI_CONVT")) : 1;
+  return v;
+}
+
+// conv2's input gradient on pre-split weights, four phases per wave
+// (convt2.hpp; needs net->conv_prep): ACMI_CONVT2 = 1 (default) or 0
+static int convt2_on() {
+  static const int v = getenv("ACMI_CONVT2") ? atoi(getenv("ACMI_CONVT2")) : 1;
   return v;
 }
 
@@ -936,7 +944,9 @@ static bool afactor_first() {
 template <int C3>
 static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a,
                     const acmi_bwd_t* bw, const float* dhead, int ldh,
-                    hipStream_t s) {
+                    hipStream_t s, const char* prep = nullptr, float* gram_part = nullptr,
+                    bool* gram_done = nullptr) {
+  if (gram_done) *gram_done = false;
   // heads -> d4 = (dhead W_h^T) * relu'(a4)
   if (L.A == 4 && ldh % 4 == 0 && (uintptr_t)(P + L.off[8]) % 16 == 0 && (uintptr_t)dhead % 16 == 0)
     hipLaunchKernelGGL(heads_dx4_kernel, dim3(cdiv((long long)B * 128, 256)), dim3(256), 0, s, dhead,
@@ -972,7 +982,19 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     RowsAsK<Src> opB{Src{bw->d2, B * Src::L}};
     EpiConvT<20, 20, 2, 32> epi{bw->d1, a->a1};
     prof_begin(ACMI_PROF_CONV2_DX, s);
-    if (g_gemm_mode == ACMI_GEMM_X3 && convt_lds() == 2)
+    const char* p2 = prep ? prep + TowerPrep<C3>::BYTES : nullptr;
+    if (p2 && g_gemm_mode == ACMI_GEMM_X3 && convt2_on()) {
+      // pre-split weights, four phases per wave (convt2.hpp); the sampled-loss
+      // chain reduces d1 to its Gram partials instead of storing it
+      if (gram_part) {
+        hipLaunchKernelGGL(convt2_kernel<true>, dim3(convt2_gram_blocks(B)), dim3(256), 0, s, p2, bw->d2,
+                           a->a1, nullptr, B, gram_part);
+        if (gram_done) *gram_done = true;
+      } else {
+hipLaunchKernelGGL(convt2_kernel<false>, dim3(cdiv(B * CT2::L, CT2::TILE)), dim3(256), 0, s, p2,
+                           bw->d2, a->a1, bw->d1, B, nullptr);
+      }
+    } else if (g_gemm_mode == ACMI_GEMM_X3 && convt_lds() == 2)
       launch_convt_x3<20, 20, 4, 4, 2, 32, 64, 128>(P + L.off[2], bw->d2, B, epi, s);
     else if (g_gemm_mode == ACMI_GEMM_X3 && convt_lds() == 3)
       launch_convt_x3<20, 20, 4, 4, 2, 32, 64, 64>(P + L.off[2], bw->d2, B, epi, s);
@@ -990,7 +1012,7 @@ template <int C3>
 static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
                          long long img_stride, int B, const acmi_acts_t* a,
                          const acmi_bwd_t* bw, float* grads, float* astat,
-                         float* ws, long long ws_cap, hipStream_t s) {
+                         float* ws, long long ws_cap, hipStream_t s, const char* prep) {
   const bool st = astat != nullptr;
   // conv1 A factor first, on the side stream (its int partials after the shared
   // split-K partials); falls back to this stream when no side stream exists
@@ -998,7 +1020,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // conv1's weight gradient fused into the A-factor pass (needs d1: after the dX chain)
   const bool fuse_c1 = st && g_gemm_mode == ACMI_GEMM_X3 && !afactor_first() && conv1_fused();
   auto dx = [&]() -> int {
-    const int r = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s);
+    const int r = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s, prep);
     if (r) return r;
     hipEvent_t* ev = dx_done_event();
     ACMI_REQUIRE(ev && hipEventRecord(*ev, s) == hipSuccess, ACMI_ERR_HIP,
@@ -1115,15 +1137,22 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
                              const acmi_acts_t* a, const acmi_bwd_t* bw,
                              uint32_t seed, uint32_t row0, uint32_t ctr,
                              float* gstat, float* ws, long long ws_cap,
-                             hipStream_t s) {
+                             hipStream_t s, const char* prep) {
   const int ldg = roundup4(L.A + 1) < 8 ? 8 : roundup4(L.A + 1);
   float* ghead = ws;  // [B][ldg]
   float* part = ws + (long long)B * ldg;
   const long long cap = ws_cap - (long long)B * ldg;
   hipLaunchKernelGGL(sampled_head_grad_kernel, dim3(cdiv(B, 128)), dim3(128), 0, s,
                      a->logits, a->ld_logits, B, L.A, seed, row0, ctr, ghead, ldg);
-  int rc = dx_chain<C3>(L, P, B, a, bw, ghead, ldg, s);
+  bool g1_done = false;
+  const bool g1_fits = (long long)convt2_gram_blocks(B) * 33 * 32 <= cap;
+  int rc = dx_chain<C3>(L, P, B, a, bw, ghead, ldg, s, prep, g1_fits ? part : nullptr, &g1_done);
   if (rc) return rc;
+  if (g1_done) {  // G of conv1's output from the conv2 dX kernel's per-block Gram partials
+    hipLaunchKernelGGL(finalize_cov_kernel, dim3(cdiv(32 * 32, 4)), dim3(256), 0, s, part,
+                       convt2_gram_blocks(B), 32, 32, gstat + L.stat_off[5 + 0], (int)(400LL * B));
+    ACMI_LAUNCH_CHECK("conv1 G factor");
+  }
   // heads: G_pi (A x A) from the first A columns, G_v = element (A, A)
   rc = gcov_layer(ghead, ldg, L.A + 1, B, L.A, part, cap, gstat + L.stat_off[5 + 4], s,
                   gstat + L.stat_off[5 + 5], L.A);
@@ -1134,7 +1163,7 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
   if (rc) return rc;
   rc = gcov_layer(bw->d2, 64, 64, 81LL * B, 64, part, cap, gstat + L.stat_off[5 + 1], s);
   if (rc) return rc;
-  rc = gcov_layer(bw->d1, 32, 32, 400LL * B, 32, part, cap, gstat + L.stat_off[5 + 0], s);
+  if (!g1_done) rc = gcov_layer(bw->d1, 32, 32, 400LL * B, 32, part, cap, gstat + L.stat_off[5 + 0], s);
   return rc;
 }
 
@@ -1242,7 +1271,8 @@ static int forward_dispatch(const acmi_net_t* net, const uint8_t* obs, int64_t i
 }
 
 int64_t acmi_conv_prep_bytes(int C3) {
-  return C3 == 32 ? TowerPrep<32>::BYTES : C3 == 64 ? TowerPrep<64>::BYTES : -1;
+  // the tower's conv weights, then conv2's input-gradient weights (convt2.hpp)
+  return C3 == 32 ? TowerPrep<32>::BYTES + CT2::BYTES : C3 == 64 ? TowerPrep<64>::BYTES + CT2::BYTES : -1;
 }
 
 int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
@@ -1251,6 +1281,9 @@ int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
                ACMI_ERR_ARG, "acmi_conv_prepare: bad arguments");
   ACMI_REQUIRE((uintptr_t)prep % 16 == 0, ACMI_ERR_ARG, "acmi_conv_prepare: prep must be 16-byte aligned");
   launch_tower_prep(net->params, L.off, L.C3, prep, (hipStream_t)stream);
+  const long long o2 = L.C3 == 32 ? TowerPrep<32>::BYTES : TowerPrep<64>::BYTES;
+  hipLaunchKernelGGL(convt2_prep_kernel, dim3(CT2::NKS * 4 * 64 / 256), dim3(256), 0, (hipStream_t)stream,
+                     net->params + L.off[2], static_cast<char*>(prep) + o2);
   ACMI_LAUNCH_CHECK("acmi_conv_prepare");
   return ACMI_OK;
 }
@@ -1314,9 +1347,9 @@ int acmi_backward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride,
   hipStream_t s = (hipStream_t)stream;
   if (L.C3 == 32)
     return backward_impl<32>(L, net->params, obs, img_stride, B, acts, bwd, grads, a_stats, ws,
-                             cap, s);
+                             cap, s, static_cast<const char*>(net->conv_prep));
   return backward_impl<64>(L, net->params, obs, img_stride, B, acts, bwd, grads, a_stats, ws,
-                           cap, s);
+                           cap, s, static_cast<const char*>(net->conv_prep));
 }
 
 int acmi_stream_wait_backward_dx(acmi_stream_t stream) {
@@ -1338,9 +1371,9 @@ int acmi_kfac_output_stats(const acmi_net_t* net, int B, const acmi_acts_t* acts
   hipStream_t s = (hipStream_t)stream;
   if (L.C3 == 32)
     return output_stats_impl<32>(L, net->params, B, acts, bwd, seed, row_offset, counter,
-                                 g_stats, ws, cap, s);
+                                 g_stats, ws, cap, s, static_cast<const char*>(net->conv_prep));
   return output_stats_impl<64>(L, net->params, B, acts, bwd, seed, row_offset, counter, g_stats,
-                               ws, cap, s);
+                               ws, cap, s, static_cast<const char*>(net->conv_prep));
 }
 
 int acmi_prof_enable(int site, int capacity) {

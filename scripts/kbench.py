@@ -120,6 +120,8 @@ if __name__ == '__main__':
         inverse()
     elif what == 'gemm':
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 4096)
+    elif what == 'c2':  # conv2 dX site (ACMI_PROF_CONV2_DX = 5)
+        backward(int(sys.argv[2]) if len(sys.argv) > 2 else 10240, False, 5, reps=10)
     elif what == 'backward1':  # a short run for PMC passes
         backward(int(sys.argv[2]) if len(sys.argv) > 2 else 10240, True, 2, reps=2)
     elif what == 'backward':

@@ -392,3 +392,62 @@ def test_conv_prep_forward_bit_identical(lib, cuda, C3):
         outs.append({k: v.cpu() for k, v in t.items()})
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.parametrize('B', [37, 1000])
+def test_convt2_matches_gemm3_path(lib, cuda, B):
+    """conv2's input gradient on pre-split weights (convt2.hpp, used when the net
+    carries conv_prep) is bit-identical to the gemm3 path (same k order, same six
+    bf16 MFMAs per 32x32x16), the parameter gradients and A factors of the whole
+    backward are unchanged, and the sampled-loss chain's conv1 G factor -- reduced
+    from the masked d1 tiles inside the kernel instead of stored and re-read -- is
+    within 2e-6 of float64 d1^T d1 / rows over the stored d1 (B = 1000: some blocks
+    of the Gram grid take two column tiles)."""
+    A, C3 = 4, 32
+    params = rand_params(A, C3, cuda, seed=12)
+    g = torch.Generator().manual_seed(13)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
+    t, acts = alloc_acts(B, A, C3, cuda)
+    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
+    nets = {False: _lib.Net(A, C3, params.data_ptr(), None), True: _lib.Net(A, C3, params.data_ptr(), prep.data_ptr())}
+    _lib.call('acmi_conv_prepare', ctypes.byref(nets[True]), _lib.ptr(prep), _lib.stream_handle())
+    _lib.call('acmi_forward', ctypes.byref(nets[False]), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+              _lib.stream_handle())
+    ldh = 8
+    dhead = torch.zeros(B, ldh)
+    dhead[:, :A + 1] = torch.randn(B, A + 1, generator=g) / B
+    dhead = dhead.to(cuda)
+    z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=cuda)
+    din = (ctypes.c_int64 * 6)()
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, din, None, so, ctypes.byref(tot))
+    ws = z(lib.acmi_backward_ws_floats(B, A, C3))
+    out = {}
+    for use_prep in (False, True):
+        d = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
+        bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
+        grads, astat = z(params.numel()), z(tot.value)
+        _lib.call('acmi_backward', ctypes.byref(nets[use_prep]), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
+                  ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), _lib.stream_handle())
+        torch.cuda.synchronize()
+        d1_loss = d[0].clone()
+        ds = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
+        bwd_s = _lib.Bwd(*[x.data_ptr() for x in ds], dhead.data_ptr(), ldh)
+        gstat = z(tot.value)
+        _lib.call('acmi_kfac_output_stats', ctypes.byref(nets[use_prep]), B, ctypes.byref(acts), ctypes.byref(bwd_s),
+                  7, 0, 3, _lib.ptr(gstat), _lib.ptr(ws), _lib.stream_handle())
+        torch.cuda.synchronize()
+        out[use_prep] = (d1_loss.cpu(), grads.cpu(), astat.cpu(), gstat.cpu(), ds[0].cpu())
+    (d1a, ga, aa, sa, d1s), (d1b, gb, ab, sb, _) = out[False], out[True]
+    assert torch.equal(d1a, d1b)
+    assert torch.equal(ga, gb)
+    assert torch.equal(aa, ab)
+    # G factors: conv1's from the kernel's Gram, the rest unchanged
+    o0 = so[5]
+    ref = (d1s.double().reshape(-1, 32).t() @ d1s.double().reshape(-1, 32)) / (400 * B)
+    got = sb[o0:o0 + 32 * 32].double().reshape(32, 32)
+    rel = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert rel < 2e-6, rel
+    assert torch.equal(got, got.t())
+    assert torch.equal(sa[so[6]:], sb[so[6]:])
