@@ -229,7 +229,7 @@ class NetEngine(object):
                   ctypes.byref(bwd), seed, self.rank * fwd.M, counter, _lib.ptr(st.gstat), _lib.ptr(ws),
                   self.stream())
 
-    concurrent_stats = os.environ.get('ACMI_CONCURRENT_STATS', '1') != '0'
+    concurrent_stats = os.environ.get('ACMI_CONCURRENT_STATS', '0') != '0'
     # measured (ACKTR 512x20, one box): plain update 5.25 ms with the G chain started
     # next to the whole backward, 5.16 ms started after the backward's dX chain
     stats_after_dx = os.environ.get('ACMI_STATS_AFTER_DX', '1') != '0'
