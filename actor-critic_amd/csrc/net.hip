@@ -545,6 +545,53 @@ __global__ __launch_bounds__(256) void finalize_wgrad_kernel(WgradDesc d) {
   }
 }
 
+// The A factor of a split-K wgrad partial ((K+1)^2, symmetric): one block per
+// 32x32 tile of the upper triangle; each element sums its chunks in exactly
+// finalize_wgrad_kernel's order (chunk group g = c mod 8 in chunk order, then
+// the groups in order), is stored at (a, b) and, through an LDS transpose, at
+// (b, a) -- both halves written by coalesced rows (the element-per-thread
+// mirror store of finalize_wgrad_kernel is a 4-byte scatter with stride K+1).
+__global__ __launch_bounds__(256) void finalize_afactor_kernel(WgradDesc d, int ntile) {
+  __shared__ float tr[32][33];
+  const int K = d.I, K1 = K + 1;
+  // upper-triangle tile (ta <= tb) of linear index blockIdx.x
+  int t = blockIdx.x, ta = 0;
+  while (t >= ntile - ta) t -= ntile - ta, ++ta;
+  const int tb = ta + t;
+  const long long cs = (long long)(d.I + 1) * d.J;
+  const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;
+  const float inv = 1.0f / (float)d.rows;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int r = r0 + 8 * it;
+    const int a = 32 * ta + r, b = 32 * tb + c;
+    float v = 0.f;
+    if (a < K1 && b < K1 && a <= b) {
+      if (a == K) {
+        v = 1.0f;  // rows / rows
+      } else {
+        const float* p = b < K ? d.part + (long long)a * d.J + b : d.part + (long long)d.I * d.J + a;
+        float s = 0.f;
+        for (int g = 0; g < kFinGroups; ++g) {
+          float sg = 0.f;
+          for (int ch = g; ch < d.nchunk; ch += kFinGroups) sg += p[(long long)ch * cs];
+          s += sg;
+        }
+        v = s * inv;
+      }
+      d.astat[(long long)a * K1 + b] = v;
+    }
+    tr[r][c] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {  // (b, a) for a < b: row b of the output reads column b of the tile
+    const int r = r0 + 8 * it;     // row offset inside tile tb
+    const int b = 32 * tb + r, a = 32 * ta + c;
+    if (a < K1 && b < K1 && a < b) d.astat[(long long)b * K1 + a] = tr[c][r];
+  }
+}
+
 // G factor: part [nchunk][I+1][J] (I == J == n, no colsum row used); one
 // wave per output element sums the chunks in a fixed (lane-strided, then
 // butterfly) order, so the result is deterministic.
@@ -811,9 +858,17 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
     launch_conv1_wgrad_u8(src, dy, (int)rows, nc, ch, epi, s);
   }
   prof_end(site, s);
-  WgradDesc d{part, nc, I, J, kp, cout, gradA, nsplit, gradB, astat, (int)rows, wscale};
-  const long long total = (long long)(K + 1) * cout + (astat ? (long long)(K + 1) * (K + 1) : 0);
+  // few chunks (fc4): the A factor on upper-triangle tiles mirrored through LDS;
+  // many (the heads' 80): one output per 8 threads, chunk groups in parallel
+  const bool tiles = astat && nc <= kFinGroups;
+  WgradDesc d{part, nc, I, J, kp, cout, gradA, nsplit, gradB, tiles ? nullptr : astat, (int)rows, wscale};
+  const long long total = (long long)(K + 1) * cout + (d.astat ? (long long)(K + 1) * (K + 1) : 0);
   hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(total, 32)), dim3(256), 0, s, d);
+  if (tiles) {
+    d.astat = astat;
+    const int nt = cdiv(K + 1, 32);
+    hipLaunchKernelGGL(finalize_afactor_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, s, d, nt);
+  }
   ACMI_LAUNCH_CHECK("wgrad_layer");
   return ACMI_OK;
 }
