@@ -55,6 +55,8 @@ class RolloutIO(ctypes.Structure):
 _SIGS = {
     'acmi_last_error': (ctypes.c_char_p, []),
     'acmi_abi_version': (c_int, []),
+    'acmi_set_forward_mode': (c_int, [c_int]),
+    'acmi_get_forward_mode': (c_int, []),
     'acmi_set_gemm_mode': (c_int, [c_int]),
     'acmi_get_gemm_mode': (c_int, []),
     'acmi_set_conv_stats_mode': (c_int, [c_int]),
@@ -121,6 +123,8 @@ _SIGS = {
 
 GEMM_F32 = 0  # acmi_set_gemm_mode: v_mfma_f32_32x32x2_f32
 GEMM_X3 = 1   # bf16x3 split operands on the bf16 matrix cores (default)
+FWD_F32 = 0   # acmi_set_forward_mode: the conv tower f32-accurate (default)
+FWD_BF16 = 1  # one bf16 MFMA per product (BASELINE configs[4] "bf16 forward")
 
 CONV_STATS_PATCHES = 0  # acmi_set_conv_stats_mode: im2col patch rows
 CONV_STATS_BAND = 1     # pixel-pair band reduction (default)

@@ -334,6 +334,12 @@ static int convf_lds() {
   return v;
 }
 
+// forward precision (acmi_set_forward_mode): the tower's arithmetic
+int g_forward_mode = [] {
+  const char* e = getenv("ACMI_FORWARD");
+  return (e && e[0] == 'b') ? ACMI_FWD_BF16 : ACMI_FWD_F32;
+}();
+
 // conv1 -> conv2 -> conv3 as one fused kernel per image (tower.hpp, bf16x3
 // mode): ACMI_TOWER = 1 (default) or 0 (the per-layer kernels below)
 static int tower_on() {
@@ -366,7 +372,8 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   if (g_gemm_mode == ACMI_GEMM_X3 && tower_on() && (uintptr_t)obs % 16 == 0 && img_stride % 16 == 0) {
     // the three convs fused per image (16-byte image loads)
     prof_begin(ACMI_PROF_CONV1_FWD, s);
-    launch_tower<C3>(obs, img_stride, B, P, L.off, a->a1, a->a2, a->a3, st, prep, s);
+    launch_tower<C3>(obs, img_stride, B, P, L.off, a->a1, a->a2, a->a3, st, prep, s,
+                     g_forward_mode == ACMI_FWD_BF16);
     prof_end(ACMI_PROF_CONV1_FWD, s);
   } else {
   {  // conv1: [B,84,84,4]u8 -> [B,20,20,32]; the u8 patches stay bytes in LDS
@@ -1238,6 +1245,14 @@ int acmi_set_gemm_mode(int mode) {
   return ACMI_OK;
 }
 int acmi_get_gemm_mode(void) { return g_gemm_mode; }
+
+int acmi_set_forward_mode(int mode) {
+  ACMI_REQUIRE(mode == ACMI_FWD_F32 || mode == ACMI_FWD_BF16, ACMI_ERR_ARG, "acmi_set_forward_mode: bad mode %d",
+               mode);
+  g_forward_mode = mode;
+  return ACMI_OK;
+}
+int acmi_get_forward_mode(void) { return g_forward_mode; }
 
 int acmi_set_conv_stats_mode(int mode) {
   ACMI_REQUIRE(mode == ACMI_CONV_STATS_PATCHES || mode == ACMI_CONV_STATS_BAND, ACMI_ERR_ARG,

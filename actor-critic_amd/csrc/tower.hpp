@@ -41,6 +41,15 @@ __device__ __forceinline__ int tow_pos(int p, int x, int ch) {
   return p * C * 4 + 16 * (ch ^ ((x / S) & (C / 4 - 1)));
 }
 
+__device__ __forceinline__ bf16x8 tow_bf16x8(const float4& x0, const float4& x1) {
+  uint4 h;
+  h.x = pk_bf16(x0.x, x0.y);
+  h.y = pk_bf16(x0.z, x0.w);
+  h.z = pk_bf16(x1.x, x1.y);
+  h.w = pk_bf16(x1.z, x1.w);
+  return __builtin_bit_cast(bf16x8, h);
+}
+
 __device__ __forceinline__ void tow_split8(const float4& x0, const float4& x1, bf16x8 (&o)[3]) {
   uint4 h, m, l;
   split3(x0.x, x0.y, h.x, m.x, l.x);
@@ -118,15 +127,20 @@ __device__ __forceinline__ int tow_row(int r, int lane) { return (r & 3) + 8 * (
 
 // a layer's B fragments, two k-steps in flight (slot = k-step parity, always a
 // compile-time index): prepared bf16 parts (PREP) or f32 weights split here
-template <bool PREP, int N>
+template <bool PREP, int N, bool BF16 = false>
 struct TowB {
   const float* w;
   const char* prep;
   uint4 q[2][3];
   float4 f[2][2];
   __device__ __forceinline__ void fetch(int s, int ct, int lane, int slot) {
-    if constexpr (PREP) tow_bprep(prep, s, N / 32, ct, lane, q[slot]);
-    else tow_bload<N>(w, s, 32 * ct, lane, f[slot]);
+    if constexpr (PREP && BF16) {  // the h part only
+      q[slot][0] = reinterpret_cast<const uint4*>(prep + ((long long)(s * (N / 32) + ct) * 3) * 1024)[lane];
+    } else if constexpr (PREP) {
+      tow_bprep(prep, s, N / 32, ct, lane, q[slot]);
+    } else {
+      tow_bload<N>(w, s, 32 * ct, lane, f[slot]);
+    }
   }
   __device__ __forceinline__ void get(int slot, bf16x8 (&b)[3]) {
     if constexpr (PREP) {
@@ -138,7 +152,9 @@ struct TowB {
   }
 };
 
-template <int C3, bool PREP>
+// BF16 (acmi_set_forward_mode ACMI_FWD_BF16): one bf16 MFMA per product -- the
+// weights' h part and conv2/conv3 inputs rounded to bf16 (u8 pixels exact).
+template <int C3, bool PREP, bool BF16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, const float* b1,
                   const float* w2, const float* b2, const float* w3, const float* b3, float* a1g,
@@ -177,7 +193,7 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
-    TowB<PREP, 32> bw{w1, prep + P::O1};
+    TowB<PREP, 32, BF16> bw{w1, prep + P::O1};
     bw.fetch(0, 0, lane, 0);
     __syncthreads();
 #pragma unroll
@@ -190,8 +206,10 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
       for (int u = 0; u < 4; ++u) {
         if (u >= nt) break;
         const bf16x8 a = u8x8_to_bf16(*reinterpret_cast<const uint2*>(imgL + abase[u] + koff));
-        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[2], acc[u], 0, 0, 0);
-        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[1], acc[u], 0, 0, 0);
+        if constexpr (!BF16) {
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[2], acc[u], 0, 0, 0);
+          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[1], acc[u], 0, 0, 0);
+        }
         acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[0], acc[u], 0, 0, 0);
       }
     }
@@ -228,7 +246,7 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
     f32x16 accF, accH;
 #pragma unroll
     for (int r = 0; r < 16; ++r) accF[r] = accH[r] = 0.f;
-    TowB<PREP, 64> bw{w2, prep + P::O2};
+    TowB<PREP, 64, BF16> bw{w2, prep + P::O2};
     bw.fetch(0, ct, lane, 0);
 #pragma unroll
     for (int s = 0; s < 32; ++s) {
@@ -244,6 +262,12 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
         const float4 x0 = *reinterpret_cast<const float4*>(a1L + tow_pos<32, 2>(p, x, ch));
         const float4 x1 = *reinterpret_cast<const float4*>(a1L + tow_pos<32, 2>(p, x, ch + 1));
         bf16x8 a[3];
+        if constexpr (BF16) {
+          a[0] = tow_bf16x8(x0, x1);
+          if (u == 0) accF = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], accF, 0, 0, 0);
+          else accH = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], accH, 0, 0, 0);
+          continue;
+        }
         tow_split8(x0, x1, a);
         if (u == 0) accF = mfma_x3(a, b, accF);
         else accH = mfma_x3(a, b, accH);
@@ -294,7 +318,7 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    TowB<PREP, C3> bw{w3, prep + P::O3};
+    TowB<PREP, C3, BF16> bw{w3, prep + P::O3};
     bw.fetch(s0, ct, lane, 0);
     for (int s = s0; s < s1; s += 2) {
 #pragma unroll
@@ -309,6 +333,10 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
         const float4 x0 = *reinterpret_cast<const float4*>(imgL + tow_pos<64, 1>(p, x, ch));
         const float4 x1 = *reinterpret_cast<const float4*>(imgL + tow_pos<64, 1>(p, x, ch + 1));
         bf16x8 a[3];
+        if constexpr (BF16) {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tow_bf16x8(x0, x1), b[0], acc, 0, 0, 0);
+          continue;
+        }
         tow_split8(x0, x1, a);
         acc = mfma_x3(a, b, acc);
       }
@@ -345,15 +373,16 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
 template <int C3>
 inline void launch_tower(const uint8_t* obs, long long img_stride, int B, const float* P,
                          const long long* off, float* a1, float* a2, float* a3, long long st,
-                         const void* prep, hipStream_t s) {
-  if (prep)
-    hipLaunchKernelGGL((tower_kernel<C3, true>), dim3(B), dim3(256), 0, s, obs, img_stride, P + off[0],
-                       P + off[1], P + off[2], P + off[3], P + off[4], P + off[5], a1, a2, a3, st,
-                       static_cast<const char*>(prep));
-  else
-    hipLaunchKernelGGL((tower_kernel<C3, false>), dim3(B), dim3(256), 0, s, obs, img_stride, P + off[0],
-                       P + off[1], P + off[2], P + off[3], P + off[4], P + off[5], a1, a2, a3, st,
-                       static_cast<const char*>(nullptr));
+                         const void* prep, hipStream_t s, bool bf16 = false) {
+#define ACMI_TOWER(PR, BF)                                                                            \
+  hipLaunchKernelGGL((tower_kernel<C3, PR, BF>), dim3(B), dim3(256), 0, s, obs, img_stride, P + off[0], \
+                     P + off[1], P + off[2], P + off[3], P + off[4], P + off[5], a1, a2, a3, st,       \
+                     static_cast<const char*>(prep))
+  if (prep && bf16) ACMI_TOWER(true, true);
+  else if (prep) ACMI_TOWER(true, false);
+  else if (bf16) ACMI_TOWER(false, true);
+  else ACMI_TOWER(false, false);
+#undef ACMI_TOWER
 }
 
 inline void launch_tower_prep(const float* P, const long long* off, int C3, void* prep, hipStream_t s) {

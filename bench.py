@@ -60,7 +60,10 @@ def parse():
     p.add_argument('--algo', choices=['acktr', 'a2c'], default='acktr')
     p.add_argument('--envs-per-gpu', type=int, default=512)
     p.add_argument('--nsteps', type=int, default=None, help='rollout length T (ACKTR 20, A2C 5)')
-    p.add_argument('--num-actions', type=int, default=4, help='Breakout: 4')
+    p.add_argument('--num-actions', type=int, default=4, help='Breakout: 4; full Atari action set: 18')
+    p.add_argument('--forward', choices=['f32', 'bf16'], default=None,
+                   help='conv tower precision (default: ACMI_FORWARD or f32; bf16: BASELINE configs[4] '
+                        '"bf16 forward / fp32 KFAC factors")')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-iters', type=int, default=3)
     p.add_argument('--quiet', action='store_true')
@@ -80,6 +83,9 @@ def main():
     from actorcritic.objectives import A2CObjective
 
     world, rank = parallel.init_from_env()
+    if args.forward is not None:
+        _lib.call('acmi_set_forward_mode', _lib.FWD_BF16 if args.forward == 'bf16' else _lib.FWD_F32)
+    args.forward = 'bf16' if _lib.load().acmi_get_forward_mode() == _lib.FWD_BF16 else 'f32'
     if world != args.gpus and rank == 0:
         print('warning: --gpus {} but WORLD_SIZE {}'.format(args.gpus, world), file=sys.stderr)
     dev = torch.device('cuda', torch.cuda.current_device())
@@ -215,10 +221,12 @@ def main():
             'metric': 'env-steps/sec (whole node) + ACKTR update ms, Breakout 84x84x4',
             'value': value, 'unit': 'env-steps/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': ms_per_step, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-            'dtype': 'fp32', 'data': 'synthetic (hashed 84x84 u8 frames, random-init orthogonal weights)',
-            'config': {'workload': 'Breakout {} {} envs/GPU x {} steps (BASELINE configs[3] shard)'.format(
-                args.algo.upper(), N, T), 'algo': args.algo, 'envs_per_gpu': N, 'num_steps': T,
-                'global_envs': N * world, 'num_actions': A, 'conv3_filters': C3,
+            'dtype': 'fp32' if args.forward == 'f32' else 'bf16 forward / fp32 update', 'data': 'synthetic (hashed 84x84 u8 frames, random-init orthogonal weights)',
+            'config': {'workload': ('Breakout {} {} envs/GPU x {} steps (BASELINE configs[3] shard)'.format(
+                args.algo.upper(), N, T) if args.forward == 'f32' else
+                'Atari {} {} envs/GPU x {} steps, {} actions, bf16 forward / fp32 K-FAC (BASELINE configs[4] '
+                'shard)'.format(args.algo.upper(), N, T, A)), 'algo': args.algo, 'envs_per_gpu': N, 'num_steps': T,
+                'global_envs': N * world, 'num_actions': A, 'conv3_filters': C3, 'forward': args.forward,
                 'parallelism': 'dp{}'.format(world)},
             'update_ms': mean(upd_ms), 'update_ms_inverse_iters': mean(upd_inv),
             'update_ms_plain_iters': mean(upd_plain), 'rollout_ms': mean(roll_ms),

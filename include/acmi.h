@@ -48,6 +48,20 @@ int acmi_abi_version(void);
 int acmi_set_gemm_mode(int mode);
 int acmi_get_gemm_mode(void);
 
+/* Precision of the forward's conv tower (rollout and update forward; BASELINE
+ * configs[4] "bf16 forward / fp32 K-FAC factors" -- an extension, the
+ * reference computes in fp32):
+ *   ACMI_FWD_F32   bf16x3 split operands, f32-accurate (default)
+ *   ACMI_FWD_BF16  one bf16 MFMA per product: weights and conv2/conv3 inputs
+ *                  rounded to bf16 (u8 pixels exact), f32 accumulation
+ * The backward, the K-FAC statistics and the optimizers stay f32-accurate; they
+ * read the activations the forward produced.  Initial mode from ACMI_FORWARD
+ * ("bf16" / "f32").  Not stream-ordered: set it between launches. */
+#define ACMI_FWD_F32 0
+#define ACMI_FWD_BF16 1
+int acmi_set_forward_mode(int mode);
+int acmi_get_forward_mode(void);
+
 /* How conv2 / conv3 form their weight gradient + A factor in ACMI_GEMM_X3 mode
  * (both fp32-accurate, same sums reassociated):
  *   ACMI_CONV_STATS_BAND    pixel-pair band reduction (default): each pair of

@@ -451,3 +451,42 @@ def test_convt2_matches_gemm3_path(lib, cuda, B):
     assert rel < 2e-6, rel
     assert torch.equal(got, got.t())
     assert torch.equal(sa[so[6]:], sb[so[6]:])
+
+
+@pytest.mark.parametrize('A,C3', [(4, 32), (18, 64)])
+def test_bf16_forward_mode(lib, cuda, A, C3):
+    """acmi_set_forward_mode(ACMI_FWD_BF16) (BASELINE configs[4] "bf16 forward"):
+    the conv tower with one bf16 MFMA per product stays within bf16 accuracy of the
+    float64 forward (max error <= 1e-2 of each tensor's range; measured ~2e-3), and
+    switching back restores the f32-accurate tower bit for bit."""
+    B = 29
+    params = rand_params(A, C3, cuda, seed=31)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=torch.Generator().manual_seed(32),
+                        dtype=torch.uint8).to(cuda)
+    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
+    net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr())
+    _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), _lib.stream_handle())
+    ref = torch_forward(params, obs.cpu(), A, C3)
+    names = ['a1', 'a2', 'a3', 'a4', 'logits', 'value']
+    outs = {}
+    prev = lib.acmi_get_forward_mode()
+    try:
+        for mode in (_lib.FWD_F32, _lib.FWD_BF16, _lib.FWD_F32):
+            _lib.call('acmi_set_forward_mode', mode)
+            t, acts = alloc_acts(B, A, C3, cuda)
+            _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+                      _lib.stream_handle())
+            torch.cuda.synchronize()
+            outs.setdefault(mode, []).append({k: v.cpu() for k, v in t.items()})
+    finally:
+        _lib.call('acmi_set_forward_mode', prev)
+    f32a, f32b = outs[_lib.FWD_F32]
+    for k in f32a:
+        assert torch.equal(f32a[k], f32b[k]), k
+    bf = outs[_lib.FWD_BF16][0]
+    for name, r in zip(names, ref):
+        got = bf[name].double().reshape(r.shape)
+        err = (got - r).abs().max().item() / max(1e-6, r.abs().max().item())
+        print(name, 'bf16 forward rel err %.2e' % err)
+        assert err < 1e-2, (name, err)
+        assert not torch.equal(bf[name], f32a[name]), name  # the mode really changed the arithmetic
