@@ -885,7 +885,8 @@ static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
                       float* part, long long part_cap, float* out,
                       hipStream_t s, float* out_v = nullptr, int v_index = -1) {
   int np, nc;
-  if (n <= 64) {  // narrow: streaming Gram kernel
+  if (n <= 32) {  // narrow: streaming Gram kernel (f32 MFMA; 64 wide runs faster on the split-K
+                  // bf16x3 GEMM below: conv2's G factor 82 + 25 -> 59 + 16 us)
     np = n <= 32 ? 32 : 64;
     long long ch;
     gram_plan(rows, &nc, &ch);
@@ -929,15 +930,14 @@ static long long bwd_partial_cap(int B, int A, int C3) {
     for (int mode : {ACMI_GEMM_F32, ACMI_GEMM_X3})
       m = std::max(m, wgrad_plan(Ks[l], co[l], false, rowsL[l], l == 0, mode).floats);
     // G factors of the same layer's output
-    if (co[l] <= 64) {
+    if (co[l] <= 64) {  // (both Gram paths sized: gcov_layer picks by width)
       int nc;
       long long ch;
       gram_plan(rowsL[l], &nc, &ch);
       const long long np = co[l] <= 32 ? 32 : 64;
       m = std::max(m, nc * (np + 1) * np);
-    } else {
-      m = std::max(m, gcov_plan(co[l], rowsL[l]).floats);
     }
+    m = std::max(m, gcov_plan(co[l], rowsL[l]).floats);
   }
   // band reductions of conv2 / conv3 (rows = images)
   m = std::max(m, band_ws_floats(band_host_plan(20, 20, 32, 4, 4, 2, 64), B));
