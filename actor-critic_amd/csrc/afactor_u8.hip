@@ -428,6 +428,344 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WG ? 2 : 4)
   }
 }
 
+// Role-split form of the fused kernel (the default for A factor + weight
+// gradient; ACMI_AF_ROLES=0 selects the kernel above).  The form above deals the
+// 36 A-factor tiles and the 8 weight-gradient tiles to all 8 waves, so every
+// wave reads its row fragments, its B fragments and the whole split d1 operand
+// from LDS -- about 230 KB of LDS reads per 64-row stage, the column sums'
+// 80-byte-strided dword reads 8-way bank conflicted.  Here:
+//  * waves 0-3 own the A factor on column-block quarters, 9 tiles each: wave 0
+//    the upper triangle of blocks 0-3 but (3,3) (from 4 fragments), wave 1 that
+//    of blocks 4-7 but (7,7), waves 2 / 3 blocks 0-3 x 4-5 / 6-7 plus (3,3) /
+//    (7,7) (from 6 fragments): 20 fragment reads per 32 rows instead of 52;
+//  * waves 4-7 own the weight gradient, 64 patch columns (two tiles) each, so
+//    one read of the split d1 operand serves two tiles, and the column sums
+//    (v_dot4 of the patch bytes they read anyway);
+//  * the gather runs two stages ahead (two register sets).
+// Integer partials are exact and each weight-gradient tile accumulates in the
+// same order as above: the results are identical bit for bit.
+__device__ __forceinline__ void af_transpose4(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                              uint32_t* out) {
+  const uint32_t p01l = __builtin_amdgcn_perm(w1, w0, 0x05010400u);
+  const uint32_t p01h = __builtin_amdgcn_perm(w1, w0, 0x07030602u);
+  const uint32_t p23l = __builtin_amdgcn_perm(w3, w2, 0x05010400u);
+  const uint32_t p23h = __builtin_amdgcn_perm(w3, w2, 0x07030602u);
+  out[0] = __builtin_amdgcn_perm(p23l, p01l, 0x05040100u);
+  out[1] = __builtin_amdgcn_perm(p23l, p01l, 0x07060302u);
+  out[2] = __builtin_amdgcn_perm(p23h, p01h, 0x05040100u);
+  out[3] = __builtin_amdgcn_perm(p23h, p01h, 0x07060302u);
+}
+
+// compile-time probes for timing (scripts/afprobe.sh); 0 in the product build
+#ifndef AF_PROBE
+#define AF_PROBE 0
+#endif
+
+struct AfRegs {  // one stage's gather: 4 rows x 8 patch bytes, one float4 of d1
+  uint2 a[4];
+  uint32_t f;  // the rows' XOR mask: 0x80 bytes (x = u - 128), 0 past the chunk
+  StF4 d;
+};
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void conv1_afactor_roles_kernel(
+    const uint8_t* obs, long long img_stride, int rows, int chunk_rows, int* part, int* colsum,
+    const float* d1, float* wpart) {
+  const int total = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, base_l = total >> 3, rem = total & 7;
+  const int chunk = xcd * base_l + min(xcd, rem) + (b >> 3);
+  const int r_begin = chunk * chunk_rows;
+  const int r_end = min(rows, r_begin + chunk_rows);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2][256 * AF_LINE];
+  constexpr int DRA = 64;             // d1 image row bytes: 32 channels x bf16
+  constexpr int DPART = AF_BK * DRA;  // 4 KB per split part
+  __shared__ __attribute__((aligned(16))) char dimg[2][3 * DPART];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // roles branch on SGPRs
+  const int half = lane >> 5;
+  // staging map (as above): 4 rows x 8 patch columns per thread; d1: one float4
+  const int drow = tid >> 3, dcol = (tid & 7) * 4;
+  const int q4 = tid & 15;
+  const int c = 8 * (tid >> 4);
+  const int coff = (((c >> 5) * AF_OBS_W) + ((c & 31) >> 2)) * 4;
+  const uint32_t istride = (uint32_t)img_stride;
+
+  // Buffer loads on 32-bit offsets: a row past r_end gets an offset past the
+  // buffer's end, so the hardware returns zeros (its patch XOR mask is then 0:
+  // x = 0; its d1 = 0).  The gather position advances AF_BK rows per fetch
+  // (fetches run in row order), so the per-stage decode is a few adds.
+  const uint32_t obs_nr = (uint32_t)(rows / 400) * istride;
+  const uint32_t d1_nr = (uint32_t)rows * 128u;
+  const __amdgpu_buffer_rsrc_t obs_rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(obs), (short)0, (int)obs_nr, 0x00020000);
+  const __amdgpu_buffer_rsrc_t d1_rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(d1), (short)0, (int)d1_nr, 0x00020000);
+  int fr = r_begin + 4 * q4;                                  // first of the thread's 4 rows
+  uint32_t fp = (uint32_t)fr % 400u;                          // its output position
+  uint32_t fimg = (uint32_t)fr / 400u * istride + (uint32_t)coff;  // image + column offset
+  int fk = r_begin + drow;                                    // d1 row
+  const uint32_t dcb = (uint32_t)dcol * 4u;
+  auto fetch = [&](AfRegs& R) {
+    if constexpr (AF_PROBE == 8) {  // no loads: synthetic bytes
+      R.a[0] = make_uint2(fr, fp); R.a[1] = make_uint2(fp, fr); R.a[2] = make_uint2(fk, fr); R.a[3] = make_uint2(fr, fk);
+      R.f = 0x80808080u;
+      R.d = make_float4((float)fk, 0.f, 1.f, 2.f);
+      fr += AF_BK; fk += AF_BK; fp += 3;
+      return;
+    }
+    const bool ok = fr < r_end;
+    const uint32_t oh = (fp * 3277u) >> 16;  // fp / 20 (fp < 400)
+    // ((4 oh) * 84 + 4 ow) * 4 with ow = fp - 20 oh
+    const uint32_t off = ok ? fimg + 16u * fp + 1024u * oh : obs_nr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      R.a[q] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(obs_rs, off + 16u * q, 0, 0));
+    R.f = ok ? 0x80808080u : 0u;
+    const uint32_t doff = fk < r_end ? (uint32_t)fk * 128u + dcb : d1_nr;
+    R.d = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(d1_rs, doff, 0, 0));
+    fr += AF_BK;
+    fk += AF_BK;
+    fp += AF_BK;
+    const bool wrap = fp >= 400u;
+    fp = wrap ? fp - 400u : fp;
+    fimg = wrap ? fimg + istride : fimg;
+  };
+  double dsum[4] = {0.0, 0.0, 0.0, 0.0};  // bias gradient (as above)
+  uint32_t sink = 0;
+  auto commit = [&](const AfRegs& R, int buf) {
+    if constexpr (AF_PROBE == 3 || AF_PROBE == 4) {
+      sink ^= R.a[0].x ^ R.a[1].x ^ R.a[2].x ^ R.a[3].x ^ R.a[0].y ^ R.a[1].y ^ R.a[2].y ^ R.a[3].y ^
+              __float_as_uint(R.d.x) ^ __float_as_uint(R.d.w);
+      return;
+    }
+    const uint32_t F = R.f;
+    uint32_t cols[8];
+    af_transpose4(R.a[0].x ^ F, R.a[1].x ^ F, R.a[2].x ^ F, R.a[3].x ^ F, cols);
+    af_transpose4(R.a[0].y ^ F, R.a[1].y ^ F, R.a[2].y ^ F, R.a[3].y ^ F, cols + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) *reinterpret_cast<uint32_t*>(lds[buf] + (c + j) * AF_LINE + 4 * q4) = cols[j];
+    dsum[0] += (double)R.d.x;
+    dsum[1] += (double)R.d.y;
+    dsum[2] += (double)R.d.z;
+    dsum[3] += (double)R.d.w;
+    uint2 h, m, l;
+    split3(R.d.x, R.d.y, h.x, m.x, l.x);
+    split3(R.d.z, R.d.w, h.y, m.y, l.y);
+    char* ds = dimg[buf] + drow * DRA + 2 * dcol;
+    *reinterpret_cast<uint2*>(ds) = h;
+    *reinterpret_cast<uint2*>(ds + DPART) = m;
+    *reinterpret_cast<uint2*>(ds + 2 * DPART) = l;
+  };
+
+  const int fb = wave == 1 ? 4 : 0;  // tri roles: first of the 4 column blocks
+  const int gb = wave == 2 ? 4 : 6;  // rect roles: column blocks gb, gb + 1
+  // d1 fragment offset in the [k][32] image (conv1_wgrad_x3_kernel's map)
+  const int daoff = (8 * half + ((lane >> 2) & 3)) * DRA + 8 * (4 * ((lane >> 4) & 1) + (lane & 3));
+  const int nst = r_end > r_begin ? (r_end - r_begin + AF_BK - 1) / AF_BK : 0;
+  int* out = part + (long long)chunk * 65536;
+  auto put = [&](const v16i& v, int ti, int tj) {
+    const int col = 32 * tj + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 32 * ti + (r & 3) + 8 * (r >> 2) + 4 * half;
+      out[row * 256 + col] = v[r];
+    }
+  };
+
+  // Each role runs the whole stage loop with its own accumulators (one loop
+  // shared by the roles merges their register sets at every join and spills).
+  // The branch is wave-uniform and every role executes the same barriers.
+  auto run = [&](auto ROLEc) {
+    constexpr int ROLE = decltype(ROLEc)::value;  // 0 tri, 1 rect, 2 weight gradient
+    constexpr int NT = ROLE == 2 ? 2 : 9;
+    v16i acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0;
+    int csum[2] = {0, 0};  // weight-gradient role: its two patch columns' sums of x
+
+    auto compute = [&](int cur) {
+      if constexpr (AF_PROBE == 1 || AF_PROBE == 4 || AF_PROBE == 7 || (AF_PROBE == 5 && ROLE == 2) ||
+                    (AF_PROBE == 6 && ROLE < 2))
+        return;
+      const uint8_t* S = lds[cur] + (lane & 31) * AF_LINE + 16 * half;
+      if constexpr (ROLE == 0) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          v4i f[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) f[i] = *reinterpret_cast<const v4i*>(S + (fb + i) * 32 * AF_LINE + 32 * s);
+          int t = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = i; j < 4 - (i == 3); ++j, ++t)
+              acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f[i], f[j], acc[t], 0, 0, 0);
+        }
+      } else if constexpr (ROLE == 1) {
+        // the diagonal tile (3,3) / (7,7): block db's fragment
+        const int db = wave == 2 ? 3 : 7;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          v4i f[4], g[2];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) f[i] = *reinterpret_cast<const v4i*>(S + i * 32 * AF_LINE + 32 * s);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) g[j] = *reinterpret_cast<const v4i*>(S + (gb + j) * 32 * AF_LINE + 32 * s);
+          const v4i dg = *reinterpret_cast<const v4i*>(S + db * 32 * AF_LINE + 32 * s);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[2 * i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f[i], g[j], acc[2 * i + j], 0, 0, 0);
+          acc[8] = __builtin_amdgcn_mfma_i32_32x32x32_i8(dg, dg, acc[8], 0, 0, 0);
+        }
+      } else {
+        // weight gradient: C^T[channel][patch column] over this stage's 64 rows.
+        // Software-pipelined: every LDS operand of the stage is read up front,
+        // and the u8 -> bf16 conversion of k-step ks + 1 (VALU) is interleaved
+        // with the six MFMAs of k-step ks (one wave issues both in order).
+        const char* dsb = dimg[cur];
+        const uint8_t* pc = lds[cur] + (64 * (wave - 4) + (lane & 31)) * AF_LINE + 8 * half;
+        constexpr int NK = AF_BK / 16;
+        bf16x8 a[NK][3];
+        uint2 xb[NK][2];
+#pragma unroll
+        for (int ks = 0; ks < NK; ++ks) {
+#pragma unroll
+          for (int pt = 0; pt < 3; ++pt) {
+            const char* ap = dsb + pt * DPART + 16 * ks * DRA + daoff;
+            a[ks][pt] = cat8(ds_tr16(ap), ds_tr16(ap + 4 * DRA));
+          }
+#pragma unroll
+          for (int tt = 0; tt < 2; ++tt) xb[ks][tt] = *reinterpret_cast<const uint2*>(pc + tt * 32 * AF_LINE + 16 * ks);
+        }
+        auto convert = [&](const uint2& x, int tt) {
+          csum[tt] = __builtin_amdgcn_sdot4((int)x.x, 0x01010101, csum[tt], false);
+          csum[tt] = __builtin_amdgcn_sdot4((int)x.y, 0x01010101, csum[tt], false);
+          const uint32_t u0 = x.x ^ 0x80808080u, u1 = x.y ^ 0x80808080u;  // back to u
+          const uint4 pb = make_uint4(pk_bf16((float)(u0 & 255u), (float)((u0 >> 8) & 255u)),
+                                      pk_bf16((float)((u0 >> 16) & 255u), (float)(u0 >> 24)),
+                                      pk_bf16((float)(u1 & 255u), (float)((u1 >> 8) & 255u)),
+                                      pk_bf16((float)((u1 >> 16) & 255u), (float)(u1 >> 24)));
+          return __builtin_bit_cast(bf16x8, pb);
+        };
+        f32x16 w0 = __builtin_bit_cast(f32x16, acc[0]);
+        f32x16 w1 = __builtin_bit_cast(f32x16, acc[1]);
+        bf16x8 b0 = convert(xb[0][0], 0), b1 = convert(xb[0][1], 1);
+#pragma unroll
+        for (int ks = 0; ks < NK; ++ks) {
+          bf16x8 n0 = b0, n1 = b1;
+          if (ks + 1 < NK) {
+            n0 = convert(xb[ks + 1][0], 0);
+            n1 = convert(xb[ks + 1][1], 1);
+          }
+#pragma unroll
+          for (int pt = 2; pt >= 0; --pt) {  // l, m, h: the order of the kernel above
+            w0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][pt], b0, w0, 0, 0, 0);
+            w1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][pt], b1, w1, 0, 0, 0);
+          }
+          if (ks + 1 < NK)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {  // one MFMA, then a share of the next conversion
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+            }
+          b0 = n0;
+          b1 = n1;
+        }
+        acc[0] = __builtin_bit_cast(v16i, w0);
+        acc[1] = __builtin_bit_cast(v16i, w1);
+      }
+    };
+
+    AfRegs R0, R1;
+    fetch(R0);
+    fetch(R1);
+    commit(R0, 0);
+    __syncthreads();
+    // stage st computes buffer st & 1, gathers stage st + 2 into the register set
+    // stage st just committed, and commits stage st + 1 from the other set
+    auto stage = [&](int st, AfRegs& Rn, const AfRegs& Rc) {
+      const int cur = st & 1;
+      fetch(Rn);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(cur);
+      __builtin_amdgcn_sched_barrier(0);
+      commit(Rc, cur ^ 1);
+      if constexpr (AF_PROBE != 7) __syncthreads();
+    };
+    // (the odd last stage after the loop: a conditional second stage inside it
+    // would leave the first set's loads pending at the back edge, and the wait
+    // at the loop head would drain every load each iteration)
+    int st = 0;
+    for (; st + 1 < nst; st += 2) {
+      stage(st, R0, R1);
+      stage(st + 1, R1, R0);
+    }
+    if (st < nst) stage(st, R0, R1);
+
+    if constexpr (ROLE == 0) {
+      int t = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = i; j < 4 - (i == 3); ++j, ++t) put(acc[t], fb + i, fb + j);
+    } else if constexpr (ROLE == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) put(acc[2 * i + j], i, gb + j);
+      put(acc[8], wave == 2 ? 3 : 7, wave == 2 ? 3 : 7);
+    } else {
+      // column sums: the two row halves (lanes l, l + 32) of each patch column;
+      // integer sums, any order
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const int v = csum[tt] + __shfl_xor(csum[tt], 32);
+        if (half == 0) colsum[(long long)chunk * 256 + 64 * (wave - 4) + 32 * tt + lane] = v;
+      }
+      // acc[tt][r]: channel (r&3) + 8(r>>2) + 4(lane>>5), patch column i
+      float* wout = wpart + (long long)chunk * 257 * 32;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const f32x16 w = __builtin_bit_cast(f32x16, acc[tt]);
+        const int i = 64 * (wave - 4) + 32 * tt + (lane & 31);
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq)
+          *reinterpret_cast<float4*>(wout + i * 32 + 8 * gq + 4 * half) =
+              make_float4(w[4 * gq], w[4 * gq + 1], w[4 * gq + 2], w[4 * gq + 3]);
+      }
+    }
+  };
+  if (wave < 2)
+    run(std::integral_constant<int, 0>{});
+  else if (wave < 4)
+    run(std::integral_constant<int, 1>{});
+  else
+    run(std::integral_constant<int, 2>{});
+  if (AF_PROBE != 0 && sink == 0x9e3779b9u && rows < 0) colsum[0] = (int)sink;
+
+  // bias gradient (row 256): the 64 row-threads of each channel group through LDS
+  double* cs = reinterpret_cast<double*>(&lds[0][0]);  // free after the last stage's barrier
+#pragma unroll
+  for (int e = 0; e < 4; ++e) cs[drow * 32 + dcol + e] = dsum[e];
+  __syncthreads();
+  if (tid < 32) {
+    double t = 0.0;
+    for (int r = 0; r < AF_BK; ++r) t += cs[r * 32 + tid];
+    wpart[(long long)chunk * 257 * 32 + 256 * 32 + tid] = (float)t;
+  }
+}
+
+// read per call (tests switch it in-process; one getenv per 400 us launch)
+static int af_roles() {
+  const char* e = getenv("ACMI_AF_ROLES");
+  return e ? atoi(e) : 1;
+}
+
 // chunks for the one-block-per-chunk kernel: 2 blocks per CU resident
 static void af_plan_tri(long long rows, int* nchunk, int* chunk) {
   const long long slots = 256 * 2;
@@ -533,7 +871,12 @@ int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* ast
   // fused weight-gradient partials after the int64 sums (16-byte aligned)
   float* wpart = reinterpret_cast<float*>(((uintptr_t)(sums + 65536 + 256) + 15) & ~(uintptr_t)15);
   if (wpart_out) *wpart_out = d1 ? wpart : nullptr;
-  if (tri && d1)
+  // the role-split kernel's buffer offsets: frames and d1 within 2^32 bytes
+  const bool roles = af_roles() && (long long)B * img_stride <= (1LL << 32) - 64 && rows * 128 < (1LL << 32);
+  if (tri && d1 && roles)
+    hipLaunchKernelGGL(conv1_afactor_roles_kernel, dim3(nchunk), dim3(512), 0, s, obs, img_stride,
+                       (int)rows, chunk, part, colsum, d1, wpart);
+  else if (tri && d1)
     hipLaunchKernelGGL(conv1_afactor_i8_tri_kernel<true>, dim3(nchunk), dim3(512), 0, s, obs, img_stride,
                        (int)rows, chunk, part, colsum, d1, wpart);
   else if (tri)

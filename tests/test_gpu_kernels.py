@@ -490,3 +490,60 @@ def test_bf16_forward_mode(lib, cuda, A, C3):
         print(name, 'bf16 forward rel err %.2e' % err)
         assert err < 1e-2, (name, err)
         assert not torch.equal(bf[name], f32a[name]), name  # the mode really changed the arithmetic
+
+
+@pytest.mark.parametrize('B', [6, 300, 1000])
+def test_conv1_afactor_roles_bit_identical(lib, cuda, B):
+    """The role-split fused conv1 A-factor + weight-gradient kernel
+    (conv1_afactor_roles_kernel, the default) against the all-waves form
+    (ACMI_AF_ROLES=0): identical gradients and factors bit for bit (exact
+    integer partials; each weight-gradient tile accumulates in the same order).
+    B = 6: one stage per chunk (the odd tail only); 300: 4 stages (the paired
+    loop only); 1000: 13 stages (both).  At B = 300 the conv1 A factor is also
+    checked against the exact integer patch Gram."""
+    import os
+    A, C3 = 4, 32
+    params = rand_params(A, C3, cuda, seed=31)
+    g = torch.Generator().manual_seed(32)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8)
+    obs_d = obs.to(cuda)
+    t, acts = alloc_acts(B, A, C3, cuda)
+    net = _net(params, A, C3)
+    _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs_d), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+              _lib.stream_handle())
+    ldh = 8
+    dhead = torch.zeros(B, ldh)
+    dhead[:, :A + 1] = torch.randn(B, A + 1, generator=g) / B
+    dhead = dhead.to(cuda)
+    z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=cuda)
+    din = (ctypes.c_int64 * 6)()
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, din, None, so, ctypes.byref(tot))
+    ws = z(lib.acmi_backward_ws_floats(B, A, C3))
+    out = {}
+    prev = os.environ.get('ACMI_AF_ROLES')
+    try:
+        for roles in ('0', '1'):
+            os.environ['ACMI_AF_ROLES'] = roles
+            d = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
+            bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
+            grads, astat = z(params.numel()), z(tot.value)
+            _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs_d), 84 * 84 * 4, B, ctypes.byref(acts),
+                      ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), _lib.stream_handle())
+            torch.cuda.synchronize()
+            out[roles] = (grads.cpu(), astat.cpu())
+    finally:
+        if prev is None:
+            os.environ.pop('ACMI_AF_ROLES', None)
+        else:
+            os.environ['ACMI_AF_ROLES'] = prev
+    assert torch.equal(out['0'][0], out['1'][0])
+    assert torch.equal(out['0'][1], out['1'][1])
+    if B == 300:
+        p = obs.double().unfold(1, 8, 4).unfold(2, 8, 4).permute(0, 1, 2, 4, 5, 3).reshape(-1, 256)
+        pb = torch.cat([p, torch.full((p.shape[0], 1), 255.0, dtype=torch.float64)], 1)
+        ref = (pb.t() @ pb) / (65025.0 * p.shape[0])  # integer sums: exact in float64
+        got = out['1'][1][so[0]:so[0] + 257 * 257].double().reshape(257, 257)
+        rel = (got - ref).abs().max().item() / ref.abs().max().item()
+        assert rel < 1e-6, rel
