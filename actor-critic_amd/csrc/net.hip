@@ -199,6 +199,19 @@ __global__ __launch_bounds__(256) void rollout_tail_kernel(
     long long l_stride, float* value, long long v_stride, TailArgs ta) {
   const int row = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  EnvPre pre;  // the env's state and current stack: in flight during the heads
+  env_prefetch(ta.io.state, row, ta.obs + (long long)row * ta.img_stride, pre);
+  // head a's weight for a4 element lane + 64 e (a == A: the value head); the
+  // wave's first two heads are loaded now, beside the slab and stack loads
+  auto head_w = [&](int a, int e) {
+    const int ai = a < A ? a : 0;
+    return a < A ? wpi[(lane + 64 * e) * A + ai] : wv[lane + 64 * e];
+  };
+  float hw[2][8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) hw[h][e] = head_w(min(wave + 4 * h, A), e);  // (unused past A)
   __shared__ float sx[512];
   __shared__ float sl[kMaxHeads];
   __shared__ int s_action;
@@ -221,17 +234,20 @@ __global__ __launch_bounds__(256) void rollout_tail_kernel(
   float xv[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) xv[e] = sx[lane + 64 * e];
-  for (int a = wave; a <= A; a += 4) {  // head a (a == A: the value head)
+  auto head = [&](int a, const float (&w)[8]) {  // head a (a == A: the value head)
     float s = 0.f;
-    if (a < A) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += xv[e] * wpi[(lane + 64 * e) * A + a];
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s += xv[e] * wv[lane + 64 * e];
-    }
+    for (int e = 0; e < 8; ++e) s += xv[e] * w[e];
     s = wave_sum(s);
     if (lane == 0) sl[a] = s + (a < A ? bpi[a] : bv[0]);
+  };
+  if (wave <= A) head(wave, hw[0]);
+  if (wave + 4 <= A) head(wave + 4, hw[1]);
+  for (int a = wave + 8; a <= A; a += 4) {
+    float w[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w[e] = head_w(a, e);
+    head(a, w);
   }
   __syncthreads();
   const acmi_rollout_io_t& io = ta.io;
@@ -247,9 +263,9 @@ __global__ __launch_bounds__(256) void rollout_tail_kernel(
     s_action = y;
   }
   __syncthreads();
-  env_step_block(io.state, row, (uint32_t)(io.env_offset + row), io.env_seed, (uint32_t)s_action,
-                 ta.obs + (long long)row * ta.img_stride, io.obs_out + (long long)row * io.out_stride,
-                 io.rewards, io.terminals, io.episode_rewards, io.ld);
+  env_step_block_pre(io.state, row, (uint32_t)(io.env_offset + row), io.env_seed, (uint32_t)s_action, pre,
+                     io.obs_out + (long long)row * io.out_stride, io.rewards, io.terminals,
+                     io.episode_rewards, io.ld);
 }
 
 inline int roundup4(int x) { return (x + 3) & ~3; }

@@ -22,22 +22,50 @@ __device__ __forceinline__ int32_t episode_length(uint32_t seed, uint32_t e, uin
   return 50 + (int32_t)(key4(seed, e, k, LEN_TAG) % 451u);
 }
 
-// One env step for env n (global id e) by a whole workgroup: reads the
-// pre-step state, lazily auto-resets, writes the next 4-frame stack, reward,
-// terminal and episode total.  Contains a __syncthreads (every thread of the
-// block must call it).
-__device__ __forceinline__ void env_step_block(acmi_env_state_t st, int n, uint32_t e, uint32_t seed,
-                                               uint32_t action, const uint8_t* obs_in,
-                                               uint8_t* obs_out, float* rewards,
-                                               uint8_t* terminals, float* ep_rewards,
-                                               long long ld) {
-  // every thread reads the (pre-step) state, then a barrier before thread 0
-  // writes the new state
-  const bool was_done = st.done[n] != 0;
-  int32_t k = st.episode[n];
-  int32_t t = st.step[n];
-  int32_t L = st.length[n];
-  float total = st.total[n];
+// One env step for env n (global id e) by a whole 256-thread workgroup: reads
+// the pre-step state, lazily auto-resets, writes the next 4-frame stack,
+// reward, terminal and episode total.  Contains a __syncthreads (every thread
+// of the block must call it).  The previous stack's words are loaded first,
+// all kEnvWords of a thread at once (env_prefetch: they do not depend on the
+// action, so the fused rollout tail issues them before its head arithmetic);
+// a load per loop iteration would wait out one memory latency per iteration.
+constexpr int kEnvThreads = 256;
+constexpr int kEnvWords = (FRAME_WORDS + kEnvThreads - 1) / kEnvThreads;  // 7
+
+struct EnvPre {  // an env's pre-step state and current stack words, loaded up front
+  uint4 old[kEnvWords];
+  int32_t k, t, L;
+  float total;
+  bool was_done;
+};
+
+__device__ __forceinline__ void env_prefetch(acmi_env_state_t st, int n, const uint8_t* obs_in, EnvPre& p) {
+  const uint4* in = reinterpret_cast<const uint4*>(obs_in);
+#pragma unroll
+  for (int i = 0; i < kEnvWords; ++i) {
+    const int g = threadIdx.x + kEnvThreads * i;
+    p.old[i] = in[g < FRAME_WORDS ? g : 0];
+  }
+  p.was_done = st.done[n] != 0;
+  p.k = st.episode[n];
+  p.t = st.step[n];
+  p.L = st.length[n];
+  p.total = st.total[n];
+}
+
+// (the state of env n must have been read by every thread -- env_prefetch --
+// before this is called: it begins with the barrier that orders those reads
+// before thread 0's state writes)
+__device__ __forceinline__ void env_step_block_pre(acmi_env_state_t st, int n, uint32_t e, uint32_t seed,
+                                                   uint32_t action, const EnvPre& pre,
+                                                   uint8_t* obs_out, float* rewards,
+                                                   uint8_t* terminals, float* ep_rewards,
+                                                   long long ld) {
+  const bool was_done = pre.was_done;
+  int32_t k = pre.k;
+  int32_t t = pre.t;
+  int32_t L = pre.L;
+  float total = pre.total;
   __syncthreads();
   if (was_done) {  // _AutoResetWrapper: reset lazily at the next step
     k += 1;
@@ -52,18 +80,18 @@ __device__ __forceinline__ void env_step_block(acmi_env_state_t st, int n, uint3
   const float rew = rh < REW_LO ? -1.f : (rh >= REW_HI ? 1.f : 0.f);
   const bool term = t >= L;
   const uint32_t rbase = key4(seed, e, (uint32_t)k, RESET_TAG);
-  const uint4* in = reinterpret_cast<const uint4*>(obs_in);
   uint4* out = reinterpret_cast<uint4*>(obs_out);
-  for (int g = threadIdx.x; g < FRAME_WORDS; g += blockDim.x) {
-    uint4 old;
+#pragma unroll
+  for (int i = 0; i < kEnvWords; ++i) {
+    const int g = threadIdx.x + kEnvThreads * i;
+    if (g >= FRAME_WORDS) break;
+    uint4 old = pre.old[i];
     if (was_done) {  // FrameStackWrapper.reset: the reset frame repeated 4x
       const uint32_t w = word_hash(rbase, (uint32_t)g);
       old.x = (w & 255u) * 0x01010101u;
       old.y = ((w >> 8) & 255u) * 0x01010101u;
       old.z = ((w >> 16) & 255u) * 0x01010101u;
       old.w = (w >> 24) * 0x01010101u;
-    } else {
-      old = in[g];
     }
     const uint32_t f = word_hash(base, (uint32_t)g);
     // np.roll(stack, -1, axis=-1); zero-fill on terminal; last channel = frame
@@ -85,6 +113,16 @@ __device__ __forceinline__ void env_step_block(acmi_env_state_t st, int n, uint3
     st.total[n] = term ? 0.f : total;
     st.done[n] = term ? 1 : 0;
   }
+}
+
+__device__ __forceinline__ void env_step_block(acmi_env_state_t st, int n, uint32_t e, uint32_t seed,
+                                               uint32_t action, const uint8_t* obs_in,
+                                               uint8_t* obs_out, float* rewards,
+                                               uint8_t* terminals, float* ep_rewards,
+                                               long long ld) {
+  EnvPre pre;
+  env_prefetch(st, n, obs_in, pre);
+  env_step_block_pre(st, n, e, seed, action, pre, obs_out, rewards, terminals, ep_rewards, ld);
 }
 
 // Categorical draw over the A logits z[0..A) (inverse CDF of softmax in f32
