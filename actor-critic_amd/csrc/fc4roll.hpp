@@ -1,0 +1,124 @@
+// fc4 at the rollout batch (envs/atari/model.py:197-201 -> nn.py:88-107 at
+// B = N images): the split-K partial slabs [nz][B+1][512] that
+// rollout_tail_kernel / heads_kernel reduce, computed without LDS.
+//
+// At B = 512 the staged gemm3 launch (64x128 tiles, 8 K chunks, 256 blocks) is
+// a chain of 13 dependent K-tiles, each behind one global load round trip and
+// a barrier: 15 us for 2.4 GFLOP.  Here W4 comes pre-split into the bf16 h/m/l
+// parts of every lane's B fragment (acmi_conv_prepare, once per parameter
+// version, fragment-major like the tower's weights), each wave loads its own
+// A fragments (8 consecutive k of one row per lane: two float4) and its B
+// fragments straight from L2, kFc4Depth k-steps ahead in registers, and owns a
+// 32-row x 64-column tile of one K chunk -- no LDS, no barrier.  Blocks map K
+// chunk z to XCD z (b % nz), so an XCD's L2 holds only its chunk's W4 columns
+// (590 KB) and a3 columns (400 KB at B = 512).
+//
+// Arithmetic: the same bf16x3 split of the same f32 values and the same
+// mfma_x3 sequence per k16-step and chunk as gemm3_kernel + EpiPartial, so the
+// slabs are bit-identical to the staged launch's (test_fc4_rollout_bit_identical).
+#pragma once
+
+#include "tower.hpp"
+
+namespace acmi {
+
+constexpr int kFc4Depth = 3;  // k-steps in flight ahead of the one computed
+
+// W4 [K][512] -> [K/16 steps][16 col tiles][part h, m, l][64 lanes] x 16 B
+__global__ void fc4_prep_kernel(const float* w4, int K, char* out) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = g & 63, f = g >> 6;  // f = step * 16 + col tile
+  if (f >= (K / 16) * 16) return;
+  const int s = f >> 4, ct = f & 15;
+  const float* p = w4 + (16 * s + 8 * (lane >> 5)) * 512 + 32 * ct + (lane & 31);
+  uint4 h, m, l;
+  split3(p[0], p[512], h.x, m.x, l.x);
+  split3(p[2 * 512], p[3 * 512], h.y, m.y, l.y);
+  split3(p[4 * 512], p[5 * 512], h.z, m.z, l.z);
+  split3(p[6 * 512], p[7 * 512], h.w, m.w, l.w);
+  uint4* d = reinterpret_cast<uint4*>(out) + (long long)f * 192 + lane;
+  d[0] = h;
+  d[64] = m;
+  d[128] = l;
+}
+
+inline long long fc4_prep_bytes(int K) { return (long long)(K / 16) * 16 * 3 * 1024; }
+
+// block b: K chunk z = b % nz, then (row tile, column half); wave w: column
+// group 4 * half + w (64 columns).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
+void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w4p, int nz, int chunk_steps,
+                     float* part) {
+  constexpr int D = kFc4Depth, NSLOT = D + 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int z = blockIdx.x % nz, rest = blockIdx.x / nz;
+  const int rt = rest >> 1, cg = 4 * (rest & 1) + wave;
+  const int s0 = z * chunk_steps;
+  const int ns = min(K / 16, s0 + chunk_steps) - s0;
+  const int col = lane & 31;
+  const int row = min(32 * rt + col, B - 1);
+  const float* ap = a3 + (long long)row * lda + 16 * s0 + 8 * (lane >> 5);
+  // fragment (step s, col tile ct, part pt): uint4 index (s * 16 + ct) * 192 + 64 pt + lane
+  const uint4* bp = reinterpret_cast<const uint4*>(w4p) + ((long long)s0 * 16 + 2 * cg) * 192 + lane;
+
+  float4 av[NSLOT][2];
+  uint4 bv[NSLOT][2][3];
+  auto load = [&](int i, int slot) {
+    const float4* a = reinterpret_cast<const float4*>(ap + 16 * i);
+    av[slot][0] = a[0];
+    av[slot][1] = a[1];
+    const uint4* b = bp + (long long)i * 16 * 192;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt) bv[slot][t][pt] = b[t * 192 + 64 * pt];
+  };
+  f32x16 acc[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (i < ns) load(i, i);
+  // step i lives in slot i % NSLOT: a runtime loop over whole slot rounds with
+  // the slots unrolled, so every register-array index is a constant
+  for (int i0 = 0; i0 < ns; i0 += NSLOT) {
+#pragma unroll
+    for (int sl = 0; sl < NSLOT; ++sl) {
+      const int i = i0 + sl;
+      if (i < ns) {
+        if (i + D < ns) load(i + D, (sl + D) % NSLOT);
+        bf16x8 a[3];
+        tow_split8(av[sl][0], av[sl][1], a);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          bf16x8 b[3];
+#pragma unroll
+          for (int pt = 0; pt < 3; ++pt) b[pt] = __builtin_bit_cast(bf16x8, bv[sl][t][pt]);
+          acc[t] = mfma_x3(a, b, acc[t]);
+        }
+      }
+    }
+  }
+  float* out = part + (long long)z * (B + 1) * 512 + 64 * cg + col;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rr = 32 * rt + tow_row(r, lane);
+      if (rr < B) out[(long long)rr * 512 + 32 * t] = acc[t][r];
+    }
+}
+
+// false when the shape is not one this kernel covers (the caller then uses gemm3)
+inline bool launch_fc4_roll(const float* a3, long long lda, int B, int K, const char* w4p, int nz, int chunk,
+                            float* part, hipStream_t s) {
+  if (chunk % 16 || K % 16 || (lda % 4) || ((uintptr_t)a3 % 16)) return false;
+  const int cs = chunk / 16;
+  const dim3 grid(nz * ((B + 31) / 32) * 2), blk(256);
+  hipLaunchKernelGGL(fc4_roll_kernel, grid, blk, 0, s, a3, lda, B, K, w4p, nz, cs, part);
+  return true;
+}
+
+}  // namespace acmi

@@ -20,6 +20,7 @@
 #include "convfwd3.hpp"
 #include "band.hpp"
 #include "tower.hpp"
+#include "fc4roll.hpp"
 #include "convt2.hpp"
 #include "stepper.hpp"
 
@@ -363,6 +364,13 @@ static int tower_on() {
   return v;
 }
 
+// fc4's split-K slabs at rollout batches on the pre-split W4 without LDS
+// (fc4roll.hpp; needs net->conv_prep): ACMI_FC4R = 1 (default) or 0 (gemm3)
+static int fc4r_on() {
+  static const int v = getenv("ACMI_FC4R") ? atoi(getenv("ACMI_FC4R")) : 1;
+  return v;
+}
+
 // split factor for fc4 at small batch (64 x 128 tiles over 512 columns)
 static void fc4_plan(int B, int K, int* nz, int* chunk) {
   static const int maxsp = getenv("ACMI_FC4_SPLIT") ? atoi(getenv("ACMI_FC4_SPLIT")) : 8;
@@ -441,8 +449,12 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   if (split) {
     // small (rollout) batches: split K over chunks; the heads kernel reduces
     // the slabs in fixed order and applies bias + relu
-    EpiPartial epi{a->ws, B, 512};
-    launch_mm<64, 128, 32, 1, 2, true, false, 16>(opA4, opB4, epi, B, 512, K4, nz, chunk, s);
+    const char* w4p = prep ? static_cast<const char*>(prep) + TowerPrep<C3>::BYTES + CT2::BYTES : nullptr;
+    if (!(g_gemm_mode == ACMI_GEMM_X3 && w4p && fc4r_on() &&
+          launch_fc4_roll(a->a3, st * K4, B, K4, w4p, nz, chunk, a->ws, s))) {
+      EpiPartial epi{a->ws, B, 512};
+      launch_mm<64, 128, 32, 1, 2, true, false, 16>(opA4, opB4, epi, B, 512, K4, nz, chunk, s);
+    }
   } else {
     EpiAct epi{a->a4, P + L.off[7], 512, 1, st * 512};
     launch_mm<64, 128, 32, 1, 2, false, false, 16>(opA4, opB4, epi, B, 512, K4, 1, 0, s);
@@ -1358,7 +1370,10 @@ static int forward_dispatch(const acmi_net_t* net, const uint8_t* obs, int64_t i
 
 int64_t acmi_conv_prep_bytes(int C3) {
   // the tower's conv weights, then conv2's input-gradient weights (convt2.hpp)
-  return C3 == 32 ? TowerPrep<32>::BYTES + CT2::BYTES : C3 == 64 ? TowerPrep<64>::BYTES + CT2::BYTES : -1;
+  // and fc4's weights (fc4roll.hpp)
+  return C3 == 32   ? TowerPrep<32>::BYTES + CT2::BYTES + fc4_prep_bytes(49 * 32)
+         : C3 == 64 ? TowerPrep<64>::BYTES + CT2::BYTES + fc4_prep_bytes(49 * 64)
+                    : -1;
 }
 
 int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
@@ -1370,6 +1385,9 @@ int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
   const long long o2 = L.C3 == 32 ? TowerPrep<32>::BYTES : TowerPrep<64>::BYTES;
   hipLaunchKernelGGL(convt2_prep_kernel, dim3(CT2::NKS * 4 * 64 / 256), dim3(256), 0, (hipStream_t)stream,
                      net->params + L.off[2], static_cast<char*>(prep) + o2);
+  const int K4 = 49 * L.C3;
+  hipLaunchKernelGGL(fc4_prep_kernel, dim3(K4 / 16 * 16 * 64 / 256), dim3(256), 0, (hipStream_t)stream,
+                     net->params + L.off[6], K4, static_cast<char*>(prep) + o2 + CT2::BYTES);
   ACMI_LAUNCH_CHECK("acmi_conv_prepare");
   return ACMI_OK;
 }

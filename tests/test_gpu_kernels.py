@@ -394,6 +394,38 @@ def test_conv_prep_forward_bit_identical(lib, cuda, C3):
         assert torch.equal(outs[0][k], outs[1][k]), k
 
 
+@pytest.mark.parametrize('C3,B', [(32, 37), (32, 512), (64, 512)])
+def test_fc4_rollout_bit_identical(lib, cuda, C3, B):
+    """fc4's split-K slabs at rollout batches on the pre-split W4 (fc4roll.hpp,
+    used when the net carries conv_prep and a forward workspace) are bit-identical
+    to the staged gemm3 split-K launch (same chunks, same bf16x3 split, same MFMA
+    order), and the forward still matches float64 within 1e-5."""
+    A = 4
+    params = rand_params(A, C3, cuda, seed=21)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=torch.Generator().manual_seed(22),
+                        dtype=torch.uint8).to(cuda)
+    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
+    ws = torch.zeros(int(lib.acmi_forward_ws_floats(B)), device=cuda)
+    outs = []
+    for use_prep in (False, True):
+        t, acts = alloc_acts(B, A, C3, cuda)
+        acts.ws, acts.ws_floats = ws.data_ptr(), ws.numel()
+        net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr() if use_prep else None)
+        if use_prep:
+            _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), _lib.stream_handle())
+        _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+                  _lib.stream_handle())
+        torch.cuda.synchronize()
+        outs.append({k: v.cpu() for k, v in t.items()})
+    for k in ('a4', 'logits', 'value'):
+        assert torch.equal(outs[0][k], outs[1][k]), k
+    ref = torch_forward(params, obs.cpu(), A, C3)
+    for name, r in zip(['a1', 'a2', 'a3', 'a4', 'logits', 'value'], ref):
+        got = outs[1][name].double().reshape(r.shape)
+        rel = (got - r).abs().max().item() / max(1e-6, r.abs().max().item())
+        assert rel < 1e-5, (name, rel)
+
+
 @pytest.mark.parametrize('B', [37, 1000])
 def test_convt2_matches_gemm3_path(lib, cuda, B):
     """conv2's input gradient on pre-split weights (convt2.hpp, used when the net
