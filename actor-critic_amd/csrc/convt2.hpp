@@ -78,40 +78,66 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
 #pragma unroll
   for (int r = 0; r < 16; ++r) gacc[r] = 0.f;
 
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // super-pixel column of this lane in a tile, and its dY image
+  struct Col {
+    bool ok;
+    int n, Y, X;
+    const float* dimg;
+  };
+  auto col_of = [&](int tile) {
+    Col c;
     const int j = tile * CT2::TILE + 32 * wave + (lane & 31);
-    const bool jok = j < J;
-    const int jj = jok ? j : 0;
-    const int n = jj / CT2::L, sp = jj - n * CT2::L;
-    const int Y = sp / CT2::PW, X = sp - Y * CT2::PW;
-    const float* dimg = d2 + (long long)n * (CT2::OH * CT2::OW * CT2::COUT);
-    // lane's B fragment for k-step ks: dY pixel (Y - a, X - b), channels co..co+7.
-    // Out-of-image taps load the zero run, selected on the ADDRESS (no branch:
-    // a load under a branch makes the waitcnt pass drain vmcnt at the join)
-    auto bload = [&](int ks, float4 (&x)[2]) {
-      const int t = ks >> 2, a = t >> 1, b = t & 1;
-      const int oy = Y - a, ox = X - b;
-      const bool ok = jok & (oy >= 0) & (oy < CT2::OH) & (ox >= 0) & (ox < CT2::OW);
-      const int oyc = max(oy, 0), oxc = max(ox, 0);  // (in range whenever ok)
-      const float* p = dimg + (oyc * CT2::OW + oxc) * CT2::COUT + 16 * (ks & 3) + 8 * hl;
-      x[0] = *reinterpret_cast<const float4*>(ok ? p : zero);
-      x[1] = *reinterpret_cast<const float4*>(ok ? p + 4 : zero);
-    };
-    // A staging: 12 KB per k-step, three 16-byte runs per thread (named
-    // registers: an array captured by the lambdas below was put in scratch)
-    uint4 ra0, ra1, ra2;
-    auto afetch = [&](int ks) {
-      const uint4* src = reinterpret_cast<const uint4*>(prep + (long long)ks * CT2::STEP_BYTES) + tid;
-      ra0 = src[0];
-      ra1 = src[256];
-      ra2 = src[512];
-    };
-    auto acommit = [&](int buf) {
-      uint4* dst = reinterpret_cast<uint4*>(lds + buf * CT2::STEP_BYTES) + tid;
-      dst[0] = ra0;
-      dst[256] = ra1;
-      dst[512] = ra2;
-    };
+    c.ok = j < J;
+    const int jj = c.ok ? j : 0;
+    c.n = jj / CT2::L;
+    const int sp = jj - c.n * CT2::L;
+    c.Y = sp / CT2::PW;
+    c.X = sp - c.Y * CT2::PW;
+    c.dimg = d2 + (long long)c.n * (CT2::OH * CT2::OW * CT2::COUT);
+    return c;
+  };
+  // lane's B fragment for k-step ks: dY pixel (Y - a, X - b), channels co..co+7.
+  // Out-of-image taps load the zero run, selected on the ADDRESS (no branch:
+  // a load under a branch makes the waitcnt pass drain vmcnt at the join)
+  auto bload = [&](int ks, const Col& c, float4 (&x)[2]) {
+    const int t = ks >> 2, a = t >> 1, b = t & 1;
+    const int oy = c.Y - a, ox = c.X - b;
+    const bool ok = c.ok & (oy >= 0) & (oy < CT2::OH) & (ox >= 0) & (ox < CT2::OW);
+    const int oyc = max(oy, 0), oxc = max(ox, 0);  // (in range whenever ok)
+    const float* p = c.dimg + (oyc * CT2::OW + oxc) * CT2::COUT + 16 * (ks & 3) + 8 * hl;
+    x[0] = *reinterpret_cast<const float4*>(ok ? p : zero);
+    x[1] = *reinterpret_cast<const float4*>(ok ? p + 4 : zero);
+  };
+  // A staging: 12 KB per k-step, three 16-byte runs per thread (named
+  // registers: an array captured by the lambdas below was put in scratch)
+  uint4 ra0, ra1, ra2;
+  auto afetch = [&](int ks) {
+    const uint4* src = reinterpret_cast<const uint4*>(prep + (long long)ks * CT2::STEP_BYTES) + tid;
+    ra0 = src[0];
+    ra1 = src[256];
+    ra2 = src[512];
+  };
+  auto acommit = [&](int buf) {
+    uint4* dst = reinterpret_cast<uint4*>(lds + buf * CT2::STEP_BYTES) + tid;
+    dst[0] = ra0;
+    dst[256] = ra1;
+    dst[512] = ra2;
+  };
+  // two B register sets, alternating by k-step parity (named, never indexed at
+  // run time: a dynamically indexed register array lands in scratch)
+  float4 bx0[2], bx1[2];
+  Col cur = col_of(blockIdx.x);
+  afetch(0);
+  bload(0, cur, bx0);
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // step 0's operands were loaded before the loop or during the previous
+    // tile's last k-step (its A is the same for every tile)
+    const Col nextc = col_of(min(tile + (int)gridDim.x, ntiles - 1));
+    const bool jok = cur.ok;
+    const int n = cur.n, Y = cur.Y, X = cur.X;
+    acommit(0);
+    __syncthreads();
 
     f32x16 acc[4];
 #pragma unroll
@@ -119,24 +145,26 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[p][r] = 0.f;
 
-    // two B register sets, alternating by k-step parity (named, never indexed at
-    // run time: a dynamically indexed register array lands in scratch)
-    float4 bx0[2], bx1[2];
-    auto step = [&](int ks, float4 (&cur)[2], float4 (&nxt)[2]) {
+    auto step = [&](int ks, float4 (&cb)[2], float4 (&nb)[2]) {
       const int buf = ks & 1;
-      // the last step prefetches step NKS-1 again (harmless): no load under a
-      // run-time branch, whose join would make the waitcnt pass drain vmcnt
-      const int kn = min(ks + 1, CT2::NKS - 1);
-      afetch(kn);
-      bload(kn, nxt);
+      // the last k-step loads step 0 of the next tile (selected, not branched:
+      // no load under a run-time branch, whose join would drain vmcnt)
+      const bool last = ks + 1 == CT2::NKS;
+      afetch(last ? 0 : ks + 1);
+      Col c;
+      c.ok = last ? nextc.ok : cur.ok;
+      c.Y = last ? nextc.Y : cur.Y;
+      c.X = last ? nextc.X : cur.X;
+      c.dimg = last ? nextc.dimg : cur.dimg;
+      bload(last ? 0 : ks + 1, c, nb);
       __builtin_amdgcn_sched_barrier(0);
       bf16x8 b[3];
       {
         uint4 h, m, l;
-        split3(cur[0].x, cur[0].y, h.x, m.x, l.x);
-        split3(cur[0].z, cur[0].w, h.y, m.y, l.y);
-        split3(cur[1].x, cur[1].y, h.z, m.z, l.z);
-        split3(cur[1].z, cur[1].w, h.w, m.w, l.w);
+        split3(cb[0].x, cb[0].y, h.x, m.x, l.x);
+        split3(cb[0].z, cb[0].w, h.y, m.y, l.y);
+        split3(cb[1].x, cb[1].y, h.z, m.z, l.z);
+        split3(cb[1].z, cb[1].w, h.w, m.w, l.w);
         b[0] = __builtin_bit_cast(bf16x8, h);
         b[1] = __builtin_bit_cast(bf16x8, m);
         b[2] = __builtin_bit_cast(bf16x8, l);
@@ -151,19 +179,16 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
         acc[p] = mfma_x3(a, b, acc[p]);
       }
       __builtin_amdgcn_sched_barrier(0);
-      acommit(buf ^ 1);
+      if (!last) acommit(buf ^ 1);  // (step 0's A is committed after the epilogue)
       __syncthreads();
     };
-    afetch(0);
-    bload(0, bx0);
-    acommit(0);
-    __syncthreads();
     // two steps per iteration, not unrolled further (a full unroll keeps every
     // step's addresses live and spills)
     for (int ks = 0; ks < CT2::NKS; ks += 2) {
       step(ks, bx0, bx1);
       step(ks + 1, bx1, bx0);
     }
+    cur = nextc;
 
     // epilogue: rows (phase p, ci) x this wave's 32 super-pixel columns
     float* scr = reinterpret_cast<float*>(lds) + wave * 32 * 36;  // [32][36] per wave
