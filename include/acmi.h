@@ -106,14 +106,15 @@ typedef struct acmi_net {
                             caller re-prepares after every parameter change) */
 } acmi_net_t;
 
-/* The forward's conv tower (bf16x3 mode) and the backward's conv2 input
- * gradient (acmi_backward, acmi_kfac_output_stats) read their weights as
- * pre-split bf16 MFMA fragments when net->conv_prep is set: acmi_conv_prepare
- * writes them (stream-ordered, two small kernels) -- once per parameter
- * version, not per rollout step or update.  With conv_prep == NULL the tower
- * splits the weights itself and the conv2 input gradient runs on the generic
- * split-per-block GEMM (same results, bit for bit; the sampled-loss chain then
- * stores its conv1-output gradient and reduces its G factor separately). */
+/* The forward's conv tower (bf16x3 mode), fc4 at rollout batches (split-K
+ * slabs with a forward workspace) and the backward's conv2 input gradient
+ * (acmi_backward, acmi_kfac_output_stats) read their weights as pre-split bf16
+ * MFMA fragments when net->conv_prep is set: acmi_conv_prepare writes them
+ * (stream-ordered, three small kernels) -- once per parameter version, not per
+ * rollout step or update.  With conv_prep == NULL the tower splits the weights
+ * itself and fc4 / the conv2 input gradient run on the generic split-per-block
+ * GEMM (same results, bit for bit; the sampled-loss chain then stores its
+ * conv1-output gradient and reduces its G factor separately). */
 int64_t acmi_conv_prep_bytes(int conv3_filters);
 int acmi_conv_prepare(const acmi_net_t* net, void* conv_prep, acmi_stream_t stream);
 
