@@ -34,14 +34,18 @@ BF16_MFMA_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA: 256 CUs x 4 SIMDs x 1024 FLOP
 # f32-equivalent ceiling of that arithmetic is the bf16 peak / 6
 X3_F32EQ_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
 HBM_PEAK_GBS = 8000.0
+PMC_PACKAGE = 'r02_final'  # profiles/<this>/: the current measurement package
 
 
 def measured_traffic(kernel, workload):
-    """HBM bytes per launch of the roofline kernel from the newest committed PMC
-    summary (profiles/*/pmc_traffic.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE,
-    separate passes) when it was measured on this kernel and workload; else None."""
+    """HBM bytes per launch of the roofline kernel from the committed PMC summary
+    of the current measurement package (PMC_PACKAGE; else any other
+    profiles/*/pmc_traffic.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate
+    passes) when it was measured on this kernel and workload; else None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*', 'pmc_traffic.json')), reverse=True):
+    first = os.path.join(ROOT, 'profiles', PMC_PACKAGE, 'pmc_traffic.json')
+    rest = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*', 'pmc_traffic.json')), reverse=True)
+    for path in [first] + [p for p in rest if p != first]:
         try:
             with open(path) as f:
                 d = json.load(f)
