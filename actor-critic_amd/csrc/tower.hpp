@@ -180,11 +180,15 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
 
   // ---- conv1: [84][84][4] u8 -> a1 [20][20][32] -------------------------------
   {
-    const int nt = wave == 0 ? 4 : 3;  // row tiles wave, wave+4, ... of 13
+    // row tiles w, w+4, ... of 13: logical wave w = 0 takes four.  Odd blocks
+    // rotate the roles by two, so the two blocks of a CU put their four-tile
+    // wave on different SIMDs (the per-SIMD conv1 load 4+3 instead of 4+4)
+    const int w = (wave + 2 * (blockIdx.x & 1)) & 3;
+    const int nt = w == 0 ? 4 : 3;
     int abase[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int p = min(32 * (wave + 4 * u) + col, 399);
+      const int p = min(32 * (w + 4 * u) + col, 399);
       const int oh = p / 20, ow = p - oh * 20;
       abase[u] = (4 * oh * 84 + 4 * ow) * 4 + 8 * kh8;
     }
@@ -220,7 +224,7 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
       if (u >= nt) break;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int p = 32 * (wave + 4 * u) + tow_row(r, lane);
+        const int p = 32 * (w + 4 * u) + tow_row(r, lane);
         if (p < 400) {
           const float v = fmaxf(__builtin_fmaf(acc[u][r], 1.0f / 255.0f, bias), 0.f);
           const int x = p % 20;
