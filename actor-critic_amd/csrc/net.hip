@@ -217,19 +217,26 @@ __global__ __launch_bounds__(256) void rollout_tail_kernel(
   __shared__ float sl[kMaxHeads];
   __shared__ int s_action;
   float* x = a4 + (long long)row * a4_stride;
-  for (int j = threadIdx.x; j < 512; j += 256) {
-    float v;
-    if (NZ > 0) {
-      const long long zs = (long long)(B + 1) * 512;
+  if (NZ > 0) {
+    // both columns' NZ slab loads issued before the (fixed-order) sums
+    const long long zs = (long long)(B + 1) * 512;
+    float pv[2][NZ > 0 ? NZ : 1];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int z = 0; z < NZ; ++z) pv[h][z] = part[z * zs + (long long)row * 512 + threadIdx.x + 256 * h];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = threadIdx.x + 256 * h;
       float acc = 0.f;
 #pragma unroll
-      for (int z = 0; z < NZ; ++z) acc += part[z * zs + (long long)row * 512 + j];
-      v = fmaxf(acc + b4[j], 0.f);
+      for (int z = 0; z < NZ; ++z) acc += pv[h][z];
+      const float v = fmaxf(acc + b4[j], 0.f);
       x[j] = v;
-    } else {
-      v = x[j];
+      sx[j] = v;
     }
-    sx[j] = v;
+  } else {
+    for (int j = threadIdx.x; j < 512; j += 256) sx[j] = x[j];
   }
   __syncthreads();
   float xv[8];
