@@ -1,4 +1,4 @@
-// fc4 at the rollout batch (envs/atari/model.py:197-201 -> nn.py:88-107 at
+// fc4 at the rollout batch (envs/atari/model.py:200-204 -> nn.py:37-52 at
 // B = N images): the split-K partial slabs [nz][B+1][512] that
 // rollout_tail_kernel / heads_kernel reduce, computed without LDS.
 //
