@@ -17,7 +17,8 @@
 // conv3 bf16x3 on both operands (mfma_x3, symred3.hpp) -- f32-accurate.  The
 // a1 / a2 LDS images use convfwd3.hpp's 16-byte chunk swizzle by pixel x, so
 // the lanes of a fragment read (consecutive output columns) hit distinct banks.
-// Work per block: conv1 13 row tiles dealt 4/3/3/3 to the waves; conv2 the 3x2
+// Work per block: conv1 three row tiles per wave + the 13th by K halves on two
+// waves (roles rotated by block parity: equal per-SIMD load); conv2 the 3x2
 // tiles as one full tile + half the K of row tile 2 per wave (the halves summed
 // in wave order through LDS); conv3 (C3 = 32) two row tiles x two K halves.
 // Activations are also written to global memory (strided rows, like EpiAct) for
@@ -31,7 +32,9 @@ namespace acmi {
 
 constexpr int kTowObs = 84 * 84 * 4;       // u8 image, later a2 [81][64] f32 + scratch
 constexpr int kTowA1 = 400 * 32 * 4;       // a1 [400][32] f32
-constexpr int kTowLds = kTowObs + kTowA1;  // 79,424 B: two blocks per CU
+constexpr int kTowLds = kTowObs + kTowA1;  // 79,424 B
+constexpr int kTowScr = 16 * 32 * 4;       // conv1's 13th row tile, second K half
+static_assert(2 * (kTowLds + kTowScr) <= 160 * 1024, "two blocks per CU");
 static_assert(81 * 64 * 4 + 2 * 17 * 32 * 4 <= kTowObs, "a2 + conv2 scratch fit the image region");
 
 // byte offset of 16-byte channel chunk `ch` of pixel p (x = its column) in an
@@ -160,7 +163,7 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
                   const float* w2, const float* b2, const float* w3, const float* b3, float* a1g,
                   float* a2g, float* a3g, long long st, const char* prep) {
   using P = TowerPrep<C3>;
-  __shared__ __attribute__((aligned(16))) char lds[kTowLds];
+  __shared__ __attribute__((aligned(16))) char lds[kTowLds + kTowScr];
   char* const imgL = lds;           // u8 image; later a2
   char* const a1L = lds + kTowObs;  // a1; later conv3 scratch
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -180,15 +183,16 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
 
   // ---- conv1: [84][84][4] u8 -> a1 [20][20][32] -------------------------------
   {
-    // row tiles w, w+4, ... of 13: logical wave w = 0 takes four.  Odd blocks
-    // rotate the roles by two, so the two blocks of a CU put their four-tile
-    // wave on different SIMDs (the per-SIMD conv1 load 4+3 instead of 4+4)
+    // row tiles w, w+4, w+8 of 13 for logical wave w; the 13th tile (rows
+    // 384-399) by K halves on waves 2 (k-steps 0-7) and 3 (8-15), added through
+    // LDS.  Odd blocks rotate the roles by two, so the two blocks of a CU give
+    // every SIMD the same conv1 load: 3 + 3.5 tiles.
     const int w = (wave + 2 * (blockIdx.x & 1)) & 3;
-    const int nt = w == 0 ? 4 : 3;
+    auto tile_of = [&](int u) { return u < 3 ? w + 4 * u : 12; };
     int abase[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int p = min(32 * (w + 4 * u) + col, 399);
+      const int p = min(32 * tile_of(u) + col, 399);
       const int oh = p / 20, ow = p - oh * 20;
       abase[u] = (4 * oh * 84 + 4 * ow) * 4 + 8 * kh8;
     }
@@ -208,7 +212,7 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
       const int koff = (s >> 1) * 336 + 16 * (s & 1);  // kernel row kh = s/2, kw half
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (u >= nt) break;
+        if (u == 3 && (w < 2 || (s >> 3) != w - 2)) continue;
         const bf16x8 a = u8x8_to_bf16(*reinterpret_cast<const uint2*>(imgL + abase[u] + koff));
         if constexpr (!BF16) {
           acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[2], acc[u], 0, 0, 0);
@@ -219,18 +223,27 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
     }
     const float bias = b1[col];
     float* g = a1g + img * st * 12800;
+    auto emit1 = [&](int p, float v) {
+      v = fmaxf(__builtin_fmaf(v, 1.0f / 255.0f, bias), 0.f);
+      *reinterpret_cast<float*>(a1L + tow_pos<32, 2>(p, p % 20, col >> 2) + 4 * (col & 3)) = v;
+      g[p * 32 + col] = v;
+    };
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (u >= nt) break;
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) emit1(32 * tile_of(u) + tow_row(r, lane), acc[u][r]);  // rows < 384
+    float* scr12 = reinterpret_cast<float*>(lds + kTowLds);  // [16 rows][32]
+    if (w == 3) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (tow_row(r, lane) < 16) scr12[tow_row(r, lane) * 32 + col] = acc[3][r];
+    }
+    __syncthreads();
+    if (w == 2) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int p = 32 * (w + 4 * u) + tow_row(r, lane);
-        if (p < 400) {
-          const float v = fmaxf(__builtin_fmaf(acc[u][r], 1.0f / 255.0f, bias), 0.f);
-          const int x = p % 20;
-          *reinterpret_cast<float*>(a1L + tow_pos<32, 2>(p, x, col >> 2) + 4 * (col & 3)) = v;
-          g[p * 32 + col] = v;
-        }
+        const int m = tow_row(r, lane);
+        if (m < 16) emit1(384 + m, acc[3][r] + scr12[m * 32 + col]);
       }
     }
   }
