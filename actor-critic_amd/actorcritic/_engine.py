@@ -7,6 +7,7 @@ size, and the update workspaces.  Every arithmetic call goes through libacmi.so.
 
 import ctypes
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -204,15 +205,24 @@ class NetEngine(object):
     def register_rollout(self, obs, fwd_out):
         """Marks `obs` ([N,T,84,84,4] device buffer) as already forwarded with the current
         parameters: the update re-uses the rollout activations instead of recomputing the
-        tower on identical (params, obs) (DESIGN.md §Rollout/update fusion)."""
-        self._rollout_cache = (obs.data_ptr(), tuple(obs.shape), self.version, fwd_out)
+        tower on identical (params, obs) (DESIGN.md §Rollout/update fusion).
+
+        The key holds a weak reference to `obs`: once the registered tensor is freed
+        (a copy_batches clone the caller dropped), its address may be handed to a
+        different tensor of the same shape by the caching allocator, so the entry dies
+        with it instead of matching that tensor."""
+        self._rollout_cache = (weakref.ref(obs), obs.data_ptr(), tuple(obs.shape), self.version, fwd_out)
 
     def lookup_rollout(self, x):
         c = self._rollout_cache
         if c is None or not isinstance(x, torch.Tensor) or not x.is_cuda:
             return None
-        if x.data_ptr() == c[0] and tuple(x.shape) == c[1] and c[2] == self.version:
-            return c[3]
+        ref = c[0]()
+        if ref is None:  # the registered buffer is gone: its address means nothing now
+            self._rollout_cache = None
+            return None
+        if x.data_ptr() == c[1] and tuple(x.shape) == c[2] and c[3] == self.version:
+            return c[4]
         return None
 
     def backward(self, fwd, st, with_stats):

@@ -11,6 +11,7 @@
 
 import concurrent.futures
 import multiprocessing
+import pickle
 
 
 class _AutoResetWrapper(object):
@@ -177,7 +178,19 @@ class SubprocessEnv(object):
         """Starts the child process (does not block)."""
         self._check_closed()
         if not self._started:
-            self._process.start()
+            try:
+                self._process.start()
+            except (pickle.PicklingError, AttributeError, TypeError) as e:
+                if self._ctx.get_start_method() == 'fork':
+                    raise
+                # the reference forks (multi_env.py:140-160), so a lambda or closure
+                # env_fn worked there; under 'spawn' it has to cross a pickle
+                raise ValueError(
+                    "env_fn {!r} cannot be sent to a '{}' child process ({}: {}). Pass a picklable "
+                    "env_fn -- a module-level function or a functools.partial of one -- or "
+                    "SubprocessEnv(env_fn, context='fork') / create_subprocess_envs(env_fns, "
+                    "context='fork') from a parent that has not initialised the GPU."
+                    .format(self._env_fn, self._ctx.get_start_method(), type(e).__name__, e)) from e
             self._child_connection.close()
             self._started = True
 

@@ -75,9 +75,10 @@ struct BandDev {
   BandGroup* groups = nullptr;
   int* tabs = nullptr;  // pairs | atab | wtab | ctab | dtab
   int o_pairs = 0, o_atab = 0, o_wtab = 0, o_ctab = 0, o_dtab = 0;
+  std::vector<int> host_tabs;  // source of the stream-ordered upload
 };
 
-inline const BandDev* band_dev(int H, int W, int C, int KH, int KW, int S, int CO) {
+inline const BandDev* band_dev(int H, int W, int C, int KH, int KW, int S, int CO, hipStream_t s) {
   const BandPlan* p = band_host_plan(H, W, C, KH, KW, S, CO);
   int dev = 0;
   if (!p || hipGetDevice(&dev) != hipSuccess) return nullptr;
@@ -101,10 +102,17 @@ inline const BandDev* band_dev(int H, int W, int C, int KH, int KW, int S, int C
   d->o_ctab = put(p->ctab);
   d->o_dtab = put(p->dtab);
   const size_t gb = p->groups.size() * sizeof(BandGroup), tb = tabs.size() * sizeof(int);
+  // the upload is ordered on the caller's stream (no null-stream serialisation);
+  // the host copies it reads must outlive it: the plan's groups are cached for the
+  // process, the tables are staged into a host buffer kept beside the plan
+  d->host_tabs = std::move(tabs);
   if (hipMalloc(&d->groups, gb) != hipSuccess || hipMalloc(&d->tabs, tb) != hipSuccess ||
-      hipMemcpy(d->groups, p->groups.data(), gb, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(d->tabs, tabs.data(), tb, hipMemcpyHostToDevice) != hipSuccess) {
-    delete d;  // (a failed allocation is retried at the next call)
+      hipMemcpyAsync(d->groups, p->groups.data(), gb, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d->tabs, d->host_tabs.data(), tb, hipMemcpyHostToDevice, s) != hipSuccess) {
+    // a failed allocation or copy is retried at the next call: release what was taken
+    if (d->groups) (void)hipFree(d->groups);
+    if (d->tabs) (void)hipFree(d->tabs);
+    delete d;
     return nullptr;
   }
   cache[key] = d;
@@ -241,7 +249,7 @@ __global__ __launch_bounds__(256) void band_fold_kernel(BandFold f) {
 inline int band_layer(const float* X, int H, int W, int C, int KH, int KW, int S, const float* dy,
                       int CO, int M, float* ws, long long ws_cap, float* grad, float* astat,
                       float wscale, hipStream_t s, int site = 0) {
-  const BandDev* d = band_dev(H, W, C, KH, KW, S, CO);
+  const BandDev* d = band_dev(H, W, C, KH, KW, S, CO, s);
   ACMI_REQUIRE(d, ACMI_ERR_ARG, "band plan unavailable for %dx%dx%d k%dx%d s%d -> %d", H, W, C, KH, KW, S,
                CO);
   const BandPlan& p = *d->plan;

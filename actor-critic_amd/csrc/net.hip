@@ -400,7 +400,10 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // act_img_stride: images between consecutive batch rows in the activation
   // buffers (1 = contiguous; T = rollout step t of an env-major buffer).
   const long long st = act_img_stride;
-  if (g_gemm_mode == ACMI_GEMM_X3 && tower_on() && (uintptr_t)obs % 16 == 0 && img_stride % 16 == 0) {
+  const bool tower = g_gemm_mode == ACMI_GEMM_X3 && tower_on() && (uintptr_t)obs % 16 == 0 && img_stride % 16 == 0;
+  ACMI_REQUIRE(tower || g_forward_mode == ACMI_FWD_F32, ACMI_ERR_ARG,
+               "bf16 forward needs the fused tower: 16-byte aligned observations and image stride");
+  if (tower) {
     // the three convs fused per image (16-byte image loads)
     prof_begin(ACMI_PROF_CONV1_FWD, s);
     launch_tower<C3>(obs, img_stride, B, P, L.off, a->a1, a->a2, a->a3, st, prep, s,
@@ -610,7 +613,7 @@ __global__ __launch_bounds__(256) void finalize_afactor_kernel(WgradDesc d, int 
     float v = 0.f;
     if (a < K1 && b < K1 && a <= b) {
       if (a == K) {
-        v = 1.0f;  // rows / rows
+        v = (float)d.rows * inv;  // rows * fl(1/rows), as finalize_wgrad_kernel (1 - 2^-24 for some rows)
       } else {
         const float* p = b < K ? d.part + (long long)a * d.J + b : d.part + (long long)d.I * d.J + a;
         float s = 0.f;
@@ -1276,6 +1279,8 @@ int acmi_abi_version(void) { return ACMI_ABI_VERSION; }
 int acmi_set_gemm_mode(int mode) {
   ACMI_REQUIRE(mode == ACMI_GEMM_F32 || mode == ACMI_GEMM_X3, ACMI_ERR_ARG,
                "acmi_set_gemm_mode: unknown mode %d", mode);
+  ACMI_REQUIRE(mode == ACMI_GEMM_X3 || g_forward_mode == ACMI_FWD_F32, ACMI_ERR_ARG,
+               "acmi_set_gemm_mode: f32 gemm mode has no bf16 forward (acmi_set_forward_mode(ACMI_FWD_F32) first)");
   g_gemm_mode = mode;
   return ACMI_OK;
 }
@@ -1284,6 +1289,10 @@ int acmi_get_gemm_mode(void) { return g_gemm_mode; }
 int acmi_set_forward_mode(int mode) {
   ACMI_REQUIRE(mode == ACMI_FWD_F32 || mode == ACMI_FWD_BF16, ACMI_ERR_ARG, "acmi_set_forward_mode: bad mode %d",
                mode);
+  // the bf16 arithmetic exists only in the fused tower (tower.hpp): refuse a mode
+  // the forward could not honour instead of silently computing in f32
+  ACMI_REQUIRE(mode == ACMI_FWD_F32 || (g_gemm_mode == ACMI_GEMM_X3 && tower_on()), ACMI_ERR_ARG,
+               "acmi_set_forward_mode: bf16 forward needs the fused tower (x3 gemm mode, ACMI_TOWER=1)");
   g_forward_mode = mode;
   return ACMI_OK;
 }

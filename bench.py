@@ -12,6 +12,12 @@ shard of BASELINE.json configs[3]).
 
   python bench.py --gpus N --steps K --warmup W
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Without torchrun's environment, ``--gpus N > 1`` launches the N ranks itself: the
+parent never touches the GPU, it spawns N fresh interpreters (one per GPU, RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_* set as torchrun would), each pins its device and
+joins the process group (nccl = RCCL; ACMI_DIST_BACKEND=gloo rehearses N ranks on one
+GPU), and rank 0 prints the one JSON line.
 """
 
 import argparse
@@ -74,8 +80,58 @@ def parse():
     return p.parse_args()
 
 
+def _free_port():
+    import socket
+    sk = socket.socket()
+    sk.bind(('127.0.0.1', 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def _rank_main(rank, world, port, argv):
+    """One self-launched rank: torchrun's environment, then the ordinary run."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    sys.argv = [sys.argv[0]] + list(argv)
+    run(parse())
+
+
+def launch(args):
+    """--gpus N without WORLD_SIZE: N spawned ranks (the parent stays off the GPU);
+    a failed rank takes the others down and its exit code is returned."""
+    import multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, args.gpus, port, sys.argv[1:]), name='bench-rank{}'.format(r))
+             for r in range(args.gpus)]
+    for p in procs:
+        p.start()
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            p.join(0.2)
+            if p.exitcode is None:
+                continue
+            alive.remove(p)
+            if p.exitcode != 0 and rc == 0:
+                rc = p.exitcode if p.exitcode > 0 else 128 - p.exitcode
+                print('bench: {} exited with {}; stopping the other ranks'.format(p.name, p.exitcode),
+                      file=sys.stderr)
+                for q in alive:
+                    q.terminate()
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(launch(args))
+    run(args)
+
+
+def run(args):
     from actorcritic import _lib, parallel
     from actorcritic import session as sess
     from actorcritic.agents import MultiEnvAgent
@@ -90,8 +146,9 @@ def main():
     if args.forward is not None:
         _lib.call('acmi_set_forward_mode', _lib.FWD_BF16 if args.forward == 'bf16' else _lib.FWD_F32)
     args.forward = 'bf16' if _lib.load().acmi_get_forward_mode() == _lib.FWD_BF16 else 'f32'
-    if world != args.gpus and rank == 0:
-        print('warning: --gpus {} but WORLD_SIZE {}'.format(args.gpus, world), file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit('bench: --gpus {} but the process group has {} ranks (WORLD_SIZE={})'.format(
+            args.gpus, world, os.environ.get('WORLD_SIZE')))
     dev = torch.device('cuda', torch.cuda.current_device())
     acktr = args.algo == 'acktr'
     N = args.envs_per_gpu

@@ -151,11 +151,33 @@ def golden_agent_layout():
     agent = mod.MultiEnvAgent(env, model, 4)
     first = agent.interact(None)
     second = agent.interact(None)
+
+    # SingleEnvAgent (agents.py:50-131): one env, [[obs]]-shaped sample batches,
+    # [1, steps] outputs, next observation kept between calls (no auto-reset)
+    class FakeEnv:
+        def __init__(self):
+            self.t, self.resets = 0, 0
+
+        def reset(self):
+            self.resets += 1
+            return 'obs(r{},t{})'.format(self.resets, self.t)
+
+        def step(self, action):
+            self.t += 1
+            return 'obs(r{},t{})'.format(self.resets, self.t), 0.5 * action, action % 2 == 1, {'t': self.t}
+
+    single_model = FakeModel()
+    single = mod.SingleEnvAgent(FakeEnv(), single_model, 3)
+    s_first = single.interact(None)
+    s_second = single.interact(None)
     out = dict(
         transpose_list=mod.transpose_list([[1, 2, 3, 4], [5, 6, 7, 8], [9, 10, 11, 12]]),
         sample_batches=model.batches,
         first=[list(x) for x in first],
         second=[list(x) for x in second],
+        single_sample_batches=single_model.batches,
+        single_first=[list(x) for x in s_first],
+        single_second=[list(x) for x in s_second],
     )
     with open(os.path.join(OUT, 'agent_layout.json'), 'w') as f:
         json.dump(out, f, indent=1)

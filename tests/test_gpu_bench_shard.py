@@ -1,0 +1,189 @@
+"""The update statistics at the bench shard's own size against float64.
+
+BASELINE configs[3] runs 512 envs x 20 steps per GPU: acmi_backward and
+acmi_kfac_output_stats see M = 10240 image rows, the size at which the production
+plans engage -- the band reduction's 4-chunk, 243-group conv2 plan (band.hpp,
+bandplan.hpp), conv2's input gradient on pre-split weights (convt2.hpp) with the
+conv1 G factor fused into the sampled chain, the role-split conv1 A-factor kernel over
+many i8 chunks, the six-slab fc4 plan.  Every parameter-gradient block, all five A
+factors and all six G factors of one backward + sampled-loss backward are compared
+with a float64 computation of the same formulas on the GPU (torch.float64 GEMMs,
+chunked over images): the reference's conv layers as patch products
+(envs/atari/model.py:173-217, nn.py:88-126), kfac's factors as the DESIGN.md section 4
+conventions (rows = every conv location of every image, homogeneous coordinate last,
+G from the sampled head gradients of oracle.sampled_head_grads).
+
+Tolerances (max-abs error over max-abs value, per block): gradients and A factors
+2e-5, G factors 5e-5 -- the section 5 bounds of the small-size tests.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from actorcritic import _lib
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), 'oracle'))
+import oracle  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _patches(x, k, s):
+    """[B,H,W,C] -> rows (img, oh, ow), columns (kh, kw, c) (extract_image_patches order)."""
+    p = x.unfold(1, k, s).unfold(2, k, s)  # B, OH, OW, C, KH, KW
+    return p.permute(0, 1, 2, 4, 5, 3).reshape(-1, k * k * x.shape[-1])
+
+
+def _conv_input_grad(dy, w, s, in_shape):
+    k, _, cin, co = w.shape
+    B, OH, OW, _ = dy.shape
+    dp = (dy.reshape(-1, co) @ w.reshape(-1, co).t()).reshape(B, OH, OW, k, k, cin)
+    dx = torch.zeros(in_shape, dtype=dy.dtype, device=dy.device)
+    for kh in range(k):
+        for kw in range(k):
+            dx[:, kh:kh + s * (OH - 1) + 1:s, kw:kw + s * (OW - 1) + 1:s, :] += dp[:, :, :, kh, kw, :]
+    return dx
+
+
+class _Ref64(object):
+    """float64 sums of grads, A factors and G factors over image chunks."""
+
+    def __init__(self, blocks, A, C3, dev):
+        self.w = [b.double() for b in blocks]
+        self.A, self.C3, self.dev = A, C3, dev
+        self.grad = None
+        self.afac = [0.0] * 5
+        self.gfac = [0.0] * 6
+        self.rows = [0] * 6
+
+    def _forward(self, obs):
+        w1, b1, w2, b2, w3, b3, w4, b4, wp, bp, wv, bv = self.w
+        x = obs.double() / 255.0
+        p1 = _patches(x, 8, 4)
+        a1 = torch.relu(p1 @ w1.reshape(-1, 32) + b1).reshape(-1, 20, 20, 32)
+        p2 = _patches(a1, 4, 2)
+        a2 = torch.relu(p2 @ w2.reshape(-1, 64) + b2).reshape(-1, 9, 9, 64)
+        p3 = _patches(a2, 3, 1)
+        a3 = torch.relu(p3 @ w3.reshape(-1, self.C3) + b3).reshape(-1, 7, 7, self.C3)
+        a3f = a3.reshape(a3.shape[0], -1)
+        a4 = torch.relu(a3f @ w4 + b4)
+        return [p1, p2, p3, a3f, a4], (a1, a2, a3, a4)
+
+    def _chain(self, masks, dlogits, dvalue):
+        w1, b1, w2, b2, w3, b3, w4, b4, wp, bp, wv, bv = self.w
+        m1, m2, m3, m4 = masks
+        d4 = (dlogits @ wp.t() + dvalue[:, None] * wv[:, 0][None, :]) * m4
+        d3 = (d4 @ w4.t()).reshape(m3.shape) * m3
+        d2 = _conv_input_grad(d3, w3, 1, m2.shape) * m2
+        d1 = _conv_input_grad(d2, w2, 2, m1.shape) * m1
+        return [d1.reshape(-1, 32), d2.reshape(-1, 64), d3.reshape(-1, self.C3), d4, dlogits, dvalue[:, None]]
+
+    def add(self, obs, gpu_acts, dlogits, dvalue, g_pi, g_v):
+        """gpu_acts: the kernel forward's f32 a1..a4 of these images, whose ReLU
+        masks the chains use: a pre-activation within f32 rounding of 0 may have
+        the other sign in float64, and at 10240 rows such flips (one whole term of
+        a cancelling sum each) would dominate the comparison of the backward's
+        arithmetic.  The forward itself is compared with float64 elsewhere."""
+        ins, _ = self._forward(obs)
+        ins = ins + [ins[4]]
+        masks = [(a > 0).double() for a in gpu_acts]
+        douts = self._chain(masks, dlogits, dvalue)
+        gouts = self._chain(masks, g_pi, g_v)
+        blocks = []
+        for l in range(6):
+            xin = torch.cat([ins[l], torch.ones(ins[l].shape[0], 1, dtype=torch.float64, device=self.dev)], 1)
+            blocks.append((xin.t() @ douts[l]).reshape(-1))
+            if l < 5:
+                self.afac[l] = self.afac[l] + xin.t() @ xin
+            self.gfac[l] = self.gfac[l] + gouts[l].t() @ gouts[l]
+            self.rows[l] += xin.shape[0]
+        g = torch.cat(blocks)
+        self.grad = g if self.grad is None else self.grad + g
+
+    def result(self):
+        return (self.grad, [a / r for a, r in zip(self.afac, self.rows)],
+                [g / r for g, r in zip(self.gfac, self.rows)])
+
+
+def _rel(got, ref):
+    return ((got.double() - ref).abs().max() / ref.abs().max()).item()
+
+
+def test_update_statistics_at_bench_shard_match_float64(lib, cuda):
+    """One acmi_backward (loss gradients + A factors) and one acmi_kfac_output_stats
+    (G factors of the sampled losses) over M = 512 x 20 = 10240 images -- the
+    BASELINE configs[3] per-GPU shard, default arithmetic (bf16x3, band reductions,
+    pre-split weights) -- against float64 on the GPU."""
+    from actorcritic._engine import Layout
+    A, C3, B = 4, 32, 512 * 20
+    L = Layout(A, C3)
+    params = torch.from_numpy(L.init_params(seed=7)).to(cuda)
+    gen = torch.Generator(device=cuda).manual_seed(2024)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=gen, device=cuda, dtype=torch.uint8)
+    info = (ctypes.c_int64 * 5)()
+    _lib.call('acmi_band_info', 1, C3, B, info)
+    assert info[2] == 4 and info[1] == 243, list(info)  # the production plan of the bench shard
+    z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=cuda)
+    t = dict(a1=z(B, 20, 20, 32), a2=z(B, 9, 9, 64), a3=z(B, 7, 7, C3), a4=z(B, 512), logits=z(B, A), value=z(B))
+    acts = _lib.Acts(*[t[k].data_ptr() for k in ('a1', 'a2', 'a3', 'a4', 'logits', 'value')], A)
+    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
+    net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr())
+    st = _lib.stream_handle()
+    _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), st)
+    _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1, st)
+    # head gradients shaped like the A2C loss's (a2c_loss: mean over M rows)
+    ldh = 8
+    dhead = z(B, ldh)
+    dhead[:, :A + 1] = torch.randn(B, A + 1, generator=gen, device=cuda) / B
+    din = (ctypes.c_int64 * 6)()
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, din, None, so, ctypes.byref(tot))
+    ws = z(int(lib.acmi_backward_ws_floats(B, A, C3)))
+    d = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
+    bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
+    grads, astat, gstat = z(params.numel()), z(tot.value), z(tot.value)
+    _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
+              ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), st)
+    ds = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
+    dhead_s = z(B, ldh)  # the sampled chain writes its own head gradients here
+    bwd_s = _lib.Bwd(*[x.data_ptr() for x in ds], dhead_s.data_ptr(), ldh)
+    seed, counter = 0x4b464143, 41
+    _lib.call('acmi_kfac_output_stats', ctypes.byref(net), B, ctypes.byref(acts), ctypes.byref(bwd_s), seed, 0,
+              counter, _lib.ptr(gstat), _lib.ptr(ws), st)
+    torch.cuda.synchronize()
+    assert torch.isfinite(grads).all() and torch.isfinite(astat).all() and torch.isfinite(gstat).all()
+
+    # the sampled head gradients from the kernel's own f32 logits and counters
+    g_pi, g_v, _ = oracle.sampled_head_grads(t['logits'].cpu().numpy(), seed, 0, counter)
+    g_pi = torch.from_numpy(np.asarray(g_pi, np.float64)).to(cuda)
+    g_v = torch.from_numpy(np.asarray(g_v, np.float64)).to(cuda)
+    ref = _Ref64(L.split(params), A, C3, cuda)
+    dh64 = dhead.double()
+    chunk = 1024
+    for i in range(0, B, chunk):
+        j = min(B, i + chunk)
+        ref.add(obs[i:j], [t[k][i:j] for k in ('a1', 'a2', 'a3', 'a4')], dh64[i:j, :A], dh64[i:j, A],
+                g_pi[i:j], g_v[i:j])
+    g_ref, a_ref, gf_ref = ref.result()
+
+    errs = {}
+    ends = L.offsets[1:] + [L.nparams]
+    for blk, (o, e) in enumerate(zip(L.offsets, ends)):
+        errs[('grad', blk)] = _rel(grads[o:e], g_ref[o:e])
+    for f in range(5):
+        n = din[f]
+        errs[('A', f)] = _rel(astat[so[f]:so[f] + n * n].reshape(n, n), a_ref[f])
+    for l in range(6):
+        n = gf_ref[l].shape[0]
+        errs[('G', l)] = _rel(gstat[so[5 + l]:so[5 + l] + n * n].reshape(n, n), gf_ref[l])
+    for k, v in errs.items():
+        print(k, '%.2e' % v)
+    for k, v in errs.items():
+        tol = 5e-5 if k[0] == 'G' else 2e-5
+        assert v < tol, (k, v)

@@ -130,3 +130,25 @@ def test_sharded_acktr_iteration_matches_full_batch(lib, cuda, tmp_path, gae, no
     step_s, step_f = shards[0]['step'].double(), full['step'].double()
     assert step_f.norm() > 0
     assert ((step_s - step_f).norm() / step_f.norm()).item() < 1e-3
+
+
+def test_bench_self_launches_ranks():
+    """`python bench.py --gpus 2` without torchrun's environment spawns the two ranks
+    itself (the parent stays off the GPU) and rank 0 prints one JSON line for the
+    whole job (n_gpus 2, dp2, global envs = 2 shards).  gloo on one card here; the
+    same launcher runs nccl (RCCL) ranks on a multi-GPU node."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, ACMI_DIST_BACKEND='gloo')
+    env.pop('WORLD_SIZE', None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--steps', '2', '--warmup', '1',
+                        '--envs-per-gpu', '16', '--no-cpu-baseline'], env=env, cwd=ROOT, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out['n_gpus'] == 2 and out['config']['parallelism'] == 'dp2'
+    assert out['config']['global_envs'] == 32 and out['config']['envs_per_gpu'] == 16
+    assert out['value'] > 0 and out['cpu_baseline'] is None

@@ -485,13 +485,15 @@ def test_convt2_matches_gemm3_path(lib, cuda, B):
     assert torch.equal(sa[so[6]:], sb[so[6]:])
 
 
-@pytest.mark.parametrize('A,C3', [(4, 32), (18, 64)])
-def test_bf16_forward_mode(lib, cuda, A, C3):
+@pytest.mark.parametrize('A,C3,B', [(4, 32, 29), (18, 64, 29), (18, 32, 1024)],
+                         ids=['breakout', 'full-actions-c64', 'configs4-shard-1024x18'])
+def test_bf16_forward_mode(lib, cuda, A, C3, B):
     """acmi_set_forward_mode(ACMI_FWD_BF16) (BASELINE configs[4] "bf16 forward"):
     the conv tower with one bf16 MFMA per product stays within bf16 accuracy of the
     float64 forward (max error <= 1e-2 of each tensor's range; measured ~2e-3), and
-    switching back restores the f32-accurate tower bit for bit."""
-    B = 29
+    switching back restores the f32-accurate tower bit for bit.  The last case is
+    the configs[4] shard itself: 1024 images per launch, the full 18-action set,
+    C3 = 32 (ACKTR)."""
     params = rand_params(A, C3, cuda, seed=31)
     obs = torch.randint(0, 256, (B, 84, 84, 4), generator=torch.Generator().manual_seed(32),
                         dtype=torch.uint8).to(cuda)

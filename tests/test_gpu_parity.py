@@ -301,11 +301,16 @@ def test_rollout_matches_oracle_env_and_tower(lib, cuda):
         np.testing.assert_array_equal(act[:, t].cpu().numpy(), oracle.sample_f32(lg[:, t], u))
 
 
-def test_acktr_update_matches_oracle(lib, cuda):
+@pytest.mark.parametrize('N,T', [(3, 5), (32, 20)], ids=['toy', 'configs2-32x20'])
+def test_acktr_update_matches_oracle(lib, cuda, N, T):
     """One steady-state ACKTR update at gs=40 (covariance update + inverse + apply)
-    against the float64 oracle on the same rollout."""
+    against the float64 oracle on the same rollout -- at a toy size and at the
+    reference's own ACKTR config, BASELINE configs[2] (32 envs x 20 steps, C3 = 32,
+    a2c_acktr.py:306-310, :51-53): A/G factors, the damped inverses, the
+    preconditioned gradients (north_star rel-L2 1e-3), the trust-region coefficient
+    and the parameter step."""
     from actorcritic import session as sess
-    N, T, A, C3 = 3, 5, 4, 32
+    A, C3 = 4, 32
     env, model, agent, obj, gs, opt, op, params = _build(N, T, A, C3)
     gs.assign(40)
     with sess.Session() as s:
@@ -339,6 +344,16 @@ def test_acktr_update_matches_oracle(lib, cuda):
         rel = np.abs(got - gfac[l]).max() / np.abs(gfac[l]).max()
         assert rel < 5e-5, ('G', l, rel)
     inv = oracle.damped_inverses(afac, gfac, 0.01)
+    # the damped inverses, each against the float64 inverse of the oracle's factors
+    # (their difference is the f32 factors' rounding seen through the damped
+    # condition number: the relative error is bounded by cond * 2e-5)
+    inv_got = st['inv']
+    for l in range(6):
+        for m, ref in ((2 * l, inv[l][0]), (2 * l + 1, inv[l][1])):
+            got = L.inverse_block(inv_got, m).cpu().numpy().astype(np.float64)
+            rel = np.abs(got - ref).max() / np.abs(ref).max()
+            print('inverse', l, m % 2, 'rel %.2e' % rel)
+            assert rel < 1e-3, ('inverse', l, m % 2, rel)
     new_p, vel, precon, coeff = oracle.kfac_step(p_before, np.zeros_like(p_before), grads, inv,
                                                  oracle.linear_decay(0.25, 0.025, 40, 1000), 0.9, 1e-4, A, C3)
     got_pre = st['precon'].cpu().numpy().astype(np.float64)
@@ -350,7 +365,7 @@ def test_acktr_update_matches_oracle(lib, cuda):
     assert gs.value == 41
 
 
-def test_cold_start_schedule_and_a2c_update(lib, cuda):
+def test_cold_start_schedule(lib, cuda):
     from actorcritic import session as sess
     env, model, agent, obj, gs, opt, op, params = _build(2, 3)
     flags = []
@@ -361,8 +376,14 @@ def test_cold_start_schedule_and_a2c_update(lib, cuda):
             flags.append(opt.last_flags)
     assert flags == [(True, False, False)] * 3 and gs.value == 6
     assert torch.isfinite(model.params).all()
-    # A2C: RMSProp + clip, one update vs the oracle
-    env, model, agent, obj, gs, opt, op, params = _build(2, 5, C3=64)
+
+
+@pytest.mark.parametrize('N', [2, 32], ids=['toy', 'configs1-32x5'])
+def test_a2c_update_matches_oracle(lib, cuda, N):
+    """A2C: RMSProp + clip 0.5, one update vs the float64 oracle -- at a toy size and
+    at BASELINE configs[1] (32 envs x 5 steps, C3 = 64, a2c_acktr.py:249-251)."""
+    from actorcritic import session as sess
+    env, model, agent, obj, gs, opt, op, params = _build(N, 5, C3=64)
     with sess.Session() as s:
         data = agent.interact(s)
         p0 = model.params.cpu().numpy().astype(np.float64)
@@ -447,3 +468,53 @@ def test_copy_batches_returns_fresh_tensors(lib, cuda):
             assert torch.equal(a, b)
         assert first[0].data_ptr() != second[0].data_ptr()
         assert model.engine.lookup_rollout(first[0]) is None  # superseded: recomputed if fed
+
+
+def test_select_max_actions_and_single_env_agent(lib, cuda):
+    """model.select_max_actions (model.py:153-169: session.run(policy.mode) on a
+    [batch, 1] feed) is the argmax of the float64 oracle's logits, and
+    SingleEnvAgent.interact (agents.py:50-131) steps one host env with
+    sample_actions([[obs]]): [1, steps] outputs whose observations, rewards and
+    terminals replay exactly through a second oracle env, and whose actions are the
+    oracle's inverse-CDF draws from the counter RNG of each step."""
+    from actorcritic import session as sess
+    from actorcritic.agents import SingleEnvAgent
+    env, model, agent, obj, gs, opt, op, params = _build(3, 4)
+    rng = np.random.default_rng(17)
+    B = 9
+    obs = rng.integers(0, 256, size=(B, 1, 84, 84, 4), dtype=np.uint8)
+    ref = oracle.forward(params, obs.reshape(B, 84, 84, 4), 4, 32)['logits']
+    with sess.Session() as s:
+        got = model.select_max_actions([list(o) for o in obs], s)
+    assert isinstance(got, list) and len(got) == B
+    top2 = np.sort(ref, axis=1)[:, -2:]
+    clear = (top2[:, 1] - top2[:, 0]) > 1e-4 * np.abs(ref).max()
+    assert clear.sum() >= B - 1
+    np.testing.assert_array_equal(np.asarray(got)[clear], ref.argmax(1)[clear])
+
+    T = 7
+    host_env = oracle.SyntheticAtari(5, 0)
+    single = SingleEnvAgent(host_env, model, T)
+    eng = model.engine
+    with sess.Session() as s:
+        c0 = eng.sample_counter
+        o, a, r, d, nxt, infos = single.interact(s)
+        c1 = eng.sample_counter
+        o2, a2, _, _, nxt2, _ = single.interact(s)
+    assert [len(x) for x in (o, a, r, d, infos)] == [1] * 5 and len(o[0]) == T and len(nxt) == 1
+    assert c1 - c0 == T
+    np.testing.assert_array_equal(o2[0][0], nxt[0])  # carried into the next call
+    replay = oracle.SyntheticAtari(5, 0)
+    np.testing.assert_array_equal(o[0][0], replay.reset())
+    logits = oracle.forward(params, np.stack(o[0]), 4, 32)['logits'].astype(np.float32)
+    for t in range(T):
+        u = oracle.sample_uniforms(3, 0, c0 + t, 1)
+        draw = int(oracle.sample_f32(logits[t:t + 1], u)[0])
+        # the GPU logits are f32 (1e-5 of the oracle's): a draw may differ only where
+        # the uniform sits on a CDF boundary
+        assert a[0][t] == draw, (t, a[0][t], draw)
+        ob, rr, dd, _ = replay.step(a[0][t])
+        assert rr == r[0][t] and dd == d[0][t]
+        if t + 1 < T:
+            np.testing.assert_array_equal(o[0][t + 1], ob)
+    np.testing.assert_array_equal(nxt[0], ob)

@@ -103,3 +103,11 @@ def test_multi_env_auto_reset_and_none_actions():
     obs, rew, term, infos = multi.step([0, 0])
     assert obs == [(1, 1), (0, 1)]
     multi.close()
+
+
+def test_unpicklable_env_fn_names_the_fix():
+    """A lambda env_fn (fine under the reference's fork) fails at start() under the
+    default spawn context with a ValueError that says what to pass instead."""
+    env = SubprocessEnv(lambda: CountingEnv())
+    with pytest.raises(ValueError, match="picklable env_fn.*functools.partial.*context='fork'"):
+        env.start()

@@ -124,6 +124,42 @@ def test_agent_layout_matches_reference(monkeypatch):
     assert json.loads(json.dumps(second)) == gold['second']
 
 
+def test_single_env_agent_matches_reference():
+    """SingleEnvAgent.interact (agents.py:50-131) against the reference class run on
+    the same fakes: [[obs]] sample batches, [1, steps] outputs, [next_obs], and the
+    last observation carried into the next call (no reset in between)."""
+    from actorcritic.agents import SingleEnvAgent
+    gold = json.load(open(os.path.join(GOLD, 'agent_layout.json')))
+
+    class FakeEnv:
+        def __init__(self):
+            self.t, self.resets = 0, 0
+
+        def reset(self):
+            self.resets += 1
+            return 'obs(r{},t{})'.format(self.resets, self.t)
+
+        def step(self, action):
+            self.t += 1
+            return 'obs(r{},t{})'.format(self.resets, self.t), 0.5 * action, action % 2 == 1, {'t': self.t}
+
+    class FakeModel:
+        def __init__(self):
+            self.batches = []
+
+        def sample_actions(self, batch, session):
+            self.batches.append(batch)
+            return [10 * i + len(self.batches) for i in range(len(batch))]
+
+    model = FakeModel()
+    agent = SingleEnvAgent(FakeEnv(), model, 3)
+    first = [list(x) for x in agent.interact(None)]
+    second = [list(x) for x in agent.interact(None)]
+    assert json.loads(json.dumps(model.batches)) == gold['single_sample_batches']
+    assert json.loads(json.dumps(first)) == gold['single_first']
+    assert json.loads(json.dumps(second)) == gold['single_second']
+
+
 def test_gae_lambda1_reduces_to_reference_targets():
     """GAE(lambda = 1) targets equal the reference's n-step targets (exact
     arithmetic; float32 differs by rounding of the telescoping V terms): pins the
