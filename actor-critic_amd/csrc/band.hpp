@@ -1,19 +1,40 @@
 // Pixel-pair ("band") conv weight gradient + K-FAC A factor (plan: bandplan.hpp).
 //
 // One conv layer's [P;1]^T [P | dY] over the M*L patch rows is computed as
-//   1. symred6_kernel over the DENSE rows [X | dY] of the M images (X the layer
+//   1. band_kernel over the DENSE rows [X | dY] of the M images (X the layer
 //      input [M][H*W*C], dY its output gradient [M][L*CO]): only the 64x64
-//      sub-tiles whose slabs share a patch, six slabs per block, bf16x3 split
-//      operands (f32-accurate, symred3.hpp), per-chunk partials in compact
-//      tile slots [chunk][tile][64][64] + column sums [chunk][ns*64];
+//      sub-tiles whose slabs share a patch, up to 8 staged slabs and 16 sub-tiles
+//      per work item, per-chunk partials in compact tile slots
+//      [chunk][tile][64][64] + column sums [chunk][ns*64];
 //   2. band_reduce_kernel: the chunks summed in chunk order (in place, chunk 0);
 //   3. band_fold_kernel: every output element sums its L pixel-pair entries in
 //      location order -- the A factor's upper triangle (written to both halves,
 //      so it is exactly symmetric), the homogeneous row/column, [dW; db].
-// Fixed summation orders throughout: deterministic, no atomics.
+// Fixed summation orders throughout: deterministic, no atomics on data.
 // Reference: kfac's conv input factor over extract_image_patches rows
 // (registration envs/atari/model.py:227-238) and tf.gradients' conv2d filter
 // gradient (objectives.py:78) -- the same sums, reassociated.
+//
+// Arithmetic: "f16x2" split operands.  Every f32 operand x of a slab is scaled
+// by a power of two s (one per tensor: X or dY) and split at the LDS commit into
+//   h = f16_rn(x s),  l = f16_rn(x s - h)        (the subtraction is exact)
+// so x s = h + l to 2^-22 relative, and each 32x32x16 tile takes the three
+// v_mfma_f32_32x32x16_f16 of l*h + h*l + h*h into one f32 accumulator (every
+// f16 x f16 product is exact in f32; the dropped l*l is <= 2^-22 |a||b|); the
+// tile is multiplied by 1/(s_a s_b) (exact) when it is stored.  The scales put
+// each tensor's bound at 2^14 < 65504: X from the layer's weights (a1, a2 are
+// ReLU outputs of [0,1] pixels, bounded by the positive weight mass,
+// band_bounds_kernel), dY from its exact max (band_absmax_kernel).  Elements far
+// below the bound lose relative precision only where their absolute error
+// (<= 2^-25 in scaled units) is < 2^-30 of the bound.  Three MFMAs per product
+// instead of bf16x3's six: the same f32-class sums (accumulation error,
+// ~sqrt(K) 2^-24, dominates the 2^-22 operand error) at twice the matrix rate.
+//
+// Work distribution: one 512-thread block per (group, chunk) item; block b runs
+// item b >> 3 of XCD b & 7's list.  A list holds the groups of one spatial region
+// of the image, chunk-major, so the blocks of one XCD stream the same image rows
+// over the columns of one region: the region's slabs are fetched into that XCD's
+// L2 once and re-read from there by the other groups of the region.
 #pragma once
 
 #include <map>
@@ -21,35 +42,13 @@
 #include <tuple>
 
 #include "bandplan.hpp"
-#include "symred3.hpp"
+#include "symred3.hpp"  // ds_tr16, stage_f4, zero_run
 
 namespace acmi {
 
 // launch-site profiling (net.hip)
 static void prof_begin(int site, hipStream_t s);
 static void prof_end(int site, hipStream_t s);
-
-struct BandPlanDev {
-  const BandGroup* g;
-  int ngroups;
-  int xcd_remap;  // 1: blocks XCD-contiguous (symred6's default map); 0: dispatch order
-};
-
-// ACMI_BAND_MAP=1: XCD-contiguous block map (each XCD's L2 sees neighbouring
-// groups); default 0: dispatch order, so all XCDs work on the same chunk of
-// images and its rows stay in the MALL while the groups re-read them
-inline int band_xcd_remap() {
-  static const int v = getenv("ACMI_BAND_MAP") ? atoi(getenv("ACMI_BAND_MAP")) : 0;
-  return v;
-}
-
-struct EpiBand {
-  float* part;  // [chunk][ntiles][64][64]
-  float* cs;    // [chunk][ncols]
-  int ntiles;
-  int ncols;
-  int z = 0;
-};
 
 // host plan per layer shape (no device needed: workspace sizing), and its
 // device copy per device (built on first use, kept for the process)
@@ -73,8 +72,9 @@ inline const BandPlan* band_host_plan(int H, int W, int C, int KH, int KW, int S
 struct BandDev {
   const BandPlan* plan = nullptr;
   BandGroup* groups = nullptr;
-  int* tabs = nullptr;  // pairs | atab | wtab | ctab | dtab
-  int o_pairs = 0, o_atab = 0, o_wtab = 0, o_ctab = 0, o_dtab = 0;
+  int* tabs = nullptr;  // pairs | atab | wtab | ctab | dtab | xlist
+  int o_pairs = 0, o_atab = 0, o_wtab = 0, o_ctab = 0, o_dtab = 0, o_xlist = 0;
+  int xoff[9] = {};
   std::vector<int> host_tabs;  // source of the stream-ordered upload
 };
 
@@ -101,10 +101,17 @@ inline const BandDev* band_dev(int H, int W, int C, int KH, int KW, int S, int C
   d->o_wtab = put(p->wtab);
   d->o_ctab = put(p->ctab);
   d->o_dtab = put(p->dtab);
+  std::vector<int> xl;
+  for (int x = 0; x < 8; ++x) {
+    d->xoff[x] = (int)xl.size();
+    xl.insert(xl.end(), p->xcd_groups[x].begin(), p->xcd_groups[x].end());
+  }
+  d->xoff[8] = (int)xl.size();
+  d->o_xlist = put(xl);
   const size_t gb = p->groups.size() * sizeof(BandGroup), tb = tabs.size() * sizeof(int);
   // the upload is ordered on the caller's stream (no null-stream serialisation);
-  // the host copies it reads must outlive it: the plan's groups are cached for the
-  // process, the tables are staged into a host buffer kept beside the plan
+  // the host copies it reads outlive it: the plan's groups are cached for the
+  // process, the tables are kept beside the device pointers
   d->host_tabs = std::move(tabs);
   if (hipMalloc(&d->groups, gb) != hipSuccess || hipMalloc(&d->tabs, tb) != hipSuccess ||
       hipMemcpyAsync(d->groups, p->groups.data(), gb, hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -120,11 +127,11 @@ inline const BandDev* band_dev(int H, int W, int C, int KH, int KW, int S, int C
 }
 
 // Chunks of the M image rows: ACMI_BAND_CHUNKS forces the count; by default
-// about four dynamic rounds of one-block-per-CU blocks (groups differ in their
-// tile counts, so many shorter blocks balance the CUs), chunks >= 512 rows.
+// about three items per CU over the whole grid (the groups differ in work, so
+// shorter items late in the grid fill the CUs), chunks >= 512 rows.
 inline void band_chunks(long long rows, int ngroups, int* nc, int* ch) {
   static const int forced = getenv("ACMI_BAND_CHUNKS") ? atoi(getenv("ACMI_BAND_CHUNKS")) : 0;
-  long long n = forced > 0 ? forced : std::max(1, (4 * 256 + ngroups / 2) / std::max(1, ngroups));
+  long long n = forced > 0 ? forced : std::max(1, (3 * 256 + ngroups / 2) / std::max(1, ngroups));
   n = std::max(1LL, std::min(n, rows / 512 > 0 ? rows / 512 : 1));
   long long c = (rows + n - 1) / n;
   c = (c + 15) / 16 * 16;
@@ -132,11 +139,350 @@ inline void band_chunks(long long rows, int ngroups, int* nc, int* ch) {
   *nc = (int)((rows + c - 1) / c);
 }
 
+// band scratch (floats, at the end of the backward's partial region): scales
+// [s_a1, s_a2, s_d2, s_d3], |d2| / |d3| max bits, the two layers' (s_X, s_dY)
+constexpr int kBandScratch = 64;
+enum { kBsA1 = 0, kBsA2 = 1, kBsD2 = 2, kBsD3 = 3, kBsMaxD2 = 4, kBsMaxD3 = 5, kBsQueue = 8,
+       kBsPairC3 = 16, kBsPairC2 = 18 };
+
 inline long long band_ws_floats(const BandPlan* p, long long rows) {
   if (!p) return 0;
   int nc, ch;
   band_chunks(rows, (int)p->groups.size(), &nc, &ch);
   return (long long)nc * ((long long)p->ntiles * 4096 + (long long)p->geom.ns * 64);
+}
+
+// ---------------------------------------------------------------------------
+// operand scales
+// ---------------------------------------------------------------------------
+// power of two putting max at < 2^14 (f16 max 65504); 1 for a zero / non-finite max
+__device__ __forceinline__ float band_scale_of(float mx) {
+  if (!(mx > 0.f) || !(mx < 3.0e38f)) return 1.f;
+  int e;
+  (void)frexpf(mx, &e);  // mx < 2^e
+  return ldexpf(1.f, 14 - e);
+}
+
+// |d2| and |d3| maxima (positive floats order as their bit patterns): float4
+// grid-stride loads, one atomicMax per block and tensor into the zeroed slots
+__global__ __launch_bounds__(256) void band_absmax_kernel(const float4* d2, long long n2, const float4* d3,
+                                                         long long n3, unsigned* out) {
+  __shared__ float red[2][4];
+  float m2 = 0.f, m3 = 0.f;
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n2; i += stride) {
+    const float4 v = d2[i];
+    m2 = fmaxf(m2, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n3; i += stride) {
+    const float4 v = d3[i];
+    m3 = fmaxf(m3, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  m2 = wave_max(m2);
+  m3 = wave_max(m3);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[0][w] = m2, red[1][w] = m3;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float a = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    const float b = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+    atomicMax(out, __float_as_uint(a));
+    atomicMax(out + 1, __float_as_uint(b));
+  }
+}
+
+// the X scales from the weights: a1 = relu(W1 x + b1) with x in [0, 1], so
+// a1[c] <= B1[c] = sum_k max(W1[k][c], 0) + max(b1[c], 0); a2 = relu(W2 a1 + b2)
+// with a1 >= 0, so a2[c'] <= sum_{k,c} max(W2[k][c][c'], 0) B1[c] + max(b2[c'], 0);
+// and the dY scales from the maxima of band_absmax_kernel.  One block.
+__global__ __launch_bounds__(256) void band_bounds_kernel(const float* w1, const float* b1, const float* w2,
+                                                         const float* b2, float* scr) {
+  __shared__ float part[8][64];
+  __shared__ float B1[32];
+  const int t = threadIdx.x;
+  {  // B1: 32 channels x 256 taps; thread (q = t / 32, c = t % 32) sums taps q, q + 8, ...
+    const int c = t & 31, q = t >> 5;
+    float acc = 0.f;
+    for (int k = q; k < 256; k += 8) acc += fmaxf(w1[k * 32 + c], 0.f);
+    part[q][c] = acc;
+  }
+  __syncthreads();
+  if (t < 32) {
+    float acc = fmaxf(b1[t], 0.f);
+    for (int q = 0; q < 8; ++q) acc += part[q][t];
+    B1[t] = acc;
+  }
+  __syncthreads();
+  {  // B2: 64 channels x 512 rows (k, c); thread (q = t / 64, c' = t % 64)
+    const int co = t & 63, q = t >> 6;
+    float acc = 0.f;
+    for (int r = q; r < 512; r += 4) acc += fmaxf(w2[r * 64 + co], 0.f) * B1[r & 31];
+    part[q][co] = acc;
+  }
+  __syncthreads();
+  if (t < 64) {
+    float acc = fmaxf(b2[t], 0.f);
+    for (int q = 0; q < 4; ++q) acc += part[q][t];
+    float m2 = wave_max(acc);
+    float m1 = wave_max(t < 32 ? B1[t] : 0.f);
+    if (t == 0) {
+      const unsigned* mx = reinterpret_cast<const unsigned*>(scr);
+      const float sa1 = band_scale_of(m1), sa2 = band_scale_of(m2);
+      const float sd2 = band_scale_of(__uint_as_float(mx[kBsMaxD2]));
+      const float sd3 = band_scale_of(__uint_as_float(mx[kBsMaxD3]));
+      scr[kBsA1] = sa1;
+      scr[kBsA2] = sa2;
+      scr[kBsD2] = sd2;
+      scr[kBsD3] = sd3;
+      // the kernels' (s_X, s_dY) pairs: conv3 (a2, d3), conv2 (a1, d2)
+      scr[kBsPairC3] = sa2;
+      scr[kBsPairC3 + 1] = sd3;
+      scr[kBsPairC2] = sa1;
+      scr[kBsPairC2 + 1] = sd2;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// the band kernel
+// ---------------------------------------------------------------------------
+constexpr int kBandRows = 16;                         // k-rows (images) per stage
+constexpr int kBandRowBytes = kBandSlabs * 64 * 2;    // 1024: one f16 row of the staged columns
+constexpr int kBandPart = kBandRows * kBandRowBytes;  // 16 KB
+constexpr int kBandBuf = 2 * kBandPart;               // h, l
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_f16(float a, float b) {
+  const f32x2v v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2v));
+}
+// (a, b) * s = h + l to 2^-22 relative: h = f16(x s), l = f16(x s - h)
+// (the residual as fma(x, s, -h): v_fma_mix_f32 reads h from the packed f16 register)
+__device__ __forceinline__ void split2(float a, float b, float s, uint32_t& h, uint32_t& l) {
+  h = pk_f16(a * s, b * s);
+  const f16x2v hv = __builtin_bit_cast(f16x2v, h);
+  l = pk_f16(fmaf(a, s, -(float)hv[0]), fmaf(b, s, -(float)hv[1]));
+}
+__device__ __forceinline__ f16x8 cat8h(s16x4 a, s16x4 b) {
+  const s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(f16x8, v);
+}
+
+struct BandArgs {
+  const float* X;    // [M][kp]
+  const float* dy;   // [M][ldy]
+  int kp, ldy, J, M;
+  int k_chunk, nc;
+  const BandGroup* groups;
+  const int* xlist;  // groups of XCD x: xlist[xoff[x] .. xoff[x + 1])
+  int xoff[9];
+  const float* scales;  // [sx, sy]
+  float* part;       // [nc][ntiles][64][64]
+  float* cs;         // [nc][ncols]
+  int ntiles, ncols;
+};
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void band_kernel(BandArgs p) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * kBandBuf];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  // staging: thread -> rows 2*rp, 2*rp + 1 of the stage; columns 4*lane .. +3
+  // (staged slab lane / 16) and 256 + 4*lane .. +3 (slab 4 + lane / 16)
+  const int rp = wave;
+  const int q = (lane >> 2) & 3, pl = lane & 3, g = (lane >> 4) & 1, kh = lane >> 5;
+  const float sx = p.scales[0], sy = p.scales[1];
+  {
+    // item: XCD x = b & 7 (the blocks b, b + 8, ... share an XCD under the
+    // round-robin dispatch), its j-th (group, chunk) in the region's list
+    const int x = blockIdx.x & 7;
+    const int it = blockIdx.x >> 3;
+    if (it >= (p.xoff[x + 1] - p.xoff[x]) * p.nc) return;
+    const int ngx = p.xoff[x + 1] - p.xoff[x];
+    const int chunk = it / ngx;
+    const BandGroup& G = p.groups[p.xlist[p.xoff[x] + (it - chunk * ngx)]];
+    const int kbeg = chunk * p.k_chunk;
+    const int kend = min(p.M, kbeg + p.k_chunk);
+    const int nk = (kend - kbeg + kBandRows - 1) / kBandRows;
+    const int nslab = G.nslab;
+
+    // this thread's two staged column runs: base pointer, row stride, scale
+    const float* cptr[2];
+    uint32_t cld[2];
+    bool cok[2];
+    float cscale[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int si = 4 * u + (lane >> 4);
+      const int col = (si < nslab ? G.base[si] : p.J) + 4 * (lane & 15);
+      cok[u] = si < nslab && col < p.J;
+      const bool isx = col < p.kp;
+      cptr[u] = isx ? p.X + col : p.dy + (col - p.kp);
+      cld[u] = isx ? (uint32_t)p.kp : (uint32_t)p.ldy;
+      cscale[u] = ((G.xmask >> (si & 7)) & 1) ? sx : sy;
+    }
+    float4 ra[2][4];
+    float csum[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+    // element offsets of this thread's first row in the next stage to fetch
+    // (stages are fetched in order: advanced by 16 rows per fetch)
+    uint32_t foff[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) foff[u] = (uint32_t)(kbeg + 2 * rp) * cld[u];
+
+    auto fetch = [&](int k0, auto S) {
+      constexpr int set = decltype(S)::value;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const bool rok = k0 + 2 * rp + r < kend;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) ra[set][2 * r + u] = stage_f4(cptr[u] + foff[u] + r * cld[u], rok && cok[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) foff[u] += (uint32_t)kBandRows * cld[u];
+    };
+    auto commit = [&](int buf, auto S) {
+      constexpr int set = decltype(S)::value;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int krow = 2 * rp + r;
+        char* s = lds + buf * kBandBuf + krow * kBandRowBytes;
+        const int q8 = 8 * (krow & 3);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const float4 v = ra[set][2 * r + u];
+          csum[4 * u] += v.x;
+          csum[4 * u + 1] += v.y;
+          csum[4 * u + 2] += v.z;
+          csum[4 * u + 3] += v.w;
+          uint2 h, l;
+          split2(v.x, v.y, cscale[u], h.x, l.x);
+          split2(v.z, v.w, cscale[u], h.y, l.y);
+          const int off = 8 * ((64 * u + lane) ^ q8);  // 8-byte slot (4 columns) of column 4*(64u + lane)
+          *reinterpret_cast<uint2*>(s + off) = h;
+          *reinterpret_cast<uint2*>(s + kBandPart + off) = l;
+        }
+      }
+    };
+
+    auto slot_off = [&](int colblock) {
+      const int slot = (colblock >> 2) + 4 * g + pl;
+      return (8 * kh + q) * kBandRowBytes + 8 * (slot ^ (8 * q));
+    };
+    int aoff[2][2], boff[2][2];
+    float inv[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int sa = G.ra[wave][t] < 0 ? 0 : G.ra[wave][t];
+      const int sb = G.cb[wave][t] < 0 ? 0 : G.cb[wave][t];
+      aoff[t][0] = slot_off(64 * sa);
+      aoff[t][1] = slot_off(64 * sa + 32);
+      boff[t][0] = slot_off(64 * sb);
+      boff[t][1] = slot_off(64 * sb + 32);
+      const float s_a = ((G.xmask >> sa) & 1) ? sx : sy, s_b = ((G.xmask >> sb) & 1) ? sx : sy;
+      inv[t] = 1.f / (s_a * s_b);  // powers of two: exact
+    }
+    const int ntile = (G.ra[wave][0] >= 0) + (G.ra[wave][1] >= 0);
+
+    f32x16 acc[2][2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[t][a][b][r] = 0.f;
+
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    if (nk > 0) {
+      fetch(kbeg, S0{});
+      fetch(kbeg + kBandRows, S1{});
+      commit(0, S0{});
+    }
+    __syncthreads();
+
+    auto tile = [&](const char* s, int t) {
+      f16x8 a[2][2], b[2][2];  // [32-column block][part h, l]
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) {
+        const char* sp = s + pt * kBandPart;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          a[cb][pt] = cat8h(ds_tr16(sp + aoff[t][cb]), ds_tr16(sp + aoff[t][cb] + 4 * kBandRowBytes));
+          b[cb][pt] = cat8h(ds_tr16(sp + boff[t][cb]), ds_tr16(sp + boff[t][cb] + 4 * kBandRowBytes));
+        }
+      }
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+          f32x16 c = acc[t][tm][tn];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][1], b[tn][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][0], b[tn][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][0], b[tn][0], c, 0, 0, 0);
+          acc[t][tm][tn] = c;
+        }
+    };
+    // step kt: loads of kt + 2 into the set that held kt, tile 0 from stage kt,
+    // the commit of kt + 1 (set SN) into the other stage, tile 1, barrier
+    auto step = [&](int kt, int cur, auto NT, auto SN) {
+      constexpr int nt = decltype(NT)::value;
+      constexpr int sn = decltype(SN)::value;
+      const char* s = lds + cur * kBandBuf;
+      fetch(kbeg + (kt + 2) * kBandRows, std::integral_constant<int, sn ^ 1>{});
+      if constexpr (nt >= 1) tile(s, 0);
+      if (kt + 1 < nk) commit(cur ^ 1, SN);
+      if constexpr (nt >= 2) tile(s, 1);
+      __syncthreads();
+    };
+    auto run = [&](auto NT) {
+      for (int kt = 0; kt < nk; kt += 2) {
+        step(kt, 0, NT, S1{});
+        if (kt + 1 < nk) step(kt + 1, 1, NT, S0{});
+      }
+    };
+    if (ntile == 0) run(std::integral_constant<int, 0>{});
+    else if (ntile == 1) run(std::integral_constant<int, 1>{});
+    else run(std::integral_constant<int, 2>{});
+
+    // tiles, unscaled, into their compact slots of this chunk
+    const int khalf = lane >> 5;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (t >= ntile) break;
+      float* dst = p.part + ((long long)chunk * p.ntiles + G.tile[wave][t]) * 4096;
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            dst[(32 * tm + (r & 3) + 8 * (r >> 2) + 4 * khalf) * 64 + 32 * tn + (lane & 31)] =
+                acc[t][tm][tn][r] * inv[t];
+    }
+    // column sums: [8 row-pair threads][512 staged columns] through the free LDS
+    float* cl = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cl[rp * 512 + 256 * u + 4 * lane + e] = csum[4 * u + e];
+    __syncthreads();
+    {
+      const int col = tid, si = col >> 6;
+      if (si < nslab && ((G.csown >> si) & 1)) {
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v += cl[r * 512 + col];
+        const int j = G.base[si] + (col & 63);
+        if (j < p.J) p.cs[(long long)chunk * p.ncols + j] = v;
+      }
+    }
+  }
 }
 
 // chunk sums in chunk order, in place into chunk 0 (float4 runs; the tile
@@ -244,11 +590,27 @@ __global__ __launch_bounds__(256) void band_fold_kernel(BandFold f) {
   }
 }
 
+// The operand scales of both band layers into scratch (kBandScratch floats):
+// |d2|, |d3| maxima, then the weight bounds of a1 / a2 and the four scales.
+inline int band_scales(const float* w1, const float* b1, const float* w2, const float* b2, const float* d2,
+                       long long n2, const float* d3, long long n3, float* scr, hipStream_t s) {
+  ACMI_REQUIRE(n2 % 4 == 0 && n3 % 4 == 0 && (uintptr_t)d2 % 16 == 0 && (uintptr_t)d3 % 16 == 0, ACMI_ERR_ARG,
+               "band_scales: dY buffers must be 16-byte aligned float4 runs");
+  ACMI_REQUIRE(hipMemsetAsync(scr, 0, kBandScratch * sizeof(float), s) == hipSuccess, ACMI_ERR_HIP,
+               "band_scales: memset failed");
+  hipLaunchKernelGGL(band_absmax_kernel, dim3(1024), dim3(256), 0, s, reinterpret_cast<const float4*>(d2), n2 / 4,
+                     reinterpret_cast<const float4*>(d3), n3 / 4, reinterpret_cast<unsigned*>(scr + kBsMaxD2));
+  hipLaunchKernelGGL(band_bounds_kernel, dim3(1), dim3(256), 0, s, w1, b1, w2, b2, scr);
+  ACMI_LAUNCH_CHECK("band_scales");
+  return ACMI_OK;
+}
+
 // [dW; db] of one conv layer and its A factor ((K+1)^2, / (M*L)) from the layer
-// input X [M][H][W][C] (f32, dense) and output gradient dY [M][OH][OW][CO].
+// input X [M][H][W][C] (f32, dense) and output gradient dY [M][OH][OW][CO];
+// scales = device [s_X, s_dY] (band_scales).
 inline int band_layer(const float* X, int H, int W, int C, int KH, int KW, int S, const float* dy,
                       int CO, int M, float* ws, long long ws_cap, float* grad, float* astat,
-                      float wscale, hipStream_t s, int site = 0) {
+                      float wscale, const float* scales, hipStream_t s, int site = 0) {
   const BandDev* d = band_dev(H, W, C, KH, KW, S, CO, s);
   ACMI_REQUIRE(d, ACMI_ERR_ARG, "band plan unavailable for %dx%dx%d k%dx%d s%d -> %d", H, W, C, KH, KW, S,
                CO);
@@ -260,14 +622,34 @@ inline int band_layer(const float* X, int H, int W, int C, int KH, int KW, int S
   const long long tile_f = (long long)p.ntiles * 4096, ncols = (long long)g.ns * 64;
   ACMI_REQUIRE((long long)nc * (tile_f + ncols) <= ws_cap, ACMI_ERR_WS,
                "band workspace too small (%lld > %lld)", (long long)nc * (tile_f + ncols), ws_cap);
+  // 32-bit element offsets inside the kernel
+  ACMI_REQUIRE((long long)M * g.kp < (1LL << 31) && (long long)M * g.L * CO < (1LL << 31), ACMI_ERR_ARG,
+               "band_layer: %d images exceed 32-bit offsets", M);
   float* part = ws;
   float* cs = ws + (long long)nc * tile_f;
-  CatRowsI<DenseRows> op{DenseRows{X, g.kp, M, g.kp}, g.kp, dy, g.L * CO, g.L * CO, g.L * CO, M};
-  EpiBand epi{part, cs, p.ntiles, (int)ncols};
-  BandPlanDev pd{d->groups, ng, band_xcd_remap()};
+  BandArgs a;
+  a.X = X;
+  a.dy = dy;
+  a.kp = g.kp;
+  a.ldy = g.L * CO;
+  a.J = g.J;
+  a.M = M;
+  a.k_chunk = ch;
+  a.nc = nc;
+  a.groups = d->groups;
+  a.xlist = d->tabs + d->o_xlist;
+  for (int x = 0; x < 9; ++x) a.xoff[x] = d->xoff[x];
+  a.scales = scales;
+  a.part = part;
+  a.cs = cs;
+  a.ntiles = p.ntiles;
+  a.ncols = (int)ncols;
   prof_begin(site, s);
-  hipLaunchKernelGGL((symred6_kernel<CatRowsI<DenseRows>, EpiBand, true, BandPlanDev>), dim3(ng * nc),
-                     dim3(512), 0, s, op, epi, pd, g.nxs * 64, g.J, M, ch);
+  // one block per item (512 threads, 64 KB of LDS, two waves per SIMD): 8 x the
+  // longest XCD list; the blocks past a shorter list's end exit at once
+  int maxg = 0;
+  for (int x = 0; x < 8; ++x) maxg = std::max(maxg, d->xoff[x + 1] - d->xoff[x]);
+  hipLaunchKernelGGL(band_kernel, dim3(8 * maxg * nc), dim3(512), 0, s, a);
   prof_end(site, s);
   if (nc > 1) {
     const long long n4 = (tile_f + ncols) / 4;

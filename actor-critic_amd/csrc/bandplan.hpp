@@ -63,21 +63,30 @@ inline int band_xoff(const BandGeom& g, int x) { return (x % g.spx) * g.C; }
 inline int band_yslab(const BandGeom& g, int l) { return g.nxs + (l * g.CO) / 64; }
 inline int band_yoff(const BandGeom& g, int l) { return (l * g.CO) % 64; }
 
-// One block of symred6_kernel: six staged slabs, up to two 64x64 sub-tiles per
-// wave (ra/cb index the staged slabs; -1: none), each with its compact tile id;
-// csown: the staged slabs whose column sums this group writes (each slab's by
-// exactly one group).  Same field names as SymGroup6 where they mean the same.
+// One work item of band_kernel (band.hpp): up to kBandSlabs staged 64-column
+// slabs of [X | dY] (a prefix of `base`, nslab of them), up to two 64x64
+// sub-tiles per wave (ra/cb index the staged slabs; -1: none), each with its
+// compact tile id; csown: the staged slabs whose column sums this group writes
+// (each slab's by exactly one group); xmask: bit i set when staged slab i is an
+// X (layer input) slab -- its operand scale is the X scale, else the dY scale.
+constexpr int kBandSlabs = 8;
 struct BandGroup {
-  int base[6];        // first [X | dY] column of each staged slab
+  int base[kBandSlabs];  // first [X | dY] column of each staged slab
   signed char ra[8][2];
   signed char cb[8][2];
   short tile[8][2];
-  int csown;
+  unsigned char csown;
+  unsigned char nslab;
+  unsigned char xmask;
+  unsigned char pad;
 };
 
 struct BandPlan {
   BandGeom geom;
   std::vector<BandGroup> groups;
+  // work lists per XCD: groups of one spatial region of the image (so an XCD's
+  // L2 holds the columns its blocks stream), balanced by SIMD units
+  std::vector<int> xcd_groups[8];
   int ntiles = 0;
   std::vector<int> tile_of;   // [ns * ns] (a <= b) -> tile id, -1 if not computed
   // fold tables: element offsets into the tile array T[ntiles][64][64] and the
@@ -109,17 +118,19 @@ inline std::vector<char> band_needed(const BandGeom& g) {
   return need;
 }
 
-// Greedy covering of the needed sub-tiles by six-slab groups of <= 16 tiles:
-// each of the 32 slabs with the most uncovered tiles seeds a candidate set grown
-// by the neighbour adding the most uncovered tiles; the candidate with the most
-// tiles (capped at 16; ties: fewest left over) wins and takes its 16 hardest tiles
-// (fewest other uncovered tiles on their slabs), full-width before half-width
-// so a half tile never sits in slot 0 above a full one.  Seeded restarts, the
-// fewest groups kept.  Groups are emitted in order of their first slab.
-inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 2) {
+// Greedy covering of the needed sub-tiles by groups of <= kBandSlabs slabs and
+// <= 16 tiles (two per wave): each of the 32 slabs with the most uncovered tiles
+// seeds a candidate set grown by the neighbour adding the most uncovered tiles;
+// the candidate with the most tiles (capped at 16; ties: fewest left over) wins
+// and takes its 16 hardest tiles (fewest other uncovered tiles on their slabs).
+// A group stages only the slabs its tiles use (the greedy's leftover groups are
+// small).  Seeded restarts, the fewest groups kept.  Conv2 (M = 10240): 190
+// groups, 117 of them full, against 243 six-slab groups of 9.5 tiles -- 8 slabs
+// double the pairs a staged set can hold (28 + 8 against 15 + 6).
+inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 3) {
+  constexpr int NS = kBandSlabs;
+  constexpr int cap = 16;
   const int ns = g.ns;
-  // ACMI_BAND_CAP: sub-tiles per group (default 16 = two per wave)
-  static const int cap = std::max(1, std::min(16, getenv("ACMI_BAND_CAP") ? atoi(getenv("ACMI_BAND_CAP")) : 16));
   const std::vector<char> need0 = band_needed(g);
   bool found = false;
   for (int rs = 0; rs < restarts; ++rs) {
@@ -145,7 +156,7 @@ inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 2) 
     auto grow = [&](int s0, int* set) {
       int n = 0;
       set[n++] = s0;
-      while (n < 6) {
+      while (n < NS) {
         cand.clear();
         for (int i = 0; i < n; ++i)
           for (int y : nbr[set[i]])
@@ -163,7 +174,7 @@ inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 2) 
           for (int i = 0; i < n; ++i) gain += nd(x, set[i]);
           if (gain > bg) bg = gain, bx = x;
         }
-        if (bx < 0) {  // fill with any other slab (staged, unused)
+        if (bx < 0) {  // fill with any other slab (dropped again below if unused)
           for (int x = 0; x < ns && bx < 0; ++x) {
             bool in = false;
             for (int i = 0; i < n; ++i) in |= set[i] == x;
@@ -173,82 +184,114 @@ inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 2) 
         set[n++] = bx;
       }
       int tot = 0;
-      for (int i = 0; i < 6; ++i)
-        for (int j = i; j < 6; ++j) tot += nd(set[i], set[j]);
+      for (int i = 0; i < NS; ++i)
+        for (int j = i; j < NS; ++j) tot += nd(set[i], set[j]);
       return tot;
     };
     while (remaining > 0) {
       std::shuffle(order.begin(), order.end(), rng);
-      // every slab with work seeds a candidate; the most tiles (capped at 16)
-      // win, ties to the fewest left over
-      int set[6], best_key = -1, best_tot = 0;
-      // seeds: the slabs with the most uncovered tiles (the first kSeeds of them)
+      int set[NS], best_key = -1, best_tot = 0;
       std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return deg[x] > deg[y]; });
       constexpr int kSeeds = 32;
       int tried = 0;
       for (int s0 : order) {
         if (deg[s0] == 0 || tried++ == kSeeds) break;
-        int cs[6];
+        int cs[NS];
         const int tot = grow(s0, cs);
         const int key = std::min(cap, tot);
         if (key > best_key || (key == best_key && tot < best_tot)) {
           best_key = key, best_tot = tot;
-          for (int i = 0; i < 6; ++i) set[i] = cs[i];
+          for (int i = 0; i < NS; ++i) set[i] = cs[i];
         }
       }
-      std::sort(set, set + 6);
       struct T {
-        int i, j, key;
-        bool half;
+        int a, b, key;
       };
       std::vector<T> tiles;
-      for (int i = 0; i < 6; ++i)
-        for (int j = i; j < 6; ++j)
-          if (nd(set[i], set[j]))
-            tiles.push_back({i, j, deg[set[i]] + deg[set[j]], 64 * set[j] + 32 >= g.J});
+      for (int i = 0; i < NS; ++i)
+        for (int j = i; j < NS; ++j) {
+          const int a = std::min(set[i], set[j]), b = std::max(set[i], set[j]);
+          if (nd(a, b)) tiles.push_back({a, b, deg[a] + deg[b]});
+        }
       std::stable_sort(tiles.begin(), tiles.end(), [](const T& x, const T& y) { return x.key < y.key; });
       if ((int)tiles.size() > cap) tiles.resize(cap);
-      std::stable_sort(tiles.begin(), tiles.end(), [](const T& x, const T& y) { return !x.half && y.half; });
+      // the staged slabs: the ones the chosen tiles use, in column order
+      std::vector<int> used;
+      for (const T& t : tiles) used.push_back(t.a), used.push_back(t.b);
+      std::sort(used.begin(), used.end());
+      used.erase(std::unique(used.begin(), used.end()), used.end());
       BandGroup G;
-      for (int i = 0; i < 6; ++i) G.base[i] = 64 * set[i];
+      G.nslab = (unsigned char)used.size();
+      G.xmask = 0;
+      for (int i = 0; i < NS; ++i) {
+        G.base[i] = i < (int)used.size() ? 64 * used[i] : -1;
+        if (i < (int)used.size() && used[i] < g.nxs) G.xmask |= (unsigned char)(1u << i);
+      }
       for (int w = 0; w < 8; ++w)
         for (int t = 0; t < 2; ++t) G.ra[w][t] = G.cb[w][t] = -1, G.tile[w][t] = -1;
       G.csown = 0;
+      G.pad = 0;
+      auto idx = [&](int slab) { return (int)(std::lower_bound(used.begin(), used.end(), slab) - used.begin()); };
       for (int m = 0; m < (int)tiles.size(); ++m) {
-        const int a = set[tiles[m].i], b = set[tiles[m].j];
+        const int a = tiles[m].a, b = tiles[m].b;
         need[(size_t)a * ns + b] = 0;
         --remaining;
         --deg[a];
         if (b != a) --deg[b];
-        G.ra[m % 8][m / 8] = (signed char)tiles[m].i;
-        G.cb[m % 8][m / 8] = (signed char)tiles[m].j;
+        G.ra[m % 8][m / 8] = (signed char)idx(a);
+        G.cb[m % 8][m / 8] = (signed char)idx(b);
       }
       groups.push_back(G);
     }
     if (found && groups.size() >= out->groups.size()) continue;
-    // emit heaviest groups first (the busiest SIMD's sub-tiles: blocks of
-    // unequal length, longest dispatched first), then in order of the first slab
-    // (neighbouring groups read neighbouring columns of the same rows);
-    // ACMI_BAND_SORT=0: by first slab only (measured 1.37 vs 1.26 ms for conv2)
-    std::stable_sort(groups.begin(), groups.end(),
-                     [](const BandGroup& x, const BandGroup& y) { return x.base[0] < y.base[0]; });
-    static const int sort_units = getenv("ACMI_BAND_SORT") ? atoi(getenv("ACMI_BAND_SORT")) : 1;
-    if (sort_units) {
-      auto units = [](const BandGroup& G) {
-        int t = 0;
-        for (int w = 0; w < 8; ++w) t += (G.ra[w][0] >= 0) + (G.ra[w][1] >= 0);
-        return (t + 3) / 4;
-      };
-      std::stable_sort(groups.begin(), groups.end(),
-                       [&](const BandGroup& x, const BandGroup& y) { return units(x) > units(y); });
-    }
     out->geom = g;
     out->groups = groups;
     found = true;
   }
   if (!found) return false;
-  // tile ids (group-major), column-sum owners (first group staging the slab)
   BandPlan& p = *out;
+  // spatial order (the image row a group's slabs sit on; dY slabs at the input
+  // row their patch starts from), then 8 contiguous regions of equal SIMD work
+  auto row_of = [&](int slab) -> double {
+    if (slab < g.nxs) return (double)((slab * g.spx) / g.W);
+    const int l = ((slab - g.nxs) * 64) / g.CO;
+    return (double)(g.S * (l / g.OW)) + 0.5 * (g.KH - 1);
+  };
+  auto units = [](const BandGroup& G) {
+    int u = 0;
+    for (int w = 0; w < 4; ++w) {
+      int t = 0;
+      for (int h = 0; h < 2; ++h) t += (G.ra[w + 4 * h][0] >= 0) + (G.ra[w + 4 * h][1] >= 0);
+      u = std::max(u, t);
+    }
+    return u;
+  };
+  std::vector<double> key(p.groups.size());
+  for (size_t i = 0; i < p.groups.size(); ++i) {
+    double k = 0;
+    for (int j = 0; j < p.groups[i].nslab; ++j) k += row_of(p.groups[i].base[j] / 64);
+    key[i] = k / std::max(1, (int)p.groups[i].nslab);
+  }
+  std::vector<int> ord(p.groups.size());
+  for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
+  std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return key[x] < key[y]; });
+  {
+    std::vector<BandGroup> sorted;
+    for (int i : ord) sorted.push_back(p.groups[i]);
+    p.groups.swap(sorted);
+  }
+  // work of a group: its busiest SIMD's sub-tiles + the staging it pays per slab
+  auto work = [&](const BandGroup& G) { return 4.0 * units(G) + 0.5 * G.nslab + 1.0; };
+  double total = 0;
+  for (const BandGroup& G : p.groups) total += work(G);
+  double acc = 0;
+  for (int x = 0; x < 8; ++x) p.xcd_groups[x].clear();
+  for (size_t i = 0; i < p.groups.size(); ++i) {
+    const int x = std::min(7, (int)(8.0 * (acc + 0.5 * work(p.groups[i])) / total));
+    p.xcd_groups[x].push_back((int)i);
+    acc += work(p.groups[i]);
+  }
+  // tile ids (group-major), column-sum owners (first group staging the slab)
   p.tile_of.assign((size_t)ns * ns, -1);
   std::vector<char> csdone(ns, 0);
   int nt = 0;
@@ -260,9 +303,9 @@ inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 2) 
         G.tile[w][t] = (short)nt;
         p.tile_of[(size_t)a * ns + b] = nt++;
       }
-    for (int i = 0; i < 6; ++i) {
+    for (int i = 0; i < G.nslab; ++i) {
       const int s = G.base[i] / 64;
-      if (!csdone[s]) csdone[s] = 1, G.csown |= 1 << i;
+      if (!csdone[s]) csdone[s] = 1, G.csown |= (unsigned char)(1u << i);
     }
   }
   p.ntiles = nt;
@@ -310,33 +353,45 @@ inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 2) 
 }
 
 // Coverage check (acmi_selftest_plans): every needed pair computed exactly once,
-// at most two tiles per wave with slot 0 filled first, a half-width tile in
-// slot 0 only above another half-width one, every slab's column sums owned once.
+// at most two tiles per wave with slot 0 filled first, tiles only on staged
+// slabs (a prefix of base, in column order), X/dY scale mask right, every slab's
+// column sums owned once, every group in exactly one XCD list.
 inline int band_plan_check(const BandPlan& p) {
   const BandGeom& g = p.geom;
   const std::vector<char> need = band_needed(g);
   std::vector<int> cov((size_t)g.ns * g.ns, 0), cs(g.ns, 0);
   for (const BandGroup& G : p.groups) {
+    if (G.nslab < 1 || G.nslab > kBandSlabs) return 6;
+    for (int i = 0; i < kBandSlabs; ++i) {
+      if ((i < G.nslab) != (G.base[i] >= 0)) return 7;
+      if (i > 0 && i < G.nslab && G.base[i] <= G.base[i - 1]) return 7;
+      if (i < G.nslab && (((G.xmask >> i) & 1) != (G.base[i] / 64 < g.nxs))) return 8;
+    }
     for (int w = 0; w < 8; ++w) {
       if (G.ra[w][0] < 0 && G.ra[w][1] >= 0) return 1;
       for (int t = 0; t < 2; ++t) {
         if (G.ra[w][t] < 0) continue;
+        if (G.ra[w][t] >= G.nslab || G.cb[w][t] >= G.nslab) return 9;
         const int a = G.base[G.ra[w][t]] / 64, b = G.base[G.cb[w][t]] / 64;
         if (a > b || a >= g.nxs) return 2;
         cov[(size_t)a * g.ns + b]++;
       }
-      if (G.ra[w][0] >= 0 && G.ra[w][1] >= 0) {
-        const bool h0 = G.base[G.cb[w][0]] + 32 >= g.J, h1 = G.base[G.cb[w][1]] + 32 >= g.J;
-        if (h0 && !h1) return 3;
-      }
     }
-    for (int i = 0; i < 6; ++i)
+    for (int i = 0; i < G.nslab; ++i)
       if (G.csown >> i & 1) cs[G.base[i] / 64]++;
   }
   for (size_t e = 0; e < need.size(); ++e)
     if (need[e] && cov[e] != 1) return 4;
   for (int s = 0; s < g.ns; ++s)
     if (cs[s] != 1) return 5;
+  std::vector<int> seen(p.groups.size(), 0);
+  for (int x = 0; x < 8; ++x)
+    for (int i : p.xcd_groups[x]) {
+      if (i < 0 || i >= (int)p.groups.size()) return 10;
+      seen[i]++;
+    }
+  for (int v : seen)
+    if (v != 1) return 10;
   return 0;
 }
 

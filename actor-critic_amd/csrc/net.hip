@@ -331,32 +331,11 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* part, int nz, c
   }
 }
 
-// conv input gradients with the dY im2col in LDS (convt3.hpp): ACMI_CONVT =
-// 1 (default) conv3 only; 0 off (gemm3 over ConvTRows); 2 / 3 / 4 conv2 too,
-// with 128- / 64- / 256-column (8-wave) blocks.  Measured (M = 10240, per
-// launch): conv3 231 -> 186 us; conv2 444 us on gemm3 vs 939 / slower / 620
-// here -- its f32 dY image (3-4 images x 81 px x 64 ch) leaves one block per CU.
-static int convt_lds() {
-  static const int v = getenv("ACMI_CONVT") ? atoi(getenv("ACMI_CONVT")) : 1;
-  return v;
-}
-
-// conv2's input gradient on pre-split weights, four phases per wave
-// (convt2.hpp; needs net->conv_prep): ACMI_CONVT2 = 1 (default) or 0
-static int convt2_on() {
-  static const int v = getenv("ACMI_CONVT2") ? atoi(getenv("ACMI_CONVT2")) : 1;
-  return v;
-}
-
-// conv forward with the im2col in LDS (convfwd3.hpp): ACMI_CONVF = 1 (default)
-// conv3 only, 0 off, 2 conv1 and conv2 too.  Measured at 512 images per launch:
-// conv3 18.7 us (vs 19.6 on the f32 128x32 tile), conv1 26.5 (= conv1_fwd_x3),
-// conv2 82 (vs 30 on gemm3: its 51 KB image + 48 KB weight stages leave one
-// block per CU; with 16-row stages 50).
-static int convf_lds() {
-  static const int v = getenv("ACMI_CONVF") ? atoi(getenv("ACMI_CONVF")) : 1;
-  return v;
-}
+// (Measured and removed: conv2's input gradient on the dY-im2col-in-LDS kernel
+// of convt3.hpp, 939 / 620 us per launch at M = 10240 against 444 on gemm3 -- its
+// f32 dY image leaves one block per CU; conv1 / conv2 forwards on convfwd3.hpp,
+// 26.5 / 82 us at 512 images against 26.5 / 30.  conv3's input gradient and
+// forward keep those kernels: 231 -> 186 us, 19.6 -> 18.7 us.)
 
 // forward precision (acmi_set_forward_mode): the tower's arithmetic
 int g_forward_mode = [] {
@@ -364,23 +343,10 @@ int g_forward_mode = [] {
   return (e && e[0] == 'b') ? ACMI_FWD_BF16 : ACMI_FWD_F32;
 }();
 
-// conv1 -> conv2 -> conv3 as one fused kernel per image (tower.hpp, bf16x3
-// mode): ACMI_TOWER = 1 (default) or 0 (the per-layer kernels below)
-static int tower_on() {
-  static const int v = getenv("ACMI_TOWER") ? atoi(getenv("ACMI_TOWER")) : 1;
-  return v;
-}
-
-// fc4's split-K slabs at rollout batches on the pre-split W4 without LDS
-// (fc4roll.hpp; needs net->conv_prep): ACMI_FC4R = 1 (default) or 0 (gemm3)
-static int fc4r_on() {
-  static const int v = getenv("ACMI_FC4R") ? atoi(getenv("ACMI_FC4R")) : 1;
-  return v;
-}
-
-// split factor for fc4 at small batch (64 x 128 tiles over 512 columns)
+// split factor for fc4 at small batch (64 x 128 tiles over 512 columns; 4 / 6 /
+// 12 / 16 chunks measured no better than 8)
 static void fc4_plan(int B, int K, int* nz, int* chunk) {
-  static const int maxsp = getenv("ACMI_FC4_SPLIT") ? atoi(getenv("ACMI_FC4_SPLIT")) : 8;
+  constexpr int maxsp = 8;
   const int blocks = cdiv(B, 64) * 4;
   int sp = blocks >= 256 ? 1 : std::min(maxsp, cdiv(256 * maxsp / 8, blocks));
   const int q = g_gemm_mode == ACMI_GEMM_X3 ? 16 : 32;  // the split GEMM's K-tile
@@ -400,7 +366,9 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // act_img_stride: images between consecutive batch rows in the activation
   // buffers (1 = contiguous; T = rollout step t of an env-major buffer).
   const long long st = act_img_stride;
-  const bool tower = g_gemm_mode == ACMI_GEMM_X3 && tower_on() && (uintptr_t)obs % 16 == 0 && img_stride % 16 == 0;
+  // conv1 -> conv2 -> conv3 as one fused kernel per image (tower.hpp) in bf16x3
+  // mode; the per-layer kernels below in f32 mode or for unaligned images
+  const bool tower = g_gemm_mode == ACMI_GEMM_X3 && (uintptr_t)obs % 16 == 0 && img_stride % 16 == 0;
   ACMI_REQUIRE(tower || g_forward_mode == ACMI_FWD_F32, ACMI_ERR_ARG,
                "bf16 forward needs the fused tower: 16-byte aligned observations and image stride");
   if (tower) {
@@ -415,10 +383,7 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     MatI<true> w{P + L.off[0], 32, 256, 32};
     EpiAct epi{a->a1, P + L.off[1], 32, 400, st * 400 * 32, 1.0f / 255.0f};
     prof_begin(ACMI_PROF_CONV1_FWD, s);
-    if (g_gemm_mode == ACMI_GEMM_X3 && convf_lds() == 2)
-      launch_convf_x3<uint8_t, 84, 84, 4, 8, 8, 4, 32, 1, 64>(obs, img_stride, B, P + L.off[0], epi, s);
-    else
-      launch_conv1_fwd_u8<32>(Src{obs, (uint32_t)img_stride, B * 400}, w, epi, B * 400, 256, s);
+    launch_conv1_fwd_u8<32>(Src{obs, (uint32_t)img_stride, B * 400}, w, epi, B * 400, 256, s);
     prof_end(ACMI_PROF_CONV1_FWD, s);
   }
   {  // conv2: -> [B,9,9,64]
@@ -426,9 +391,7 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     RowsAsK<Src> opA{Src{a->a1, (uint32_t)(st * 400 * 32), B * 81}};
     MatI<true> opB{P + L.off[2], 64, 512, 64};
     EpiAct epi{a->a2, P + L.off[3], 64, 81, st * 81 * 64};
-    if (g_gemm_mode == ACMI_GEMM_X3 && convf_lds() == 2)
-      launch_convf_x3<float, 20, 20, 32, 4, 4, 2, 64, 1, 64>(a->a1, st * 400 * 32, B, P + L.off[2], epi, s);
-    else if (B <= 2048)
+    if (B <= 2048)
       launch_mm<64, 64, 32, 1, 1, false, false, 32>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
     else
       launch_mm<128, 64, 32, 2, 1, false, false, 16>(opA, opB, epi, B * 81, 64, 512, 1, 0, s);
@@ -438,7 +401,7 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     RowsAsK<Src> opA{Src{a->a2, (uint32_t)(st * 81 * 64), B * 49}};
     MatI<true> opB{P + L.off[4], C3, 576, C3};
     EpiAct epi{a->a3, P + L.off[5], C3, 49, st * 49 * C3};
-    if (g_gemm_mode == ACMI_GEMM_X3 && convf_lds())
+    if (g_gemm_mode == ACMI_GEMM_X3)
       launch_convf_x3<float, 9, 9, 64, 3, 3, 1, C3, 2, 64>(a->a2, st * 81 * 64, B, P + L.off[4], epi, s);
     else if constexpr (C3 == 32)
       // (f32 MFMA: the 128x32 bf16x3 tile needs BK = 32 and fits 2 blocks per CU;
@@ -460,7 +423,7 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     // small (rollout) batches: split K over chunks; the heads kernel reduces
     // the slabs in fixed order and applies bias + relu
     const char* w4p = prep ? static_cast<const char*>(prep) + TowerPrep<C3>::BYTES + CT2::BYTES : nullptr;
-    if (!(g_gemm_mode == ACMI_GEMM_X3 && w4p && fc4r_on() &&
+    if (!(g_gemm_mode == ACMI_GEMM_X3 && w4p &&
           launch_fc4_roll(a->a3, st * K4, B, K4, w4p, nz, chunk, a->ws, s))) {
       EpiPartial epi{a->ws, B, 512};
       launch_mm<64, 128, 32, 1, 2, true, false, 16>(opA4, opB4, epi, B, 512, K4, nz, chunk, s);
@@ -802,11 +765,6 @@ struct WgradPlan {
   long long floats;
 };
 
-// ACMI_SIX_GREEDY=0: fc4's wgrad + A factor on gemm3 128x128 live tiles instead
-static bool six_greedy_on() {
-  static const bool v = !getenv("ACMI_SIX_GREEDY") || atoi(getenv("ACMI_SIX_GREEDY")) != 0;
-  return v;
-}
 static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows, bool u8 = false,
                             int mode = g_gemm_mode) {
   WgradPlan p;
@@ -817,9 +775,9 @@ static WgradPlan wgrad_plan(int K, int cout, bool with_stats, long long rows, bo
   // column-sum row's P part, by symmetry
   p.J = p.kp + p.cout_pad;
   p.slabs = with_stats && sym_plan(K, p.cout_pad, &p.sp);  // (f32 patch sources only)
-  p.six = p.slabs && mode == ACMI_GEMM_X3 && (symred_variant() == 0 || symred_variant() == 5) && sym_plan6(K, p.cout_pad, &p.sp6);
+  p.six = p.slabs && mode == ACMI_GEMM_X3 && sym_plan6(K, p.cout_pad, &p.sp6);
   // fc4 (K = 1568, no four-slab plan): greedy six-slab groups instead of 128x128 tiles
-  p.six_greedy = !p.slabs && !u8 && with_stats && mode == ACMI_GEMM_X3 && K % 4 == 0 && six_greedy_on() &&
+  p.six_greedy = !p.slabs && !u8 && with_stats && mode == ACMI_GEMM_X3 && K % 4 == 0 &&
                  sym_plan6_greedy(K, p.cout_pad, &p.sp6);
   if (p.six_greedy) p.six = true;
   if (u8)  // conv1 weight gradient: conv1_wgrad_u8/x3_kernel, one 256x32 block per chunk
@@ -980,36 +938,10 @@ static long long bwd_partial_cap(int B, int A, int C3) {
   // band reductions of conv2 / conv3 (rows = images)
   m = std::max(m, band_ws_floats(band_host_plan(20, 20, 32, 4, 4, 2, 64), B));
   m = std::max(m, band_ws_floats(band_host_plan(9, 9, 64, 3, 3, 1, C3), B));
-  return m;
+  // + the band reductions' scratch (operand scales, queue counters) at the end
+  return (m + 3) / 4 * 4 + kBandScratch;
 }
 
-// The conv1 A factor reads only the frames: it can run on a library-owned side
-// stream (one per device) concurrently with the input-gradient chain and the
-// other reductions, in its own workspace region after the shared partials.
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-static SideStream* side_stream() {
-  // opt-in (ACMI_SIDE=1): at the bench shape the overlap costs more than it
-  // hides (update 5.69 vs 5.64 ms -- the i8 gather competes with the
-  // symmetric reductions for L2 and LDS)
-  static const bool on = getenv("ACMI_SIDE") && atoi(getenv("ACMI_SIDE")) == 1;
-  if (!on) return nullptr;
-  static SideStream ss[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  SideStream& x = ss[dev];
-  if (!x.s) {
-    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) {
-      x.s = nullptr;
-      return nullptr;
-    }
-  }
-  return &x;
-}
 static long long afactor_ws_floats(int B) { return conv1_afactor_ws_ints(400LL * B); }
 
 // Recorded on the backward's stream right after its input-gradient chain (per
@@ -1026,18 +958,6 @@ static hipEvent_t* dx_done_event() {
   }
   return &ev[dev];
 }
-// the conv1 A factor after the dX chain (default), so that it too runs next to
-// the sampled-loss chain started at the dX event; ACMI_AF_FIRST=1: before it
-// ACMI_FUSE_C1=0: the conv1 weight gradient in its own pass (conv1_wgrad_x3_kernel)
-static bool conv1_fused() {
-  static const bool v = !getenv("ACMI_FUSE_C1") || atoi(getenv("ACMI_FUSE_C1")) != 0;
-  return v;
-}
-static bool afactor_first() {
-  static const bool v = getenv("ACMI_AF_FIRST") && atoi(getenv("ACMI_AF_FIRST")) != 0;
-  return v;
-}
-
 // ---------------------------------------------------------------------------
 // backward (dX chain) shared by the loss backward and the sampled backward
 // ---------------------------------------------------------------------------
@@ -1069,7 +989,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     W opA{P + L.off[4]};
     RowsAsK<Src> opB{Src{bw->d3, B * Src::L}};
     EpiConvT<9, 9, 1, 64> epi{bw->d2, a->a2};
-    if (g_gemm_mode == ACMI_GEMM_X3 && convt_lds())
+    if (g_gemm_mode == ACMI_GEMM_X3)
       launch_convt_x3<9, 9, 3, 3, 1, 64, C3, 256>(P + L.off[4], bw->d3, B, epi, s);
     else
       launch_mm<64, 128, 16, 1, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
@@ -1083,7 +1003,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     EpiConvT<20, 20, 2, 32> epi{bw->d1, a->a1};
     prof_begin(ACMI_PROF_CONV2_DX, s);
     const char* p2 = prep ? prep + TowerPrep<C3>::BYTES : nullptr;
-    if (p2 && g_gemm_mode == ACMI_GEMM_X3 && convt2_on()) {
+    if (p2 && g_gemm_mode == ACMI_GEMM_X3) {
       // pre-split weights, four phases per wave (convt2.hpp); the sampled-loss
       // chain reduces d1 to its Gram partials instead of storing it
       if (gram_part) {
@@ -1094,13 +1014,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
 hipLaunchKernelGGL(convt2_kernel<false>, dim3(cdiv(B * CT2::L, CT2::TILE)), dim3(256), 0, s, p2,
                            bw->d2, a->a1, bw->d1, B, nullptr);
       }
-    } else if (g_gemm_mode == ACMI_GEMM_X3 && convt_lds() == 2)
-      launch_convt_x3<20, 20, 4, 4, 2, 32, 64, 128>(P + L.off[2], bw->d2, B, epi, s);
-    else if (g_gemm_mode == ACMI_GEMM_X3 && convt_lds() == 3)
-      launch_convt_x3<20, 20, 4, 4, 2, 32, 64, 64>(P + L.off[2], bw->d2, B, epi, s);
-    else if (g_gemm_mode == ACMI_GEMM_X3 && convt_lds() == 4)
-      launch_convt_x3<20, 20, 4, 4, 2, 32, 64, 256, 8>(P + L.off[2], bw->d2, B, epi, s);
-    else
+    } else
       launch_mm<128, 128, 16, 2, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
     prof_end(ACMI_PROF_CONV2_DX, s);
   }
@@ -1114,46 +1028,35 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
                          const acmi_bwd_t* bw, float* grads, float* astat,
                          float* ws, long long ws_cap, hipStream_t s, const char* prep) {
   const bool st = astat != nullptr;
-  // conv1 A factor first, on the side stream (its int partials after the shared
-  // split-K partials); falls back to this stream when no side stream exists
-  SideStream* side = st ? side_stream() : nullptr;
-  // conv1's weight gradient fused into the A-factor pass (needs d1: after the dX chain)
-  const bool fuse_c1 = st && g_gemm_mode == ACMI_GEMM_X3 && !afactor_first() && conv1_fused();
-  auto dx = [&]() -> int {
-    const int r = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s, prep);
-    if (r) return r;
+  // conv1's weight gradient is fused into the A-factor pass (bf16x3 mode; it needs
+  // d1, so the pass follows the dX chain).  (Measured and removed: the A factor on a
+  // library side stream next to the dX chain, 5.69 vs 5.64 ms per update -- the i8
+  // gather competes with the symmetric reductions for L2 and LDS; the A factor
+  // before the dX chain.)
+  const bool fuse_c1 = st && g_gemm_mode == ACMI_GEMM_X3;
+  int rc = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s, prep);
+  if (rc) return rc;
+  {
     hipEvent_t* ev = dx_done_event();
-    ACMI_REQUIRE(ev && hipEventRecord(*ev, s) == hipSuccess, ACMI_ERR_HIP,
-                 "acmi_backward: dX event record failed");
-    return ACMI_OK;
-  };
-  int rc = ACMI_OK;
-  if (!afactor_first() && (rc = dx())) return rc;
+    ACMI_REQUIRE(ev && hipEventRecord(*ev, s) == hipSuccess, ACMI_ERR_HIP, "acmi_backward: dX event record failed");
+  }
   if (st) {
     const long long pcap = bwd_partial_cap(B, L.A, L.C3);
-    hipStream_t as = s;
-    if (side) {
-      ACMI_REQUIRE(hipEventRecord(side->fork, s) == hipSuccess &&
-                       hipStreamWaitEvent(side->s, side->fork, 0) == hipSuccess,
-                   ACMI_ERR_HIP, "acmi_backward: side-stream fork failed");
-      as = side->s;
-    }
-    prof_begin(ACMI_PROF_CONV1_AFACTOR, as);
+    prof_begin(ACMI_PROF_CONV1_AFACTOR, s);
     float* wpart = nullptr;
     const int rc0 = conv1_afactor_u8(obs, img_stride, B, astat + L.stat_off[0],
-                                     reinterpret_cast<int*>(ws + pcap), afactor_ws_floats(B), as,
+                                     reinterpret_cast<int*>(ws + pcap), afactor_ws_floats(B), s,
                                      fuse_c1 ? bw->d1 : nullptr, &wpart);
-    prof_end(ACMI_PROF_CONV1_AFACTOR, as);
+    prof_end(ACMI_PROF_CONV1_AFACTOR, s);
     if (rc0) return rc0;
     if (fuse_c1) {  // the conv1 weight gradient came with the A factor: reduce its chunks
       const long long rows = 400LL * B;
       WgradDesc d{wpart, conv1_afactor_fused_chunks(rows), 256, 32, 0, 32, grads + L.off[0], 32,
                   nullptr, nullptr, (int)rows, 1.0f / 255.0f};
-      hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(257 * 32, 32)), dim3(256), 0, as, d);
+      hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(257 * 32, 32)), dim3(256), 0, s, d);
       ACMI_LAUNCH_CHECK("conv1 fused weight gradient");
     }
   }
-  if (afactor_first() && (rc = dx())) return rc;
   float* part = ws;
   // heads: X = a4 (512), dY = dhead (A+1 columns: pi | v)
   rc = wgrad_layer(DenseRows{a->a4, 512, B, 512}, 512, B, bw->dhead, bw->ldh, L.A + 1, st,
@@ -1167,17 +1070,27 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   if (rc) return rc;
   // conv3 / conv2: pixel-pair band reductions over the dense activation rows
   // (band.hpp), or the patches of a2 / a1
-  if (band_on(st))
-    rc = band_layer(a->a2, 9, 9, 64, 3, 3, 1, bw->d3, C3, B, part, ws_cap, grads + L.off[4],
-                    astat + L.stat_off[2], 1.f, s);
-  else
+  const long long pcap_all = bwd_partial_cap(B, L.A, L.C3);
+  float* bscr = ws + pcap_all - kBandScratch;  // operand scales + queue counters
+  const long long band_cap = pcap_all - kBandScratch;
+  if (band_on(st)) {
+    rc = band_scales(P + L.off[0], P + L.off[1], P + L.off[2], P + L.off[3], bw->d2, 81LL * 64 * B, bw->d3,
+                     49LL * C3 * B, bscr, s);
+    if (rc) return rc;
+  }
+  float* sc_c3 = bscr + kBsPairC3;  // [s_a2, s_d3] and [s_a1, s_d2]: the kernels' (s_X, s_dY)
+  float* sc_c2 = bscr + kBsPairC2;
+  if (band_on(st)) {
+    rc = band_layer(a->a2, 9, 9, 64, 3, 3, 1, bw->d3, C3, B, part, band_cap, grads + L.off[4],
+                    astat + L.stat_off[2], 1.f, sc_c3, s);
+  } else
     rc = wgrad_layer(ConvRows<float, 9, 9, 64, 3, 3, 1>{a->a2, 81 * 64, B * 49}, 576, 49LL * B,
                      bw->d3, C3, C3, st, part, ws_cap, grads + L.off[4], C3, nullptr,
                      st ? astat + L.stat_off[2] : nullptr, s);
   if (rc) return rc;
   if (band_on(st))
-    rc = band_layer(a->a1, 20, 20, 32, 4, 4, 2, bw->d2, 64, B, part, ws_cap, grads + L.off[2],
-                    astat + L.stat_off[1], 1.f, s, ACMI_PROF_CONV2_WGRAD);
+    rc = band_layer(a->a1, 20, 20, 32, 4, 4, 2, bw->d2, 64, B, part, band_cap, grads + L.off[2],
+                    astat + L.stat_off[1], 1.f, sc_c2, s, ACMI_PROF_CONV2_WGRAD);
   else
     rc = wgrad_layer(ConvRows<float, 20, 20, 32, 4, 4, 2>{a->a1, 400 * 32, B * 81}, 512,
                      81LL * B, bw->d2, 64, 64, st, part, ws_cap, grads + L.off[2], 64, nullptr,
@@ -1190,13 +1103,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
     rc = wgrad_layer(ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>{obs, (uint32_t)img_stride, B * 400}, 256,
                      400LL * B, bw->d1, 32, 32, false, part, ws_cap, grads + L.off[0], 32, nullptr,
                      nullptr, s, ACMI_PROF_CONV1_WGRAD, 1.0f / 255.0f);  // raw u8 patches
-  if (rc || !st) return rc;
-  if (side) {  // join the conv1 A factor
-    ACMI_REQUIRE(hipEventRecord(side->join, side->s) == hipSuccess &&
-                     hipStreamWaitEvent(s, side->join, 0) == hipSuccess,
-                 ACMI_ERR_HIP, "acmi_backward: side-stream join failed");
-  }
-  return ACMI_OK;
+  return rc;
 }
 
 // sampled-loss output gradients at the heads (kfac "gradients" mode):
@@ -1291,8 +1198,8 @@ int acmi_set_forward_mode(int mode) {
                mode);
   // the bf16 arithmetic exists only in the fused tower (tower.hpp): refuse a mode
   // the forward could not honour instead of silently computing in f32
-  ACMI_REQUIRE(mode == ACMI_FWD_F32 || (g_gemm_mode == ACMI_GEMM_X3 && tower_on()), ACMI_ERR_ARG,
-               "acmi_set_forward_mode: bf16 forward needs the fused tower (x3 gemm mode, ACMI_TOWER=1)");
+  ACMI_REQUIRE(mode == ACMI_FWD_F32 || g_gemm_mode == ACMI_GEMM_X3, ACMI_ERR_ARG,
+               "acmi_set_forward_mode: bf16 forward needs the fused tower (x3 gemm mode)");
   g_forward_mode = mode;
   return ACMI_OK;
 }

@@ -96,7 +96,7 @@ constexpr int kX3Part = kX3Rows * kX3RowBytes;
 constexpr int kX3Buf = 3 * kX3Part;         // h, m, l
 constexpr int symred3_lds_bytes() { return 2 * kX3Buf; }
 
-template <class Op, class Epi, int DBG = 0>
+template <class Op, class Epi>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 void symred3_kernel(Op op, Epi epi, SymPlan plan, int I, int J, int K, int k_chunk) {
   constexpr int BK = kX3Rows;
@@ -160,17 +160,10 @@ void symred3_kernel(Op op, Epi epi, SymPlan plan, int I, int J, int K, int k_chu
       csum[6] += x1.z;
       csum[7] += x1.w;
       uint4 h, m, lo;
-      if constexpr (DBG == 1) {  // timing probe: no split (wrong numerics)
-        h = make_uint4(pk_bf16(x0.x, x0.y), pk_bf16(x0.z, x0.w), pk_bf16(x1.x, x1.y),
-                       pk_bf16(x1.z, x1.w));
-        m = h;
-        lo = h;
-      } else {
-        split3(x0.x, x0.y, h.x, m.x, lo.x);
-        split3(x0.z, x0.w, h.y, m.y, lo.y);
-        split3(x1.x, x1.y, h.z, m.z, lo.z);
-        split3(x1.z, x1.w, h.w, m.w, lo.w);
-      }
+      split3(x0.x, x0.y, h.x, m.x, lo.x);
+      split3(x0.z, x0.w, h.y, m.y, lo.y);
+      split3(x1.x, x1.y, h.z, m.z, lo.z);
+      split3(x1.z, x1.w, h.w, m.w, lo.w);
       const int off = k * kX3RowBytes + 16 * (c16 ^ (4 * (k & 3)));
       *reinterpret_cast<uint4*>(s + off) = h;
       *reinterpret_cast<uint4*>(s + kX3Part + off) = m;
@@ -179,7 +172,7 @@ void symred3_kernel(Op op, Epi epi, SymPlan plan, int I, int J, int K, int k_chu
   };
 
   const int sa = G.wa[wave], sb = G.wb[wave];
-  const bool idle = sa < 0 || DBG == 2;  // DBG 2: timing probe without MFMAs
+  const bool idle = sa < 0;
   const int ib = idle ? 0 : G.base[sa];  // row slabs are P slabs: column == row index
   const int jb = idle ? 0 : G.base[sb];
   const bool do_cs = !idle && ib == 0;
@@ -248,181 +241,6 @@ void symred3_kernel(Op op, Epi epi, SymPlan plan, int I, int J, int K, int k_chu
   }
 
   // column sums: [8 k-row threads][256 columns] through the (now free) LDS
-  float* cs = reinterpret_cast<float*>(lds);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) cs[(tid >> 5) * 256 + scol + e] = csum[e];
-  __syncthreads();
-  if (idle) return;
-  store_tile<2, 2>(epi, acc, ib, jb, lane, I, J);
-  if (do_cs) {
-    const int col = 64 * sb + lane;
-    float t = 0.f;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) t += cs[r * 256 + col];
-    if (jb + lane < J) epi.colsum(jb + lane, t);
-  }
-}
-
-// Interleaved variant: loads run two K-tiles ahead, and the three-way split
-// and LDS commit of tile kt+1 (already in registers) are issued between the
-// MFMAs of tile kt (sched_group_barrier: the split VALU fills the MFMA gaps of
-// the same wave instead of a separate commit phase after them).  One barrier
-// per K-tile as before: buffer cur^1 was last read in step kt-1.
-template <class Op, class Epi>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
-void symred3i_kernel(Op op, Epi epi, SymPlan plan, int I, int J, int K, int k_chunk) {
-  constexpr int BK = kX3Rows;
-  constexpr int NR = BK / 8;
-  __shared__ __attribute__((aligned(16))) char lds[2 * kX3Buf];
-
-  const int total = gridDim.x;
-  const int b = blockIdx.x;
-  const int xcd = b & 7, base8 = total >> 3, rem = total & 7;
-  const int l = xcd * base8 + min(xcd, rem) + (b >> 3);
-  const int ng = plan.ngroups;
-  const int bz = l / ng;
-  const SymGroup& G = plan.g[l - bz * ng];
-  set_z(epi, bz);
-  const int kbeg = bz * k_chunk;
-  const int kend = min(K, kbeg + k_chunk);
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int c16 = tid & 31;
-  const int scol = c16 * 8;
-  const int sbase = G.base[scol >> 6];
-  const int jcol = sbase >= 0 ? sbase + (scol & 63) : J;
-  const typename Op::CB c0 = op.col_base(jcol), c1 = op.col_base(jcol + 4);
-  typename Op::St ra[2][NR][2];
-  float csum[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) csum[e] = 0.f;
-  typename Op::It it[NR];
-#pragma unroll
-  for (int rr = 0; rr < NR; ++rr) it[rr] = op.iter(kbeg + (tid >> 5) + 8 * rr);
-
-  auto fetch = [&](int k0, auto S) {
-    constexpr int set = decltype(S)::value;
-#pragma unroll
-    for (int rr = 0; rr < NR; ++rr) {
-      const int k = k0 + (tid >> 5) + 8 * rr;
-      ra[set][rr][0] = op.stage_it(it[rr], c0, k < kend);
-      ra[set][rr][1] = op.stage_it(it[rr], c1, k < kend);
-      op.template advance<BK>(it[rr]);
-    }
-  };
-  auto commit = [&](int buf, auto S) {
-    constexpr int set = decltype(S)::value;
-    char* s = lds + buf * kX3Buf;
-#pragma unroll
-    for (int rr = 0; rr < NR; ++rr) {
-      const int k = (tid >> 5) + 8 * rr;
-      const float4 x0 = finish(ra[set][rr][0]);
-      const float4 x1 = finish(ra[set][rr][1]);
-      csum[0] += x0.x;
-      csum[1] += x0.y;
-      csum[2] += x0.z;
-      csum[3] += x0.w;
-      csum[4] += x1.x;
-      csum[5] += x1.y;
-      csum[6] += x1.z;
-      csum[7] += x1.w;
-      uint4 h, m, lo;
-      split3(x0.x, x0.y, h.x, m.x, lo.x);
-      split3(x0.z, x0.w, h.y, m.y, lo.y);
-      split3(x1.x, x1.y, h.z, m.z, lo.z);
-      split3(x1.z, x1.w, h.w, m.w, lo.w);
-      const int off = k * kX3RowBytes + 16 * (c16 ^ (4 * (k & 3)));
-      *reinterpret_cast<uint4*>(s + off) = h;
-      *reinterpret_cast<uint4*>(s + kX3Part + off) = m;
-      *reinterpret_cast<uint4*>(s + 2 * kX3Part + off) = lo;
-    }
-  };
-
-  const int sa = G.wa[wave], sb = G.wb[wave];
-  const bool idle = sa < 0;
-  const int ib = idle ? 0 : G.base[sa];
-  const int jb = idle ? 0 : G.base[sb];
-  const bool do_cs = !idle && ib == 0;
-  const int q = (lane >> 2) & 3, p = lane & 3, g = (lane >> 4) & 1, kh = lane >> 5;
-  auto slot_off = [&](int colblock) {
-    const int slot = (colblock >> 2) + 4 * g + p;
-    return (8 * kh + q) * kX3RowBytes + 8 * (slot ^ (8 * q));
-  };
-  const int aoff0 = slot_off(64 * (idle ? 0 : sa)), aoff1 = slot_off(64 * (idle ? 0 : sa) + 32);
-  const int boff0 = slot_off(64 * (idle ? 0 : sb)), boff1 = slot_off(64 * (idle ? 0 : sb) + 32);
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[x][y][r] = 0.f;
-
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
-  if (nk > 0) {
-    fetch(kbeg, S0{});
-    fetch(kbeg + BK, S1{});
-    commit(0, S0{});
-  }
-  __syncthreads();
-
-  // step kt: MFMAs on buffer cur; tile kt+1 (register set SN) split + written
-  // to buffer cur^1 in the MFMA gaps; tile kt+2's loads into set SN^1
-  auto step = [&](int kt, int cur, auto MF, auto NTc, auto SN) {
-    constexpr bool mf = decltype(MF)::value;
-    constexpr int NT = decltype(NTc)::value;
-    constexpr int sn = decltype(SN)::value;
-    fetch(kbeg + (kt + 2) * BK, std::integral_constant<int, sn ^ 1>{});
-    if constexpr (mf) {
-      const char* s = lds + cur * kX3Buf;
-      bf16x8 a[2][3], bb[2][3];
-#pragma unroll
-      for (int pt = 0; pt < 3; ++pt) {
-        const char* sp = s + pt * kX3Part;
-        a[0][pt] = cat8(ds_tr16(sp + aoff0), ds_tr16(sp + aoff0 + 4 * kX3RowBytes));
-        a[1][pt] = cat8(ds_tr16(sp + aoff1), ds_tr16(sp + aoff1 + 4 * kX3RowBytes));
-        bb[0][pt] = cat8(ds_tr16(sp + boff0), ds_tr16(sp + boff0 + 4 * kX3RowBytes));
-        if constexpr (NT == 2)
-          bb[1][pt] = cat8(ds_tr16(sp + boff1), ds_tr16(sp + boff1 + 4 * kX3RowBytes));
-      }
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < NT; ++tn) acc[tm][tn] = mfma_x3(a[tm], bb[tn], acc[tm][tn]);
-      if (kt + 1 < nk) commit(cur ^ 1, SN);
-      // interleave: loads, fragment reads, then one MFMA per 5 VALU
-      __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 6 * (2 + NT), 0);
-#pragma unroll
-      for (int i = 0; i < 6 * 2 * NT; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-      }
-    } else {
-      if (kt + 1 < nk) commit(cur ^ 1, SN);
-    }
-    __syncthreads();
-  };
-  using T = std::integral_constant<bool, true>;
-  using F = std::integral_constant<bool, false>;
-  using N2 = std::integral_constant<int, 2>;
-  using N1 = std::integral_constant<int, 1>;
-  const bool half = jb + 32 >= J;
-  auto run = [&](auto MF, auto NTc) {
-    for (int kt = 0; kt < nk; kt += 2) {
-      step(kt, 0, MF, NTc, S1{});
-      if (kt + 1 < nk) step(kt + 1, 1, MF, NTc, S0{});
-    }
-  };
-  if (idle) run(F{}, N2{});
-  else if (half) run(T{}, N1{});
-  else run(T{}, N2{});
-
   float* cs = reinterpret_cast<float*>(lds);
 #pragma unroll
   for (int e = 0; e < 8; ++e) cs[(tid >> 5) * 256 + scol + e] = csum[e];
@@ -930,24 +748,18 @@ inline bool sym_plan6_greedy(int K, int cout_pad, SymPlan6* p) {
 // instead of after both sub-tiles.  With one 512-thread block per CU the two
 // waves of a SIMD share the block's barrier phase, so without this a SIMD's
 // MFMA pipe idles through every commit.
-// Plan = SymPlan6 (by value: groups over the upper triangle, dense partials
-// [chunk][I+1][J] through store_tile) or BandPlanDev (band.hpp: groups in device
-// memory, each sub-tile stored to its compact slot [chunk][tile][64][64] and
-// each slab's column sums by its owning group, EpiBand).
-template <class Op, class Epi, bool PIPE = false, class Plan = SymPlan6>
+// The plan (by value) covers the upper triangle with groups; dense partials
+// [chunk][I+1][J] through store_tile.
+template <class Op, class Epi, bool PIPE = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-void symred6_kernel(Op op, Epi epi, Plan plan, int I, int J, int K, int k_chunk) {
-  constexpr bool kBand = !std::is_same<Plan, SymPlan6>::value;
+void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_chunk) {
   constexpr int BK = kX3Rows;
   __shared__ __attribute__((aligned(16))) char lds[2 * kSixBuf];
 
   const int total = gridDim.x;
   const int b = blockIdx.x;
   const int xcd = b & 7, base8 = total >> 3, rem = total & 7;
-  int l = xcd * base8 + min(xcd, rem) + (b >> 3);
-  if constexpr (kBand) {
-    if (!plan.xcd_remap) l = b;  // dispatch order: every XCD on the same chunk of rows
-  }
+  const int l = xcd * base8 + min(xcd, rem) + (b >> 3);
   const int ng = plan.ngroups;
   const int bz = l / ng;
   const auto& G = plan.g[l - bz * ng];
@@ -1123,29 +935,7 @@ void symred6_kernel(Op op, Epi epi, Plan plan, int I, int J, int K, int k_chunk)
 #pragma unroll
   for (int e = 0; e < 12; ++e) cs[srow * 384 + scol + e] = csum[e];
   __syncthreads();
-  if constexpr (kBand) {
-    const int khalf = lane >> 5;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if (t >= ntile) break;
-      float* dst = epi.part + ((long long)bz * epi.ntiles + G.tile[wave][t]) * 4096;
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < 2; ++tn)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            dst[(32 * tm + (r & 3) + 8 * (r >> 2) + 4 * khalf) * 64 + 32 * tn + (lane & 31)] =
-                acc[t][tm][tn][r];
-    }
-    if (wave < 6 && ((G.csown >> wave) & 1)) {  // this group owns staged slab `wave`'s sums
-      const int col = 64 * wave + lane;
-      float v = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v += cs[r * 384 + col];
-      epi.cs[(long long)bz * epi.ncols + G.base[wave] + lane] = v;
-    }
-  } else {
+  {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       if (t >= ntile) break;
@@ -1161,48 +951,23 @@ void symred6_kernel(Op op, Epi epi, Plan plan, int I, int J, int K, int k_chunk)
   }
 }
 
-inline int symred_variant();
 template <class Op, class Epi>
 inline void launch_symred6(const Op& op, const Epi& e, const SymPlan6& plan, int I, int J, int K,
                            int nchunk, int k_chunk, hipStream_t s) {
-  if (symred_variant() != 5)
-    hipLaunchKernelGGL((symred6_kernel<Op, Epi, true>), dim3(plan.ngroups * nchunk), dim3(512), 0, s,
-                       op, e, plan, I, J, K, k_chunk);
-  else
-    hipLaunchKernelGGL((symred6_kernel<Op, Epi, false>), dim3(plan.ngroups * nchunk), dim3(512), 0, s,
-                       op, e, plan, I, J, K, k_chunk);
+  hipLaunchKernelGGL((symred6_kernel<Op, Epi, true>), dim3(plan.ngroups * nchunk), dim3(512), 0, s, op, e,
+                     plan, I, J, K, k_chunk);
 }
 
-// ACMI_SYMRED: default six-slab groups (symred6_kernel, PIPE) where sym_plan6
-// has a covering; =s the same without PIPE; =4 four-slab groups
-// (symred3_kernel); =i its interleaved variant; =n / =m its no-split / no-MFMA
-// timing probes (wrong results).  Measured at the bench shape (conv2, M =
-// 10240): six PIPE 1.27 ms, six 1.36, four 1.52, four interleaved 1.50, four
-// without the split 1.43, four without MFMAs 0.87.
-inline int symred_variant() {
-  static const int v = [] {
-    const char* e = getenv("ACMI_SYMRED");
-    return !e ? 0 : e[0] == 'i' ? 1 : e[0] == 'n' ? 2 : e[0] == 'm' ? 3 : e[0] == '4' ? 4 : e[0] == 's' ? 5 : 0;
-  }();
-  return v;
-}
-
+// Six-slab groups (symred6_kernel, loads two K-tiles ahead) where sym_plan6 has
+// a covering, else four-slab groups (symred3_kernel).  Measured at the bench
+// shape (conv2 patch rows, M = 10240): six 1.27 ms, six without the two-ahead
+// loads 1.36, four 1.52, four with interleaved tiles 1.50; timing probes of the
+// four-slab kernel without the operand split 1.43, without MFMAs 0.87.
 template <class Op, class Epi>
 inline void launch_symred3(const Op& op, const Epi& e, const SymPlan& plan, int I, int J, int K,
                            int nchunk, int k_chunk, hipStream_t s) {
-  const int v = symred_variant();
-  if (v == 1)
-    hipLaunchKernelGGL((symred3i_kernel<Op, Epi>), dim3(plan.ngroups * nchunk), dim3(256), 0, s, op,
-                       e, plan, I, J, K, k_chunk);
-  else if (v == 2)
-    hipLaunchKernelGGL((symred3_kernel<Op, Epi, 1>), dim3(plan.ngroups * nchunk), dim3(256), 0, s, op,
-                       e, plan, I, J, K, k_chunk);
-  else if (v == 3)
-    hipLaunchKernelGGL((symred3_kernel<Op, Epi, 2>), dim3(plan.ngroups * nchunk), dim3(256), 0, s, op,
-                       e, plan, I, J, K, k_chunk);
-  else
-    hipLaunchKernelGGL((symred3_kernel<Op, Epi>), dim3(plan.ngroups * nchunk), dim3(256), 0, s, op,
-                       e, plan, I, J, K, k_chunk);
+  hipLaunchKernelGGL((symred3_kernel<Op, Epi>), dim3(plan.ngroups * nchunk), dim3(256), 0, s, op, e, plan, I, J,
+                     K, k_chunk);
 }
 
 }  // namespace acmi

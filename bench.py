@@ -62,6 +62,21 @@ def measured_traffic(kernel, workload):
     return None
 
 
+def workload_name(algo, N, T, A, forward, world):
+    """The BASELINE.json config a line measures (configs[1]-[4]; others: as given)."""
+    if forward == 'bf16':
+        return ('Atari {} {} envs/GPU x {} steps, {} actions, bf16 forward / fp32 K-FAC (BASELINE configs[4] '
+                'shard)'.format(algo.upper(), N, T, A))
+    name = 'Breakout {} {} envs/GPU x {} steps'.format(algo.upper(), N, T)
+    if algo == 'a2c' and N * world == 32 and T == 5:
+        return name + ' (BASELINE configs[1])'
+    if algo == 'acktr' and N * world == 32 and T == 20:
+        return name + ' (BASELINE configs[2])'
+    if algo == 'acktr' and N == 512 and T == 20:
+        return name + ' (BASELINE configs[3] shard)'
+    return name
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
@@ -75,7 +90,7 @@ def parse():
                    help='conv tower precision (default: ACMI_FORWARD or f32; bf16: BASELINE configs[4] '
                         '"bf16 forward / fp32 KFAC factors")')
     p.add_argument('--no-cpu-baseline', action='store_true')
-    p.add_argument('--cpu-iters', type=int, default=3)
+    p.add_argument('--cpu-iters', type=int, default=3, help='timed CPU-baseline iterations (at most ~20 s)')
     p.add_argument('--quiet', action='store_true')
     return p.parse_args()
 
@@ -270,12 +285,14 @@ def run(args):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, 'oracle'))
         import cpu_baseline
-        r = cpu_baseline.run(n_envs=32, n_steps=20 if acktr else 5, iters=args.cpu_iters, A=A, C3=C3)
+        # the same workload as the GPU line (envs, steps, algorithm, actions, C3)
+        r = cpu_baseline.run(n_envs=N, n_steps=T, iters=args.cpu_iters, A=A, C3=C3, algo=args.algo)
         cpu = {'value': r['env_steps_per_s'], 'unit': 'env-steps/s', 'cores': r['threads'], 'kind': 'port',
-               'sample': '{} iterations of the reference {} config ({} envs x {} steps), numpy float32 '
-                         'oracle port, inverse amortised 1/10'.format(r['iters'], args.algo.upper(),
-                                                                      r['n_envs'], r['n_steps']),
-               'update_ms': r['update_ms']}
+               'sample': '{} timed iterations (after one warm-up) of the same {} workload ({} envs x {} steps): '
+                         'torch-CPU fp32 restatement, {}{}'.format(
+                             r['iters'], args.algo.upper(), r['n_envs'], r['n_steps'], r['structure'],
+                             ', K-FAC inverse timed once and amortised 1/10' if acktr else ''),
+               'update_ms': r['update_ms'], 'rollout_ms': r['rollout_ms']}
 
     if rank == 0:
         out = {
@@ -283,10 +300,8 @@ def run(args):
             'value': value, 'unit': 'env-steps/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': ms_per_step, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
             'dtype': 'fp32' if args.forward == 'f32' else 'bf16 forward / fp32 update', 'data': 'synthetic (hashed 84x84 u8 frames, random-init orthogonal weights)',
-            'config': {'workload': ('Breakout {} {} envs/GPU x {} steps (BASELINE configs[3] shard)'.format(
-                args.algo.upper(), N, T) if args.forward == 'f32' else
-                'Atari {} {} envs/GPU x {} steps, {} actions, bf16 forward / fp32 K-FAC (BASELINE configs[4] '
-                'shard)'.format(args.algo.upper(), N, T, A)), 'algo': args.algo, 'envs_per_gpu': N, 'num_steps': T,
+            'config': {'workload': workload_name(args.algo, N, T, A, args.forward, world), 'algo': args.algo,
+                       'envs_per_gpu': N, 'num_steps': T,
                 'global_envs': N * world, 'num_actions': A, 'conv3_filters': C3, 'forward': args.forward,
                 'parallelism': 'dp{}'.format(world)},
             'update_ms': mean(upd_ms), 'update_ms_inverse_iters': mean(upd_inv),

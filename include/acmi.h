@@ -58,7 +58,7 @@ int acmi_get_gemm_mode(void);
  * read the activations the forward produced.  Initial mode from ACMI_FORWARD
  * ("bf16" / "f32").  Not stream-ordered: set it between launches.
  * The bf16 arithmetic lives in the fused conv tower only: setting ACMI_FWD_BF16
- * fails (ACMI_ERR_ARG) in ACMI_GEMM_F32 mode or with ACMI_TOWER=0, and a forward
+ * fails (ACMI_ERR_ARG) in ACMI_GEMM_F32 mode, and a forward
  * in that mode fails on observations or an image stride that are not 16-byte
  * aligned -- the mode is never silently ignored. */
 #define ACMI_FWD_F32 0

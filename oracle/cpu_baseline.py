@@ -1,107 +1,293 @@
-"""CPU baseline for bench.py — test/measurement infrastructure, never the product path.
+"""CPU baseline for bench.py -- test/measurement infrastructure, never the product path.
 
-A float32 numpy run of the oracle's restatement of the reference's ACKTR iteration with
-the reference's structure (a2c_acktr.py:104-137): a T-step rollout that per step runs
-the tower on the N current observations (model.py:149-151), samples, and steps N
-synthetic Atari envs with the reference wrapper semantics; then one update: forward on
-the N*T batch, n-step targets, A2C losses and head gradients, backward fused with the
-K-FAC A factors, the sampled-loss backward for the G factors, EMA, natural-gradient
-step; the damped inverses (every 10 updates in the reference schedule) are timed once
-and amortised at 1/10 per update.  Threads: whatever OpenBLAS uses (reported).
+The reference (TensorFlow 1.x + kfac + gym, a2c_acktr.py) cannot run here or on the
+GPU box, so the baseline is a restatement with the reference's process structure and
+arithmetic placement (kind "port"):
 
-The reference itself (TensorFlow 1.x + kfac + gym) cannot run here or on the GPU box,
-so this port is the baseline (kind "port").
+* environments: one synthetic Atari game per env producing 84x84x1 u8 frames (the
+  same counter-hash frames, rewards and episode lengths as the device stepper and
+  oracle.SyntheticAtari) inside ``EpisodeInfoWrapper`` semantics; with ``ipc`` each
+  game runs in its own child process behind the reference's ``SubprocessEnv`` Pipe
+  protocol (actorcritic.multi_env, the restatement of multi_env.py:140-362), the
+  4-frame stack is kept in the parent (FrameStackWrapper, a2c_acktr.py:170-171) and
+  ``MultiEnv`` fans the steps out over a ThreadPoolExecutor(N) with the lazy
+  auto-reset (multi_env.py:18-89); without ``ipc`` (large N: one process per env is
+  not practical at 512 envs) the same wrapped games step in-process on the pool;
+* rollout: T serial batch-N forwards + categorical draws (agents.py:202-216,
+  model.py:149-151);
+* update (a2c_acktr.py:117-126): forward over the N*T batch and the bootstrap
+  observations, the n-step targets of objectives.py:178-214, the A2C losses
+  (objectives.py:123-154), the backward; ACKTR: the K-FAC A factors (patch Grams),
+  the sampled-loss backward for the G factors, the EMA, the damped inverses every 10
+  updates (timed once, amortised 1/10), the preconditioned trust-region momentum
+  step (DESIGN.md section 4 conventions); A2C: global-norm clip 0.5 + RMSProp;
+* arithmetic: torch on the CPU in float32 (oneDNN convolutions, BLAS GEMMs) on every
+  core this process may use (torch.set_num_threads).
 """
 
+import functools
 import os
 import sys
 import time
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
 import oracle  # noqa: E402
 
+_ROOT = os.path.dirname(HERE)
+_PKG = os.path.join(_ROOT, 'actor-critic_amd')
+if _PKG not in sys.path:
+    sys.path.insert(0, _PKG)
 
-def blas_threads():
+
+def cpu_threads():
+    """Cores this process may use (the GPU box's CPU share), capped by OMP_NUM_THREADS."""
     try:
-        from threadpoolctl import threadpool_info
-        n = [i.get('num_threads') for i in threadpool_info() if i.get('user_api') == 'blas']
-        if n:
-            return int(n[0])
-    except Exception:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    if os.environ.get('OMP_NUM_THREADS', '').isdigit():
+        n = min(n, int(os.environ['OMP_NUM_THREADS']))
+    return max(1, n)
+
+
+class _Discrete(object):
+    def __init__(self, n):
+        self.n = n
+
+
+class _Box(object):
+    def __init__(self, shape):
+        self.low = np.zeros(shape, np.uint8)
+        self.high = np.full(shape, 255, np.uint8)
+        self.shape = shape
+        self.dtype = np.dtype(np.uint8)
+
+
+class SyntheticRawAtari(object):
+    """One synthetic game, raw 84x84x1 frames, with EpisodeInfoWrapper's episode total
+    in info (wrappers.py:263-294).  Frames/rewards/lengths: oracle.SyntheticAtari's."""
+
+    def __init__(self, seed, env_id, num_actions):
+        self.seed, self.e = seed, env_id
+        self.k, self.t, self.total = -1, 0, 0.0
+        self.L = 0
+        self.action_space = _Discrete(num_actions)
+        self.observation_space = _Box((84, 84, 1))
+
+    def reset(self):
+        self.k += 1
+        self.t, self.total = 0, 0.0
+        self.L = oracle.episode_length(self.seed, self.e, self.k)
+        return oracle.reset_frame(self.seed, self.e, self.k)[..., None]
+
+    def step(self, action):
+        self.t += 1
+        a = int(action) & 255
+        base = int(oracle.key4(self.seed, self.e, self.k, self.t * 256 + a))
+        rh = int(oracle.mix32(np.uint32(base) ^ oracle.REW_SALT)) >> 8
+        r = -1.0 if rh < oracle.REW_LO else (1.0 if rh >= oracle.REW_HI else 0.0)
+        term = self.t >= self.L
+        self.total += r
+        info = {}
+        if term:
+            info['episode'] = {'total_reward': self.total}
+            self.total = 0.0
+        return oracle._frame(base)[..., None], r, term, info
+
+    def close(self):
         pass
-    for var in ('OPENBLAS_NUM_THREADS', 'OMP_NUM_THREADS'):
-        if os.environ.get(var):
-            return int(os.environ[var])
-    return os.cpu_count() or 1
 
 
-def run(n_envs=32, n_steps=20, iters=3, A=4, C3=32, seed=0, time_budget_s=30.0):
-    f32 = np.float32
-    params = oracle.init_params(A, C3, seed).astype(f32)
+def make_raw_env(seed, env_id, num_actions):
+    return SyntheticRawAtari(seed, env_id, num_actions)
+
+
+def make_envs(n_envs, num_actions, seed, ipc):
+    from actorcritic.envs.atari.wrappers import FrameStackWrapper
+    from actorcritic.multi_env import MultiEnv, create_subprocess_envs
+    fns = [functools.partial(make_raw_env, seed, e, num_actions) for e in range(n_envs)]
+    raw = create_subprocess_envs(fns) if ipc else [fn() for fn in fns]
+    return MultiEnv([FrameStackWrapper(env, 4) for env in raw])
+
+
+class TorchNet(object):
+    """The Nature CNN of envs/atari/model.py:173-217 in torch fp32 on the CPU, on the
+    flat parameter layout of the GPU engine (HWIO convs, [in, out] FCs)."""
+
+    def __init__(self, params, A, C3):
+        import torch
+        self.torch = torch
+        self.A, self.C3 = A, C3
+        off, n = oracle.param_offsets(A, C3)
+        shapes = [s for pair in oracle.layer_shapes(A, C3) for s in pair]
+        ends = list(off[1:]) + [n]
+        flat = torch.from_numpy(np.asarray(params, np.float32).copy())
+        self.blocks = [flat[o:e].reshape(s).clone().requires_grad_(True) for o, e, s in zip(off, ends, shapes)]
+
+    def forward(self, obs, grad):
+        torch = self.torch
+        F = torch.nn.functional
+        w1, b1, w2, b2, w3, b3, w4, b4, wp, bp, wv, bv = self.blocks
+        with torch.set_grad_enabled(grad):
+            x = torch.from_numpy(np.ascontiguousarray(obs)).permute(0, 3, 1, 2).float() / 255.0
+            z1 = F.conv2d(x, w1.permute(3, 2, 0, 1), b1, stride=4)
+            a1 = torch.relu(z1)
+            z2 = F.conv2d(a1, w2.permute(3, 2, 0, 1), b2, stride=2)
+            a2 = torch.relu(z2)
+            z3 = F.conv2d(a2, w3.permute(3, 2, 0, 1), b3, stride=1)
+            a3 = torch.relu(z3)
+            a3f = a3.permute(0, 2, 3, 1).reshape(a3.shape[0], -1)  # NHWC flatten (model.py:197-206)
+            z4 = a3f @ w4 + b4
+            a4 = torch.relu(z4)
+            logits = a4 @ wp + bp
+            value = (a4 @ wv + bv)[:, 0]
+        return dict(x=x, z1=z1, a1=a1, z2=z2, a2=a2, z3=z3, a3=a3, a3f=a3f, z4=z4, a4=a4, logits=logits,
+                    value=value)
+
+    def a_factors(self, fw):
+        """[x;1]^T[x;1] / rows per layer; conv rows = every location, columns (kh, kw, c)."""
+        torch = self.torch
+        nhwc = lambda t: t.permute(0, 2, 3, 1)
+
+        def patches(x, k, s):
+            p = x.unfold(1, k, s).unfold(2, k, s)
+            return p.permute(0, 1, 2, 4, 5, 3).reshape(-1, k * k * x.shape[-1])
+
+        ins = [patches(nhwc(fw['x']), 8, 4), patches(nhwc(fw['a1']), 4, 2), patches(nhwc(fw['a2']), 3, 1),
+               fw['a3f'], fw['a4']]
+        out = []
+        for xin in ins:
+            xin = xin.detach()
+            xb = torch.cat([xin, torch.ones(xin.shape[0], 1)], 1)
+            out.append(xb.t() @ xb / xb.shape[0])
+        return out
+
+
+def _sample(torch, logits, gen):
+    p = torch.softmax(logits, -1)
+    return torch.multinomial(p, 1, generator=gen)[:, 0]
+
+
+def run(n_envs=32, n_steps=20, iters=3, A=4, C3=32, algo='acktr', seed=0, time_budget_s=20.0, ipc=None,
+        threads=None):
+    """Times warm-up + up to `iters` iterations (at most ~time_budget_s); returns
+    env-steps/s and the update / rollout split."""
+    import torch
+    threads = threads or cpu_threads()
+    torch.set_num_threads(threads)
+    if ipc is None:
+        ipc = n_envs <= 64
+    acktr = algo == 'acktr'
+    gen = torch.Generator().manual_seed(seed)
+    net = TorchNet(oracle.init_params(A, C3, seed), A, C3)
+    W = net.blocks
     din, dout = oracle.kfac_dims(A, C3)
-    envs = [oracle.SyntheticAtari(seed, e) for e in range(n_envs)]
-    obs = np.stack([e.reset() for e in envs])
-    factors_A = [np.zeros((d, d), f32) for d in din[:5]]
-    factors_G = [np.zeros((d, d), f32) for d in dout]
-    inverses = [(np.eye(din[l], dtype=f32), np.eye(dout[l], dtype=f32)) for l in range(6)]
-    velocity = np.zeros_like(params)
-    gp_gamma = 0.99
-    rollout_s = update_s = 0.0
-    done_iters = 0
+    fac_A = [torch.zeros(d, d) for d in din[:5]]
+    fac_G = [torch.zeros(d, d) for d in dout]
+    inverses = [(torch.eye(din[l]), torch.eye(dout[l])) for l in range(6)]
+    vel = [torch.zeros_like(w) for w in W]
+    ms = [torch.ones_like(w) for w in W]
+    gamma, beta, lr_acktr, lr_a2c = 0.99, 0.01, 0.25, 7e-4
+    env = make_envs(n_envs, A, seed, ipc)
+    obs = np.stack(env.reset())
+    stats = dict(rollout=0.0, update=0.0, n=0)
+    inv_s = 0.0
     t_start = time.perf_counter()
-    for it in range(iters):
-        t0 = time.perf_counter()
-        ob_steps = np.zeros((n_envs, n_steps, 84, 84, 4), np.uint8)
-        actions = np.zeros((n_envs, n_steps), np.int64)
-        rewards = np.zeros((n_envs, n_steps), f32)
-        terms = np.zeros((n_envs, n_steps), bool)
-        for t in range(n_steps):
-            ob_steps[:, t] = obs
-            fw = oracle.forward(params, obs, A, C3, dtype=f32)
-            u = oracle.sample_uniforms(seed, 0, it * n_steps + t, n_envs)
-            a = oracle.sample_f32(fw['logits'], u)
-            actions[:, t] = a
-            nxt = []
-            for n, env in enumerate(envs):
-                o, r, d, _ = env.step(a[n])
-                nxt.append(o)
-                rewards[n, t], terms[n, t] = r, d
-            obs = np.stack(nxt)
-        t1 = time.perf_counter()
-        M = n_envs * n_steps
-        fw = oracle.forward(params, ob_steps.reshape(M, 84, 84, 4), A, C3, dtype=f32)
-        vb = oracle.forward(params, obs, A, C3, dtype=f32)['value']
-        tg = oracle.targets_f64(rewards, terms, vb, gp_gamma).astype(f32).reshape(-1)
-        lg = oracle.a2c_loss_and_head_grads(fw['logits'], fw['value'], actions.reshape(-1), tg)
-        grads, _, afac = oracle.backward(params, fw, lg['dlogits'].astype(f32), lg['dvalue'].astype(f32), A, C3,
-                                         dtype=f32, with_a_factors=True)
-        g_pi, g_v, _ = oracle.sampled_head_grads(fw['logits'], 0x4b464143, 0, it)
-        gfac = oracle.g_factors(params, fw, g_pi.astype(f32), g_v.astype(f32), A, C3, dtype=f32)
-        decay = f32(0.99)
-        factors_A = [decay * F + (1 - decay) * S.astype(f32) for F, S in zip(factors_A, afac)]
-        factors_G = [decay * F + (1 - decay) * S.astype(f32) for F, S in zip(factors_G, gfac)]
-        params, velocity, _, _ = oracle.kfac_step(params, velocity, grads, inverses, 0.25, 0.9, 1e-4, A, C3)
-        params, velocity = params.astype(f32), velocity.astype(f32)
-        t2 = time.perf_counter()
-        rollout_s += t1 - t0
-        update_s += t2 - t1
-        done_iters += 1
-        if time.perf_counter() - t_start > time_budget_s:
-            break
-    # damped inverses, timed once, amortised over invert_every = 10 updates
-    t3 = time.perf_counter()
-    inverses = [(Ai.astype(f32), Gi.astype(f32)) for Ai, Gi in
-                oracle.damped_inverses([F.astype(np.float64) for F in factors_A],
-                                       [F.astype(np.float64) for F in factors_G], 0.01)]
-    inv_s = time.perf_counter() - t3
-    per_iter = (rollout_s + update_s) / done_iters + inv_s / 10.0
-    steps = n_envs * n_steps
-    return dict(env_steps_per_s=steps / per_iter, update_ms=1e3 * (update_s / done_iters + inv_s / 10.0),
-                rollout_ms=1e3 * rollout_s / done_iters, inverse_ms=1e3 * inv_s, iters=done_iters,
-                threads=blas_threads(), n_envs=n_envs, n_steps=n_steps)
+    try:
+        for it in range(iters + 1):  # iteration 0: warm-up (oneDNN primitives, pools)
+            t0 = time.perf_counter()
+            ob_steps = np.zeros((n_envs, n_steps, 84, 84, 4), np.uint8)
+            actions = np.zeros((n_envs, n_steps), np.int64)
+            rewards = np.zeros((n_envs, n_steps), np.float32)
+            terms = np.zeros((n_envs, n_steps), bool)
+            for t in range(n_steps):
+                ob_steps[:, t] = obs
+                a = _sample(torch, net.forward(obs, False)['logits'], gen).numpy()
+                nxt, r, d, _ = env.step(a.tolist())
+                obs = np.stack(nxt)
+                actions[:, t], rewards[:, t], terms[:, t] = a, r, d
+            t1 = time.perf_counter()
+            M = n_envs * n_steps
+            fw = net.forward(ob_steps.reshape(M, 84, 84, 4), True)
+            vb = net.forward(obs, False)['value'].numpy()
+            tg = torch.from_numpy(oracle.targets_f64(rewards, terms, vb, gamma).astype(np.float32).reshape(-1))
+            logits, value = fw['logits'], fw['value']
+            logp_all = torch.log_softmax(logits, -1)
+            logp = logp_all.gather(1, torch.from_numpy(actions.reshape(-1, 1)))[:, 0]
+            ent = -(logp_all.exp() * logp_all).sum(-1)
+            adv = tg - value.detach()
+            l_pi = -((adv * logp).mean() + beta * ent.mean())
+            l_v = ((tg - value) ** 2 / 2).mean()
+            grads = torch.autograd.grad(l_pi + 0.5 * l_v, W, retain_graph=acktr)
+            with torch.no_grad():
+                if acktr:
+                    # K-FAC statistics: A from the layer inputs, G from the sampled losses
+                    ys = _sample(torch, logits.detach(), gen)
+                    yv = value.detach() + torch.randn(M, generator=gen)
+                    with torch.enable_grad():
+                        ls = -torch.log_softmax(logits, -1).gather(1, ys[:, None]).sum() + \
+                            ((yv - value) ** 2 / 2).sum()
+                        gz = torch.autograd.grad(ls, [fw['z1'], fw['z2'], fw['z3'], fw['z4'], logits, value])
+                    gs = [g.permute(0, 2, 3, 1).reshape(-1, g.shape[1]) for g in gz[:3]] + [gz[3], gz[4],
+                                                                                             gz[5][:, None]]
+                    stat_A = net.a_factors(fw)
+                    stat_G = [g.t() @ g / g.shape[0] for g in gs]
+                    fac_A = [0.99 * F_ + 0.01 * S for F_, S in zip(fac_A, stat_A)]
+                    fac_G = [0.99 * F_ + 0.01 * S for F_, S in zip(fac_G, stat_G)]
+                    pre = []
+                    for l in range(6):
+                        gb = torch.cat([grads[2 * l].reshape(din[l] - 1, dout[l]), grads[2 * l + 1].reshape(1, -1)])
+                        Ai, Gi = inverses[l]
+                        pre.append(Ai @ gb @ Gi)
+                    sq = sum(float((torch.cat([grads[2 * l].reshape(din[l] - 1, dout[l]),
+                                               grads[2 * l + 1].reshape(1, -1)]) * pre[l]).sum()) for l in range(6))
+                    coeff = min(1.0, (1e-4 / (sq * lr_acktr * lr_acktr)) ** 0.5) if sq > 0 else 1.0
+                    for l in range(6):
+                        for j, part in ((2 * l, pre[l][:-1].reshape(W[2 * l].shape)),
+                                        (2 * l + 1, pre[l][-1].reshape(W[2 * l + 1].shape))):
+                            vel[j].mul_(0.9).add_(part, alpha=coeff)
+                            W[j].sub_(lr_acktr * vel[j])
+                else:
+                    norm = float(torch.sqrt(sum((g * g).sum() for g in grads)))
+                    scale = 0.5 / max(norm, 0.5)
+                    for w, g, m in zip(W, grads, ms):
+                        g = g * scale
+                        m.mul_(0.9).addcmul_(g, g, value=0.1)
+                        w.sub_(lr_a2c * g / torch.sqrt(m + 1e-10))
+            t2 = time.perf_counter()
+            if it > 0:
+                stats['rollout'] += t1 - t0
+                stats['update'] += t2 - t1
+                stats['n'] += 1
+                if time.perf_counter() - t_start > time_budget_s:
+                    break
+        if acktr:  # the damped inverses (every 10 updates), timed once, amortised
+            t3 = time.perf_counter()
+            with torch.no_grad():
+                for l in range(6):
+                    A_, G_ = fac_A[min(l, 4)], fac_G[l]
+                    pi = float(torch.sqrt((torch.trace(A_) / A_.shape[0]) / (torch.trace(G_) / G_.shape[0]).clamp_min(
+                        1e-30)))
+                    inverses[l] = (torch.linalg.inv(A_ + pi * 0.1 * torch.eye(A_.shape[0])),
+                                   torch.linalg.inv(G_ + 0.1 / pi * torch.eye(G_.shape[0])))
+            inv_s = time.perf_counter() - t3
+    finally:
+        env.close()
+    n = max(1, stats['n'])
+    per_iter = (stats['rollout'] + stats['update']) / n + inv_s / 10.0
+    return dict(env_steps_per_s=n_envs * n_steps / per_iter, update_ms=1e3 * (stats['update'] / n + inv_s / 10.0),
+                rollout_ms=1e3 * stats['rollout'] / n, inverse_ms=1e3 * inv_s, iters=stats['n'], threads=threads,
+                n_envs=n_envs, n_steps=n_steps, ipc=ipc, algo=algo,
+                structure=('{} SubprocessEnv children (Pipe protocol) + ThreadPoolExecutor({})'.format(n_envs, n_envs)
+                           if ipc else '{} in-process envs on a ThreadPoolExecutor({})'.format(n_envs, n_envs)))
 
 
 if __name__ == '__main__':
-    print(run(iters=int(sys.argv[1]) if len(sys.argv) > 1 else 2))
+    import json
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+    algo = sys.argv[2] if len(sys.argv) > 2 else 'acktr'
+    print(json.dumps(run(n_envs=n, n_steps=20 if algo == 'acktr' else 5, C3=32 if algo == 'acktr' else 64,
+                         algo=algo, iters=3)))

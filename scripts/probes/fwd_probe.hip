@@ -7,7 +7,7 @@
 #include <vector>
 #include <algorithm>
 
-#include "../../actor-critic_amd/csrc/gemm_stream.hpp"
+#include "gemm_stream.hpp"
 #include "wsgemm.hpp"
 #include "../../actor-critic_amd/csrc/conv1u8.hpp"
 

@@ -7,7 +7,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "../../actor-critic_amd/csrc/gemm_stream.hpp"
+#include "gemm_stream.hpp"
 
 namespace acmi {
 void set_error(const char*, ...) {}
