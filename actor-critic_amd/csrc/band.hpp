@@ -24,7 +24,8 @@
 // tile is multiplied by 1/(s_a s_b) (exact) when it is stored.  The scales put
 // each tensor's bound at 2^14 < 65504: X from the layer's weights (a1, a2 are
 // ReLU outputs of [0,1] pixels, bounded by the positive weight mass,
-// band_bounds_kernel), dY from its exact max (band_absmax_kernel).  Elements far
+// band_bounds_kernel), dY from its exact max (published by the dX epilogues that
+// produce it, gemm.hpp has_amax).  Elements far
 // below the bound lose relative precision only where their absolute error
 // (<= 2^-25 in scaled units) is < 2^-30 of the bound.  Three MFMAs per product
 // instead of bf16x3's six: the same f32-class sums (accumulation error,
@@ -139,11 +140,12 @@ inline void band_chunks(long long rows, int ngroups, int* nc, int* ch) {
   *nc = (int)((rows + c - 1) / c);
 }
 
-// band scratch (floats, at the end of the backward's partial region): scales
-// [s_a1, s_a2, s_d2, s_d3], |d2| / |d3| max bits, the two layers' (s_X, s_dY)
+// band scratch (kBandScratch words at the end of the backward's partial region,
+// zeroed before the dX chain): the bit patterns of max |d3|, |d2| (published by
+// the dX epilogues, gemm.hpp has_amax) and of the a1 / a2 bounds
+// (band_bounds_kernel); the kernels turn them into their operand scales
 constexpr int kBandScratch = 64;
-enum { kBsA1 = 0, kBsA2 = 1, kBsD2 = 2, kBsD3 = 3, kBsMaxD2 = 4, kBsMaxD3 = 5, kBsQueue = 8,
-       kBsPairC3 = 16, kBsPairC2 = 18 };
+enum { kBsMaxA1 = 0, kBsMaxA2 = 1, kBsMaxD2 = 2, kBsMaxD3 = 3 };
 
 inline long long band_ws_floats(const BandPlan* p, long long rows) {
   if (!p) return 0;
@@ -163,46 +165,21 @@ __device__ __forceinline__ float band_scale_of(float mx) {
   return ldexpf(1.f, 14 - e);
 }
 
-// |d2| and |d3| maxima (positive floats order as their bit patterns): float4
-// grid-stride loads, one atomicMax per block and tensor into the zeroed slots
-__global__ __launch_bounds__(256) void band_absmax_kernel(const float4* d2, long long n2, const float4* d3,
-                                                         long long n3, unsigned* out) {
-  __shared__ float red[2][4];
-  float m2 = 0.f, m3 = 0.f;
-  const long long stride = (long long)gridDim.x * 256;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n2; i += stride) {
-    const float4 v = d2[i];
-    m2 = fmaxf(m2, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-  }
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n3; i += stride) {
-    const float4 v = d3[i];
-    m3 = fmaxf(m3, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-  }
-  m2 = wave_max(m2);
-  m3 = wave_max(m3);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) red[0][w] = m2, red[1][w] = m3;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float a = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
-    const float b = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
-    atomicMax(out, __float_as_uint(a));
-    atomicMax(out + 1, __float_as_uint(b));
-  }
-}
-
-// the X scales from the weights: a1 = relu(W1 x + b1) with x in [0, 1], so
+// The X bounds from the weights: a1 = relu(W1 x + b1) with x in [0, 1], so
 // a1[c] <= B1[c] = sum_k max(W1[k][c], 0) + max(b1[c], 0); a2 = relu(W2 a1 + b2)
-// with a1 >= 0, so a2[c'] <= sum_{k,c} max(W2[k][c][c'], 0) B1[c] + max(b2[c'], 0);
-// and the dY scales from the maxima of band_absmax_kernel.  One block.
+// with a1 >= 0, so a2[c'] <= sum_{k,c} max(W2[k][c][c'], 0) B1[c] + max(b2[c'], 0).
+// Block c' (64 blocks) recomputes B1 (8192 weights) and sums conv2's column c'
+// (512 rows); both maxima atomicMax-ed into the zeroed scratch.
 __global__ __launch_bounds__(256) void band_bounds_kernel(const float* w1, const float* b1, const float* w2,
-                                                         const float* b2, float* scr) {
-  __shared__ float part[8][64];
+                                                         const float* b2, unsigned* scr) {
+  __shared__ float part[8][32];
   __shared__ float B1[32];
-  const int t = threadIdx.x;
-  {  // B1: 32 channels x 256 taps; thread (q = t / 32, c = t % 32) sums taps q, q + 8, ...
+  __shared__ float red[4];
+  const int t = threadIdx.x, co = blockIdx.x;
+  {  // B1: thread (q = t / 32, c = t % 32) sums taps q, q + 8, ... (coalesced rows of 32)
     const int c = t & 31, q = t >> 5;
     float acc = 0.f;
+#pragma unroll 8
     for (int k = q; k < 256; k += 8) acc += fmaxf(w1[k * 32 + c], 0.f);
     part[q][c] = acc;
   }
@@ -213,32 +190,18 @@ __global__ __launch_bounds__(256) void band_bounds_kernel(const float* w1, const
     B1[t] = acc;
   }
   __syncthreads();
-  {  // B2: 64 channels x 512 rows (k, c); thread (q = t / 64, c' = t % 64)
-    const int co = t & 63, q = t >> 6;
-    float acc = 0.f;
-    for (int r = q; r < 512; r += 4) acc += fmaxf(w2[r * 64 + co], 0.f) * B1[r & 31];
-    part[q][co] = acc;
-  }
+  // conv2 column co: rows r = (kh, kw, c) of W2 [512][64]
+  const float v = fmaxf(w2[t * 64 + co], 0.f) * B1[t & 31] + fmaxf(w2[(t + 256) * 64 + co], 0.f) * B1[t & 31];
+  const float sum = wave_sum(v);
+  if ((t & 63) == 0) red[t >> 6] = sum;
   __syncthreads();
-  if (t < 64) {
-    float acc = fmaxf(b2[t], 0.f);
-    for (int q = 0; q < 4; ++q) acc += part[q][t];
-    float m2 = wave_max(acc);
-    float m1 = wave_max(t < 32 ? B1[t] : 0.f);
-    if (t == 0) {
-      const unsigned* mx = reinterpret_cast<const unsigned*>(scr);
-      const float sa1 = band_scale_of(m1), sa2 = band_scale_of(m2);
-      const float sd2 = band_scale_of(__uint_as_float(mx[kBsMaxD2]));
-      const float sd3 = band_scale_of(__uint_as_float(mx[kBsMaxD3]));
-      scr[kBsA1] = sa1;
-      scr[kBsA2] = sa2;
-      scr[kBsD2] = sd2;
-      scr[kBsD3] = sd3;
-      // the kernels' (s_X, s_dY) pairs: conv3 (a2, d3), conv2 (a1, d2)
-      scr[kBsPairC3] = sa2;
-      scr[kBsPairC3 + 1] = sd3;
-      scr[kBsPairC2] = sa1;
-      scr[kBsPairC2 + 1] = sd2;
+  if (t == 0) {
+    const float b2c = red[0] + red[1] + red[2] + red[3] + fmaxf(b2[co], 0.f);
+    atomicMax(scr + kBsMaxA2, __float_as_uint(b2c));
+    if (co == 0) {
+      float m = 0.f;
+      for (int c = 0; c < 32; ++c) m = fmaxf(m, B1[c]);
+      atomicMax(scr + kBsMaxA1, __float_as_uint(m));
     }
   }
 }
@@ -278,7 +241,8 @@ struct BandArgs {
   const BandGroup* groups;
   const int* xlist;  // groups of XCD x: xlist[xoff[x] .. xoff[x + 1])
   int xoff[9];
-  const float* scales;  // [sx, sy]
+  const unsigned* xmax;  // bit patterns of the X bound and of max |dY| (band scratch)
+  const unsigned* ymax;
   float* part;       // [nc][ntiles][64][64]
   float* cs;         // [nc][ncols]
   int ntiles, ncols;
@@ -293,7 +257,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
   // (staged slab lane / 16) and 256 + 4*lane .. +3 (slab 4 + lane / 16)
   const int rp = wave;
   const int q = (lane >> 2) & 3, pl = lane & 3, g = (lane >> 4) & 1, kh = lane >> 5;
-  const float sx = p.scales[0], sy = p.scales[1];
+  const float sx = band_scale_of(__uint_as_float(*p.xmax)), sy = band_scale_of(__uint_as_float(*p.ymax));
   {
     // item: XCD x = b & 7 (the blocks b, b + 8, ... share an XCD under the
     // round-robin dispatch), its j-th (group, chunk) in the region's list
@@ -590,27 +554,14 @@ __global__ __launch_bounds__(256) void band_fold_kernel(BandFold f) {
   }
 }
 
-// The operand scales of both band layers into scratch (kBandScratch floats):
-// |d2|, |d3| maxima, then the weight bounds of a1 / a2 and the four scales.
-inline int band_scales(const float* w1, const float* b1, const float* w2, const float* b2, const float* d2,
-                       long long n2, const float* d3, long long n3, float* scr, hipStream_t s) {
-  ACMI_REQUIRE(n2 % 4 == 0 && n3 % 4 == 0 && (uintptr_t)d2 % 16 == 0 && (uintptr_t)d3 % 16 == 0, ACMI_ERR_ARG,
-               "band_scales: dY buffers must be 16-byte aligned float4 runs");
-  ACMI_REQUIRE(hipMemsetAsync(scr, 0, kBandScratch * sizeof(float), s) == hipSuccess, ACMI_ERR_HIP,
-               "band_scales: memset failed");
-  hipLaunchKernelGGL(band_absmax_kernel, dim3(1024), dim3(256), 0, s, reinterpret_cast<const float4*>(d2), n2 / 4,
-                     reinterpret_cast<const float4*>(d3), n3 / 4, reinterpret_cast<unsigned*>(scr + kBsMaxD2));
-  hipLaunchKernelGGL(band_bounds_kernel, dim3(1), dim3(256), 0, s, w1, b1, w2, b2, scr);
-  ACMI_LAUNCH_CHECK("band_scales");
-  return ACMI_OK;
-}
-
 // [dW; db] of one conv layer and its A factor ((K+1)^2, / (M*L)) from the layer
 // input X [M][H][W][C] (f32, dense) and output gradient dY [M][OH][OW][CO];
-// scales = device [s_X, s_dY] (band_scales).
+// xmax / ymax: device bit patterns of the X bound and of max |dY| (the operand
+// scales, band_scale_of).
 inline int band_layer(const float* X, int H, int W, int C, int KH, int KW, int S, const float* dy,
                       int CO, int M, float* ws, long long ws_cap, float* grad, float* astat,
-                      float wscale, const float* scales, hipStream_t s, int site = 0) {
+                      float wscale, const unsigned* xmax, const unsigned* ymax, hipStream_t s,
+                      int site = 0) {
   const BandDev* d = band_dev(H, W, C, KH, KW, S, CO, s);
   ACMI_REQUIRE(d, ACMI_ERR_ARG, "band plan unavailable for %dx%dx%d k%dx%d s%d -> %d", H, W, C, KH, KW, S,
                CO);
@@ -639,7 +590,8 @@ inline int band_layer(const float* X, int H, int W, int C, int KH, int KW, int S
   a.groups = d->groups;
   a.xlist = d->tabs + d->o_xlist;
   for (int x = 0; x < 9; ++x) a.xoff[x] = d->xoff[x];
-  a.scales = scales;
+  a.xmax = xmax;
+  a.ymax = ymax;
   a.part = part;
   a.cs = cs;
   a.ntiles = p.ntiles;

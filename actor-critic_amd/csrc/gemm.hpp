@@ -74,10 +74,29 @@ struct has_vec4 : std::false_type {};
 template <class T>
 struct has_vec4<T, std::void_t<decltype(T::VEC4)>> : std::integral_constant<bool, T::VEC4> {};
 
+// Epilogues with a member `unsigned* amax` (nullable) also publish the largest
+// |value| they stored: store/store4 return what they wrote, each wave takes the
+// max of its lanes and one lane atomicMax-es its bit pattern (non-negative floats
+// order as their bits) into *amax, zeroed by the caller before the launch.  The
+// band reductions and the f16x2 operand splits scale a tensor by it (band.hpp).
+template <class T, class = void>
+struct has_amax : std::false_type {};
+template <class T>
+struct has_amax<T, std::void_t<decltype(std::declval<T&>().amax)>> : std::true_type {};
+
+__device__ __forceinline__ void amax_publish(unsigned* amax, float m, int lane) {
+  m = wave_max(m);
+  if (amax && lane == 0) atomicMax(amax, __float_as_uint(m));
+}
+__device__ __forceinline__ float absmax4(float m, float4 v) {
+  return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+
 template <int WTM, int WTN, class Epi, class Acc>
 __device__ __forceinline__ void store_tile(const Epi& epi, const Acc& acc, int ib, int jb, int lane,
                                            int I, int J) {
   const int khalf = lane >> 5;
+  float am = 0.f;
   if constexpr (has_vec4<Epi>::value) {
     float4 x[WTM][WTN][4];
 #pragma unroll
@@ -99,7 +118,10 @@ __device__ __forceinline__ void store_tile(const Epi& epi, const Acc& acc, int i
           const int i0 = ib + tm * 32 + 8 * g + 4 * khalf;
           const float4 v = make_float4(acc[tm][tn][4 * g], acc[tm][tn][4 * g + 1],
                                        acc[tm][tn][4 * g + 2], acc[tm][tn][4 * g + 3]);
-          if (i0 < I && j < J) epi.store4(i0, j, v, x[tm][tn][g]);
+          if (i0 < I && j < J) {
+            if constexpr (has_amax<Epi>::value) am = absmax4(am, epi.store4(i0, j, v, x[tm][tn][g]));
+            else epi.store4(i0, j, v, x[tm][tn][g]);
+          }
         }
       }
   } else {
@@ -123,10 +145,14 @@ __device__ __forceinline__ void store_tile(const Epi& epi, const Acc& acc, int i
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int i = ib + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
-          if (i < I && j < J) epi.store(i, j, acc[tm][tn][r], x[tm][tn][r]);
+          if (i < I && j < J) {
+            if constexpr (has_amax<Epi>::value) am = fmaxf(am, fabsf(epi.store(i, j, acc[tm][tn][r], x[tm][tn][r])));
+            else epi.store(i, j, acc[tm][tn][r], x[tm][tn][r]);
+          }
         }
       }
   }
+  if constexpr (has_amax<Epi>::value) amax_publish(epi.amax, am, lane);
 }
 
 // LDS bytes of one gemm_kernel block and the blocks one CU holds (160 KiB LDS,
@@ -159,6 +185,7 @@ __device__ __forceinline__ void store_tile_lds(const Epi& epi, const Acc& acc, i
   constexpr int S = 36;  // [32 columns][32 rows + 4]
   const int khalf = lane >> 5, c = lane & 31;
   const int ri = 4 * (lane & 7), cj = lane >> 3;  // read-back map: rows ri..ri+3 of column cj+8p
+  float am = 0.f;
 #pragma unroll
   for (int tm = 0; tm < WTM; ++tm)
 #pragma unroll
@@ -181,12 +208,16 @@ __device__ __forceinline__ void store_tile_lds(const Epi& epi, const Acc& acc, i
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int j = jb + tn * 32 + cj + 8 * p;
-        if (i0 < I && j < J) epi.store4(i0, j, v[p], x[p]);
+        if (i0 < I && j < J) {
+          if constexpr (has_amax<Epi>::value) am = absmax4(am, epi.store4(i0, j, v[p], x[p]));
+          else epi.store4(i0, j, v[p], x[p]);
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+  if constexpr (has_amax<Epi>::value) amax_publish(epi.amax, am, lane);
 }
 
 // DEPTH: K-tiles of staging loads in flight (register sets): 1 = the next
@@ -538,9 +569,12 @@ struct EpiReluGrad {
   float* out;
   const float* act;
   long long ld;
+  unsigned* amax = nullptr;  // nullable: max |out| (has_amax)
   __device__ __forceinline__ float aux(int i, int j) const { return act[(long long)i * ld + j]; }
-  __device__ __forceinline__ void store(int i, int j, float v, float x) const {
-    out[(long long)i * ld + j] = x > 0.f ? v : 0.f;
+  __device__ __forceinline__ float store(int i, int j, float v, float x) const {
+    const float o = x > 0.f ? v : 0.f;
+    out[(long long)i * ld + j] = o;
+    return o;
   }
 };
 
@@ -556,6 +590,7 @@ struct EpiConvT {
   static_assert(CIN % 4 == 0, "channel runs of 4");
   float* out;
   const float* act;
+  unsigned* amax = nullptr;  // nullable: max |out| (has_amax)
   __device__ __forceinline__ long long offset(int i, int j) const {
     constexpr int PH = IH / S, PW = IW / S, L = PH * PW;
     const uint32_t img = (uint32_t)j / L;
@@ -571,13 +606,14 @@ struct EpiConvT {
   __device__ __forceinline__ float4 aux4(int i0, int j) const {
     return *reinterpret_cast<const float4*>(act + offset(i0, j));
   }
-  __device__ __forceinline__ void store4(int i0, int j, float4 v, float4 x) const {
+  __device__ __forceinline__ float4 store4(int i0, int j, float4 v, float4 x) const {
     float4 o;
     o.x = x.x > 0.f ? v.x : 0.f;
     o.y = x.y > 0.f ? v.y : 0.f;
     o.z = x.z > 0.f ? v.z : 0.f;
     o.w = x.w > 0.f ? v.w : 0.f;
     *reinterpret_cast<float4*>(out + offset(i0, j)) = o;
+    return o;
   }
 };
 

@@ -938,7 +938,7 @@ static long long bwd_partial_cap(int B, int A, int C3) {
   // band reductions of conv2 / conv3 (rows = images)
   m = std::max(m, band_ws_floats(band_host_plan(20, 20, 32, 4, 4, 2, 64), B));
   m = std::max(m, band_ws_floats(band_host_plan(9, 9, 64, 3, 3, 1, C3), B));
-  // + the band reductions' scratch (operand scales, queue counters) at the end
+  // + the band reductions' scratch (operand-scale maxima, band.hpp) at the end
   return (m + 3) / 4 * 4 + kBandScratch;
 }
 
@@ -965,7 +965,9 @@ template <int C3>
 static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a,
                     const acmi_bwd_t* bw, const float* dhead, int ldh,
                     hipStream_t s, const char* prep = nullptr, float* gram_part = nullptr,
-                    bool* gram_done = nullptr) {
+                    bool* gram_done = nullptr, unsigned* amax_d3 = nullptr, unsigned* amax_d2 = nullptr) {
+  // amax_d3 / amax_d2 (nullable, zeroed by the caller): max |d3|, |d2| published by
+  // the producing epilogues for the band reductions' operand scales
   if (gram_done) *gram_done = false;
   // heads -> d4 = (dhead W_h^T) * relu'(a4)
   if (L.A == 4 && ldh % 4 == 0 && (uintptr_t)(P + L.off[8]) % 16 == 0 && (uintptr_t)dhead % 16 == 0)
@@ -978,7 +980,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     const int K3 = 49 * C3;
     RowsAsK<DenseRows> opA{DenseRows{bw->d4, 512, B, 512}};
     MatTK<true> opB{P + L.off[6], 512, 512, K3};
-    EpiReluGrad epi{bw->d3, a->a3, K3};
+    EpiReluGrad epi{bw->d3, a->a3, K3, amax_d3};
     launch_mm<64, 128, 32, 1, 2, false, false, 16>(opA, opB, epi, B, K3, 512, 1, 0, s);
   }
   // conv input gradients as transposed products: rows = (phase, channel) of
@@ -988,7 +990,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     using W = ConvTWeights<3, 3, 1, 64, C3>;
     W opA{P + L.off[4]};
     RowsAsK<Src> opB{Src{bw->d3, B * Src::L}};
-    EpiConvT<9, 9, 1, 64> epi{bw->d2, a->a2};
+    EpiConvT<9, 9, 1, 64> epi{bw->d2, a->a2, amax_d2};
     if (g_gemm_mode == ACMI_GEMM_X3)
       launch_convt_x3<9, 9, 3, 3, 1, 64, C3, 256>(P + L.off[4], bw->d3, B, epi, s);
     else
@@ -1034,7 +1036,16 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // gather competes with the symmetric reductions for L2 and LDS; the A factor
   // before the dX chain.)
   const bool fuse_c1 = st && g_gemm_mode == ACMI_GEMM_X3;
-  int rc = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s, prep);
+  // band reductions: operand-scale scratch (band.hpp) after the partial region;
+  // the dX epilogues publish max |d3|, |d2| into it
+  const long long pcap_all = bwd_partial_cap(B, L.A, L.C3);
+  unsigned* bscr = reinterpret_cast<unsigned*>(ws + pcap_all - kBandScratch);
+  const bool band = band_on(st);
+  if (band)
+    ACMI_REQUIRE(hipMemsetAsync(bscr, 0, kBandScratch * sizeof(unsigned), s) == hipSuccess, ACMI_ERR_HIP,
+                 "acmi_backward: band scratch reset failed");
+  int rc = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s, prep, nullptr, nullptr,
+                        band ? bscr + kBsMaxD3 : nullptr, band ? bscr + kBsMaxD2 : nullptr);
   if (rc) return rc;
   {
     hipEvent_t* ev = dx_done_event();
@@ -1070,27 +1081,21 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   if (rc) return rc;
   // conv3 / conv2: pixel-pair band reductions over the dense activation rows
   // (band.hpp), or the patches of a2 / a1
-  const long long pcap_all = bwd_partial_cap(B, L.A, L.C3);
-  float* bscr = ws + pcap_all - kBandScratch;  // operand scales + queue counters
   const long long band_cap = pcap_all - kBandScratch;
-  if (band_on(st)) {
-    rc = band_scales(P + L.off[0], P + L.off[1], P + L.off[2], P + L.off[3], bw->d2, 81LL * 64 * B, bw->d3,
-                     49LL * C3 * B, bscr, s);
-    if (rc) return rc;
-  }
-  float* sc_c3 = bscr + kBsPairC3;  // [s_a2, s_d3] and [s_a1, s_d2]: the kernels' (s_X, s_dY)
-  float* sc_c2 = bscr + kBsPairC2;
-  if (band_on(st)) {
+  if (band) {
+    // a1 / a2 bounds from the weights (max |d2|, |d3| came with the dX chain)
+    hipLaunchKernelGGL(band_bounds_kernel, dim3(64), dim3(256), 0, s, P + L.off[0], P + L.off[1], P + L.off[2],
+                       P + L.off[3], bscr);
     rc = band_layer(a->a2, 9, 9, 64, 3, 3, 1, bw->d3, C3, B, part, band_cap, grads + L.off[4],
-                    astat + L.stat_off[2], 1.f, sc_c3, s);
+                    astat + L.stat_off[2], 1.f, bscr + kBsMaxA2, bscr + kBsMaxD3, s);
   } else
     rc = wgrad_layer(ConvRows<float, 9, 9, 64, 3, 3, 1>{a->a2, 81 * 64, B * 49}, 576, 49LL * B,
                      bw->d3, C3, C3, st, part, ws_cap, grads + L.off[4], C3, nullptr,
                      st ? astat + L.stat_off[2] : nullptr, s);
   if (rc) return rc;
-  if (band_on(st))
+  if (band)
     rc = band_layer(a->a1, 20, 20, 32, 4, 4, 2, bw->d2, 64, B, part, band_cap, grads + L.off[2],
-                    astat + L.stat_off[1], 1.f, sc_c2, s, ACMI_PROF_CONV2_WGRAD);
+                    astat + L.stat_off[1], 1.f, bscr + kBsMaxA1, bscr + kBsMaxD2, s, ACMI_PROF_CONV2_WGRAD);
   else
     rc = wgrad_layer(ConvRows<float, 20, 20, 32, 4, 4, 2>{a->a1, 400 * 32, B * 81}, 512,
                      81LL * B, bw->d2, 64, 64, st, part, ws_cap, grads + L.off[2], 64, nullptr,
