@@ -43,7 +43,7 @@
 #include <tuple>
 
 #include "bandplan.hpp"
-#include "symred3.hpp"  // ds_tr16, stage_f4, zero_run
+#include "f16x2.hpp"  // split2, f16x2_scale, ds_tr16, stage_f4, zero_run
 
 namespace acmi {
 
@@ -145,24 +145,13 @@ inline void band_chunks(long long rows, int ngroups, int* nc, int* ch) {
 // the dX epilogues, gemm.hpp has_amax) and of the a1 / a2 bounds
 // (band_bounds_kernel); the kernels turn them into their operand scales
 constexpr int kBandScratch = 64;
-enum { kBsMaxA1 = 0, kBsMaxA2 = 1, kBsMaxD2 = 2, kBsMaxD3 = 3 };
+enum { kBsMaxA1 = 0, kBsMaxA2 = 1, kBsMaxD2 = 2, kBsMaxD3 = 3, kBsMaxW3 = 4, kBsMaxD4 = 5, kBsMaxW4 = 6 };
 
 inline long long band_ws_floats(const BandPlan* p, long long rows) {
   if (!p) return 0;
   int nc, ch;
   band_chunks(rows, (int)p->groups.size(), &nc, &ch);
   return (long long)nc * ((long long)p->ntiles * 4096 + (long long)p->geom.ns * 64);
-}
-
-// ---------------------------------------------------------------------------
-// operand scales
-// ---------------------------------------------------------------------------
-// power of two putting max at < 2^14 (f16 max 65504); 1 for a zero / non-finite max
-__device__ __forceinline__ float band_scale_of(float mx) {
-  if (!(mx > 0.f) || !(mx < 3.0e38f)) return 1.f;
-  int e;
-  (void)frexpf(mx, &e);  // mx < 2^e
-  return ldexpf(1.f, 14 - e);
 }
 
 // The X bounds from the weights: a1 = relu(W1 x + b1) with x in [0, 1], so
@@ -214,25 +203,6 @@ constexpr int kBandRowBytes = kBandSlabs * 64 * 2;    // 1024: one f16 row of th
 constexpr int kBandPart = kBandRows * kBandRowBytes;  // 16 KB
 constexpr int kBandBuf = 2 * kBandPart;               // h, l
 
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t pk_f16(float a, float b) {
-  const f32x2v v = {a, b};
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2v));
-}
-// (a, b) * s = h + l to 2^-22 relative: h = f16(x s), l = f16(x s - h)
-// (the residual as fma(x, s, -h): v_fma_mix_f32 reads h from the packed f16 register)
-__device__ __forceinline__ void split2(float a, float b, float s, uint32_t& h, uint32_t& l) {
-  h = pk_f16(a * s, b * s);
-  const f16x2v hv = __builtin_bit_cast(f16x2v, h);
-  l = pk_f16(fmaf(a, s, -(float)hv[0]), fmaf(b, s, -(float)hv[1]));
-}
-__device__ __forceinline__ f16x8 cat8h(s16x4 a, s16x4 b) {
-  const s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(f16x8, v);
-}
-
 struct BandArgs {
   const float* X;    // [M][kp]
   const float* dy;   // [M][ldy]
@@ -257,7 +227,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
   // (staged slab lane / 16) and 256 + 4*lane .. +3 (slab 4 + lane / 16)
   const int rp = wave;
   const int q = (lane >> 2) & 3, pl = lane & 3, g = (lane >> 4) & 1, kh = lane >> 5;
-  const float sx = band_scale_of(__uint_as_float(*p.xmax)), sy = band_scale_of(__uint_as_float(*p.ymax));
+  const float sx = f16x2_scale_of_bits(p.xmax), sy = f16x2_scale_of_bits(p.ymax);
   {
     // item: XCD x = b & 7 (the blocks b, b + 8, ... share an XCD under the
     // round-robin dispatch), its j-th (group, chunk) in the region's list
@@ -557,7 +527,7 @@ __global__ __launch_bounds__(256) void band_fold_kernel(BandFold f) {
 // [dW; db] of one conv layer and its A factor ((K+1)^2, / (M*L)) from the layer
 // input X [M][H][W][C] (f32, dense) and output gradient dY [M][OH][OW][CO];
 // xmax / ymax: device bit patterns of the X bound and of max |dY| (the operand
-// scales, band_scale_of).
+// scales, f16x2_scale).
 inline int band_layer(const float* X, int H, int W, int C, int KH, int KW, int S, const float* dy,
                       int CO, int M, float* ws, long long ws_cap, float* grad, float* astat,
                       float wscale, const unsigned* xmax, const unsigned* ymax, hipStream_t s,

@@ -1,6 +1,7 @@
-// conv2's input gradient (d1 = conv2^T d2 * relu'(a1)) on bf16x3 with the
-// weights split ONCE per parameter version, and the sampled-loss variant that
-// reduces d1 to the K-FAC G factor of conv1's output without storing it.
+// conv2's input gradient (d1 = conv2^T d2 * relu'(a1)) on f16x2 split operands
+// (f16x2.hpp) with the weights split ONCE per parameter version, and the
+// sampled-loss variant that reduces d1 to the K-FAC G factor of conv1's output
+// without storing it.
 //
 // gemm3_kernel / convt_x3_kernel run this product with every block splitting
 // the 128 x 256 weight matrix into h/m/l again (8000 blocks at the bench shape)
@@ -8,28 +9,30 @@
 // than the matrix cores need (rocprofv3: SQ_INSTS_VALU 1.24e8 against 12.3 M
 // MFMAs, 43 % MFMA-busy at 424 us).  Here
 //   * the weights come pre-split from acmi_conv_prepare ([k16 step][phase]
-//     [part h,m,l][lane] x 16 B, the A fragments of v_mfma_f32_32x32x16_bf16),
-//     staged per k-step into LDS by a straight 16-byte copy (12 KB, read back
-//     lane-contiguous: conflict-free ds_read_b128);
+//     [part h,l][lane] x 16 B, the A fragments of v_mfma_f32_32x32x16_f16, scaled
+//     by the power of two of max |W2|), staged per k-step into LDS by a straight
+//     16-byte copy (8 KB, read back lane-contiguous: conflict-free ds_read_b128);
 //   * a wave owns 32 super-pixel columns and ALL FOUR stride phases (rows
 //     (phase, ci)): the four phases of a super-pixel gather the same dY pixels
 //     (tap (a, b) of phase (py, px) is kernel position (py + 2a, px + 2b)), so
 //     one B fragment -- 8 channels of one dY pixel, two float4 loads from L2,
-//     one split -- feeds 4 x 6 MFMAs;
+//     one split by the scale of max |d2| (published by the conv3 dX epilogue) --
+//     feeds 4 x 3 MFMAs; the accumulators are unscaled before the epilogue;
 //   * epilogue STORE: the ReLU'-masked d1 as float4 channel runs; epilogue
 //     GRAM: the masked tile goes through LDS ([ci][super-pixel], stride 36:
-//     conflict-free) and its Gram D D^T accumulates on the same bf16x3 MFMAs
-//     across the wave's tiles; blocks write part[block][33][32] for
+//     conflict-free) and its Gram D D^T accumulates on bf16x3 MFMAs (d1 has no
+//     bound yet) across the wave's tiles; blocks write part[block][33][32] for
 //     finalize_cov_kernel (the layout gcov_layer's partials use).
-// Arithmetic per output element is gemm3's (six bf16 MFMAs per 32x32x16, k in
-// the same order: tap-major, channel-minor), so d1 is f32-accurate.
+// k runs in gemm3's order (tap-major, channel-minor); d1 is f32-accurate.
+// (Measured on bf16x3, six MFMAs per product: 392 / 411 us per launch at
+// M = 10240.)
 // Reference: tf.gradients of the conv2d at envs/atari/model.py:184-189
 // (objectives.py:78) and kfac's G factor of conv1's output (registration
 // envs/atari/model.py:227-231) -- the same sums.
 #pragma once
 
+#include "f16x2.hpp"
 #include "gemm.hpp"
-#include "symred3.hpp"
 
 namespace acmi {
 
@@ -37,10 +40,20 @@ namespace acmi {
 struct CT2 {
   static constexpr int CIN = 32, COUT = 64, OH = 9, OW = 9, PW = 10, L = 100;
   static constexpr int NKS = 16;                    // k16 steps: 4 taps x 64 channels
-  static constexpr int STEP_BYTES = 4 * 3 * 1024;   // 4 phases x 3 parts x 64 lanes x 16 B
-  static constexpr int BYTES = NKS * STEP_BYTES;    // 196,608 B of prepared weights
+  static constexpr int STEP_BYTES = 4 * 2 * 1024;   // 4 phases x 2 parts x 64 lanes x 16 B
+  static constexpr int FRAG_BYTES = NKS * STEP_BYTES;  // 131,072 B of prepared weights
+  static constexpr int BYTES = FRAG_BYTES + 16;     // + max |W2| (bit pattern) and padding
   static constexpr int TILE = 128;                  // columns per block tile (4 waves x 32)
 };
+
+// max |W2| into the prepared block's scale word (zeroed by the caller)
+__global__ __launch_bounds__(256) void convt2_wmax_kernel(const float* w2, char* out) {
+  float m = 0.f;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < 16 * CT2::CIN * CT2::COUT; i += gridDim.x * 256)
+    m = fmaxf(m, fabsf(w2[i]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(out + CT2::FRAG_BYTES), __float_as_uint(m));
+}
 
 // prepared weights: fragment (ks, phase) lane l holds W[py+2a][px+2b][ci][co..co+7],
 // ci = l & 31, tap t = ks >> 2 = (a, b), co = 16 (ks & 3) + 8 (l >> 5)
@@ -52,27 +65,30 @@ __global__ void convt2_prep_kernel(const float* w2, char* out) {
   const int kh = py + 2 * a, kw = px + 2 * b;
   const int ci = lane & 31, co = 16 * (ks & 3) + 8 * (lane >> 5);
   const float* p = w2 + ((kh * 4 + kw) * CT2::CIN + ci) * CT2::COUT + co;
-  uint4 h, m, l;
-  split3(p[0], p[1], h.x, m.x, l.x);
-  split3(p[2], p[3], h.y, m.y, l.y);
-  split3(p[4], p[5], h.z, m.z, l.z);
-  split3(p[6], p[7], h.w, m.w, l.w);
-  uint4* d = reinterpret_cast<uint4*>(out + (long long)ks * CT2::STEP_BYTES + ph * 3 * 1024) + lane;
+  const float sw = f16x2_scale_of_bits(reinterpret_cast<const unsigned*>(out + CT2::FRAG_BYTES));
+  uint4 h, l;
+  split2(p[0], p[1], sw, h.x, l.x);
+  split2(p[2], p[3], sw, h.y, l.y);
+  split2(p[4], p[5], sw, h.z, l.z);
+  split2(p[6], p[7], sw, h.w, l.w);
+  uint4* d = reinterpret_cast<uint4*>(out + (long long)ks * CT2::STEP_BYTES + ph * 2 * 1024) + lane;
   d[0] = h;
-  d[64] = m;
-  d[128] = l;
+  d[64] = l;
 }
 
 template <bool GRAM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* __restrict__ a1,
-                   float* __restrict__ d1, int B, float* __restrict__ gpart) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * CT2::STEP_BYTES];  // 24 KB ring
+                   float* __restrict__ d1, int B, float* __restrict__ gpart, const unsigned* d2max) {
+  // 16 KB ring; the epilogue's transpose scratch (4 x 32 x 36 floats) reuses it
+  __shared__ __attribute__((aligned(16))) char lds[std::max(2 * CT2::STEP_BYTES, 4 * 32 * 36 * 4)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int J = B * CT2::L;
   const int ntiles = (J + CT2::TILE - 1) / CT2::TILE;
   const int hl = lane >> 5;  // k half of the fragment; row offset 4 of the accumulator
   const float* zero = zero_run();
+  const float sd = f16x2_scale_of_bits(d2max);
+  const float inv = 1.f / (f16x2_scale_of_bits(reinterpret_cast<const unsigned*>(prep + CT2::FRAG_BYTES)) * sd);
 
   f32x16 gacc;  // GRAM: this wave's D D^T over its tiles
 #pragma unroll
@@ -108,20 +124,18 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
     x[0] = *reinterpret_cast<const float4*>(ok ? p : zero);
     x[1] = *reinterpret_cast<const float4*>(ok ? p + 4 : zero);
   };
-  // A staging: 12 KB per k-step, three 16-byte runs per thread (named
+  // A staging: 8 KB per k-step, two 16-byte runs per thread (named
   // registers: an array captured by the lambdas below was put in scratch)
-  uint4 ra0, ra1, ra2;
+  uint4 ra0, ra1;
   auto afetch = [&](int ks) {
     const uint4* src = reinterpret_cast<const uint4*>(prep + (long long)ks * CT2::STEP_BYTES) + tid;
     ra0 = src[0];
     ra1 = src[256];
-    ra2 = src[512];
   };
   auto acommit = [&](int buf) {
     uint4* dst = reinterpret_cast<uint4*>(lds + buf * CT2::STEP_BYTES) + tid;
     dst[0] = ra0;
     dst[256] = ra1;
-    dst[512] = ra2;
   };
   // two B register sets, alternating by k-step parity (named, never indexed at
   // run time: a dynamically indexed register array lands in scratch)
@@ -158,25 +172,15 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
       c.dimg = last ? nextc.dimg : cur.dimg;
       bload(last ? 0 : ks + 1, c, nb);
       __builtin_amdgcn_sched_barrier(0);
-      bf16x8 b[3];
-      {
-        uint4 h, m, l;
-        split3(cb[0].x, cb[0].y, h.x, m.x, l.x);
-        split3(cb[0].z, cb[0].w, h.y, m.y, l.y);
-        split3(cb[1].x, cb[1].y, h.z, m.z, l.z);
-        split3(cb[1].z, cb[1].w, h.w, m.w, l.w);
-        b[0] = __builtin_bit_cast(bf16x8, h);
-        b[1] = __builtin_bit_cast(bf16x8, m);
-        b[2] = __builtin_bit_cast(bf16x8, l);
-      }
+      f16x8 b[2];
+      split2x8(cb[0], cb[1], sd, b[0], b[1]);
       const char* As = lds + buf * CT2::STEP_BYTES + lane * 16;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        bf16x8 a[3];
+        f16x8 a[2];
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-          a[q] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(As + (p * 3 + q) * 1024));
-        acc[p] = mfma_x3(a, b, acc[p]);
+        for (int q = 0; q < 2; ++q) a[q] = as_f16x8(*reinterpret_cast<const uint4*>(As + (p * 2 + q) * 1024));
+        acc[p] = mfma_x2(a, b, acc[p]);
       }
       __builtin_amdgcn_sched_barrier(0);
       if (!last) acommit(buf ^ 1);  // (step 0's A is committed after the epilogue)
@@ -189,6 +193,10 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
       step(ks + 1, bx1, bx0);
     }
     cur = nextc;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[p][r] *= inv;  // unscale (exact: powers of two)
 
     // epilogue: rows (phase p, ci) x this wave's 32 super-pixel columns
     float* scr = reinterpret_cast<float*>(lds) + wave * 32 * 36;  // [32][36] per wave

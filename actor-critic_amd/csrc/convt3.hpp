@@ -1,5 +1,5 @@
-// Conv input gradient (transposed conv over all stride phases) on bf16x3 with
-// the dY im2col served from LDS.
+// Conv input gradient (transposed conv over all stride phases) on f16x2 split
+// operands (f16x2.hpp) with the dY im2col served from LDS.
 //
 // gemm3_kernel runs dX as C[(phase, ci)][super-pixel] = sum_k W(k, i) dY(k, j)
 // with B = RowsAsK<ConvTRows>: every column re-gathers its KHP x KWP dY pixels
@@ -10,17 +10,45 @@
 //     LDS as f32 ([pixel][COUT], 16-byte chunks XOR-swizzled by pixel so the
 //     fragment reads of 16 lanes at different pixels are bank-conflict free),
 //     plus one zero pixel for taps that fall outside the image;
-//   * the K loop streams only the weights (three-way split at the commit into
-//     gemm3's k-contiguous image, ds_read_b128 fragments);
+//   * the K loop streams only the weights (split into f16 h/l by the scale of
+//     max |W| at the commit into gemm3's k-contiguous image layout, ds_read_b128
+//     fragments);
 //   * a lane's B fragment (8 consecutive k = 8 channels of one tap of its
-//     column) is two ds_read_b128 of its dY pixel, split into h/m/l on the fly.
-// Same arithmetic as gemm3 (six bf16 MFMAs per 32x32x16), same epilogue
-// (EpiConvT through the LDS transpose).
+//     column) is two ds_read_b128 of its dY pixel, split into h/l on the fly by
+//     the scale of max |dY| (published by the dY producer's epilogue);
+//   * three f16 MFMAs per 32x32x16 (bf16x3 took six: 183 us per launch at
+//     M = 10240), accumulators unscaled before the epilogue (EpiConvT through
+//     the LDS transpose; it publishes max |dX| in turn).
 #pragma once
 
+#include "f16x2.hpp"
 #include "gemm3.hpp"
 
 namespace acmi {
+
+// gemm3's k-contiguous LDS image (X3Image<true, BX, BK>) with two f16 parts
+template <int BX, int BK>
+struct X2ImageKC {
+  static constexpr int PART = BX * BK * 2;  // bytes per part
+  static constexpr int BYTES = 2 * PART;
+  static constexpr int RB = BK * 2;         // bytes per LDS row
+  // commit of 4 consecutive k of row x, scaled by s
+  __device__ __forceinline__ static void write(char* sm, int k, int x, const float4& f, float s) {
+    uint2 h, l;
+    split2(f.x, f.y, s, h.x, l.x);
+    split2(f.z, f.w, s, h.y, l.y);
+    const int off = x * RB + 16 * sw_kc<BK>(k >> 3, x) + 8 * ((k >> 2) & 1);
+    *reinterpret_cast<uint2*>(sm + off) = h;
+    *reinterpret_cast<uint2*>(sm + PART + off) = l;
+  }
+  __device__ __forceinline__ static int frag_off(int lane, int ks, int x0) {
+    const int x = x0 + (lane & 31);
+    return x * RB + 16 * sw_kc<BK>(2 * ks + (lane >> 5), x);
+  }
+  __device__ __forceinline__ static f16x8 frag(const char* part, int off) {
+    return as_f16x8(*reinterpret_cast<const uint4*>(part + off));
+  }
+};
 
 template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, int NWAVES = 4>
 struct ConvTX3 {
@@ -38,7 +66,7 @@ struct ConvTX3 {
   static constexpr int PIXW = 256 / (COUT * 4) > 0 ? 256 / (COUT * 4) : 1;  // pixels per bank window
   static constexpr int ZP = NIMG * OP;             // the zero pixel
   static constexpr int DY_BYTES = (ZP + 1) * COUT * 4;
-  using IA = X3Image<true, NI, 16>;
+  using IA = X2ImageKC<NI, 16>;
   static constexpr int LDS_BYTES = DY_BYTES + 2 * IA::BYTES;
   static_assert(NI % 64 == 0 && NWAVES % WM == 0 && NJ % (32 * WN) == 0 && COUT % 16 == 0, "shape");
   static_assert(IH % S == 0 && IW % S == 0 && KH % S == 0 && KW % S == 0, "phases");
@@ -55,7 +83,7 @@ constexpr int convt_x3_blocks_per_cu() {
 template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, int NWAVES, class Epi>
 __global__ __launch_bounds__(64 * NWAVES) __attribute__((amdgpu_waves_per_eu(
     convt_x3_blocks_per_cu<ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES>>() * NWAVES / 4)))
-void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi) {
+void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi, const unsigned* wmax, const unsigned* dymax) {
   using CT = ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES>;
   using IA = typename CT::IA;
   using W = ConvTWeights<KH, KW, S, CIN, COUT>;
@@ -68,6 +96,8 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / CT::WN, wn = wave - wm * CT::WN;
+  const float sw = f16x2_scale_of_bits(wmax), sd = f16x2_scale_of_bits(dymax);
+  const float inv = 1.f / (sw * sd);
   const int J = B * L;
   const int j0 = blockIdx.x * NJ;
   const int img_lo = j0 / L;
@@ -91,7 +121,7 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi) {
     for (int v = 0; v < NA; ++v) {
       const int idx = tid + NTHR * v;
       const int i = idx / 4;
-      IA::write(As, (idx - i * 4) * 4, i, finish(ra[v]));
+      IA::write(As, (idx - i * 4) * 4, i, finish(ra[v]), sw);
     }
   };
 
@@ -153,9 +183,9 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi) {
     fetch((ks + 1) * 16);
     __builtin_amdgcn_sched_barrier(0);
     const char* As = abuf + cur * IA::BYTES;
-    bf16x8 a[2][3];
+    f16x8 a[2][2];
 #pragma unroll
-    for (int pt = 0; pt < 3; ++pt)
+    for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
       for (int tm = 0; tm < 2; ++tm) a[tm][pt] = IA::frag(As + pt * IA::PART, aoff[tm]);
     // this lane's 8 k: channels co..co+7 of tap (khp, kwp)
@@ -169,32 +199,34 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi) {
       const int p = ok ? cimg[tn] * CT::OP + oh * CT::OW + ow : CT::ZP;
       const float4 x0 = *reinterpret_cast<const float4*>(dimg + CT::chunk_pos(p, co / 4));
       const float4 x1 = *reinterpret_cast<const float4*>(dimg + CT::chunk_pos(p, co / 4 + 1));
-      uint4 h, m, l;
-      split3(x0.x, x0.y, h.x, m.x, l.x);
-      split3(x0.z, x0.w, h.y, m.y, l.y);
-      split3(x1.x, x1.y, h.z, m.z, l.z);
-      split3(x1.z, x1.w, h.w, m.w, l.w);
-      const bf16x8 b[3] = {__builtin_bit_cast(bf16x8, h), __builtin_bit_cast(bf16x8, m),
-                           __builtin_bit_cast(bf16x8, l)};
+      f16x8 b[2];
+      split2x8(x0, x1, sd, b[0], b[1]);
 #pragma unroll
-      for (int tm = 0; tm < 2; ++tm) acc[tm][tn] = mfma_x3(a[tm], b, acc[tm][tn]);
+      for (int tm = 0; tm < 2; ++tm) acc[tm][tn] = mfma_x2(a[tm], b, acc[tm][tn]);
     }
     __builtin_amdgcn_sched_barrier(0);
     if (ks + 1 < NK) commit(cur ^ 1);
     __syncthreads();
   }
   // epilogue through the LDS transpose (the dY image is free now)
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < CT::TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] *= inv;  // unscale (exact: powers of two)
   store_tile_lds<2, CT::TN>(epi, acc, wm * 64, j0 + wn * CT::WCOLS, lane,
                             reinterpret_cast<float*>(lds) + wave * 32 * 36, NI, J);
 }
 
 template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, int NWAVES = 4,
           class Epi>
-inline void launch_convt_x3(const float* w, const float* dy, int B, const Epi& e, hipStream_t s) {
+inline void launch_convt_x3(const float* w, const float* dy, int B, const Epi& e, const unsigned* wmax,
+                            const unsigned* dymax, hipStream_t s) {
   using CT = ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES>;
   static_assert(CT::DY_BYTES >= NWAVES * 32 * 36 * 4, "epilogue transpose needs the dY region");
   hipLaunchKernelGGL((convt_x3_kernel<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES, Epi>),
-                     dim3(cdiv(B * CT::L, NJ)), dim3(CT::NTHR), 0, s, w, dy, B, e);
+                     dim3(cdiv(B * CT::L, NJ)), dim3(CT::NTHR), 0, s, w, dy, B, e, wmax, dymax);
 }
 
 }  // namespace acmi

@@ -4,7 +4,7 @@
 //
 // At B = 512 the staged gemm3 launch (64x128 tiles, 8 K chunks, 256 blocks) is
 // a chain of 13 dependent K-tiles, each behind one global load round trip and
-// a barrier: 15 us for 2.4 GFLOP.  Here W4 comes pre-split into the bf16 h/m/l
+// a barrier: 15 us for 2.4 GFLOP.  Here W4 comes pre-split into the f16 h/l
 // parts of every lane's B fragment (acmi_conv_prepare, once per parameter
 // version, fragment-major like the tower's weights), each wave loads its own
 // A fragments (8 consecutive k of one row per lane: two float4) and its B
@@ -13,9 +13,10 @@
 // chunk z to XCD z (b % nz), so an XCD's L2 holds only its chunk's W4 columns
 // (590 KB) and a3 columns (400 KB at B = 512).
 //
-// Arithmetic: the same bf16x3 split of the same f32 values and the same
-// mfma_x3 sequence per k16-step and chunk as gemm3_kernel + EpiPartial, so the
-// slabs are bit-identical to the staged launch's (test_fc4_rollout_bit_identical).
+// Arithmetic: f16x2 (f16x2.hpp) -- W4 scaled by its max |W4|, a3 by the weight-
+// derived a3 bound of the tower's header (tower_stats3_kernel), three MFMAs per
+// k16-step and tile, the slabs unscaled before they are stored: f32-class like
+// the staged bf16x3 launch (test_fc4_rollout_matches_gemm3), not bit-identical.
 #pragma once
 
 #include "tower.hpp"
@@ -24,31 +25,32 @@ namespace acmi {
 
 constexpr int kFc4Depth = 3;  // k-steps in flight ahead of the one computed
 
-// W4 [K][512] -> [K/16 steps][16 col tiles][part h, m, l][64 lanes] x 16 B
-__global__ void fc4_prep_kernel(const float* w4, int K, char* out) {
+// W4 [K][512] -> [K/16 steps][16 col tiles][part h, l][64 lanes] x 16 B, scaled
+// by the power of two of hdr[kTowMaxW4] (the tower's header)
+__global__ void fc4_prep_kernel(const float* w4, int K, char* out, const unsigned* hdr) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = g & 63, f = g >> 6;  // f = step * 16 + col tile
   if (f >= (K / 16) * 16) return;
+  const float sw = f16x2_scale_of_bits(hdr + kTowMaxW4);
   const int s = f >> 4, ct = f & 15;
   const float* p = w4 + (16 * s + 8 * (lane >> 5)) * 512 + 32 * ct + (lane & 31);
-  uint4 h, m, l;
-  split3(p[0], p[512], h.x, m.x, l.x);
-  split3(p[2 * 512], p[3 * 512], h.y, m.y, l.y);
-  split3(p[4 * 512], p[5 * 512], h.z, m.z, l.z);
-  split3(p[6 * 512], p[7 * 512], h.w, m.w, l.w);
-  uint4* d = reinterpret_cast<uint4*>(out) + (long long)f * 192 + lane;
+  uint4 h, l;
+  split2(p[0], p[512], sw, h.x, l.x);
+  split2(p[2 * 512], p[3 * 512], sw, h.y, l.y);
+  split2(p[4 * 512], p[5 * 512], sw, h.z, l.z);
+  split2(p[6 * 512], p[7 * 512], sw, h.w, l.w);
+  uint4* d = reinterpret_cast<uint4*>(out) + (long long)f * 128 + lane;
   d[0] = h;
-  d[64] = m;
-  d[128] = l;
+  d[64] = l;
 }
 
-inline long long fc4_prep_bytes(int K) { return (long long)(K / 16) * 16 * 3 * 1024; }
+inline long long fc4_prep_bytes(int K) { return (long long)(K / 16) * 16 * 2 * 1024; }
 
 // block b: K chunk z = b % nz, then (row tile, column half); wave w: column
 // group 4 * half + w (64 columns).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
 void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w4p, int nz, int chunk_steps,
-                     float* part) {
+                     float* part, const unsigned* hdr) {
   constexpr int D = kFc4Depth, NSLOT = D + 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int z = blockIdx.x % nz, rest = blockIdx.x / nz;
@@ -58,20 +60,22 @@ void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w
   const int col = lane & 31;
   const int row = min(32 * rt + col, B - 1);
   const float* ap = a3 + (long long)row * lda + 16 * s0 + 8 * (lane >> 5);
-  // fragment (step s, col tile ct, part pt): uint4 index (s * 16 + ct) * 192 + 64 pt + lane
-  const uint4* bp = reinterpret_cast<const uint4*>(w4p) + ((long long)s0 * 16 + 2 * cg) * 192 + lane;
+  // fragment (step s, col tile ct, part pt): uint4 index (s * 16 + ct) * 128 + 64 pt + lane
+  const uint4* bp = reinterpret_cast<const uint4*>(w4p) + ((long long)s0 * 16 + 2 * cg) * 128 + lane;
+  const float sa = f16x2_scale_of_bits(hdr + kTowMaxA3);
+  const float inv = 1.0f / (sa * f16x2_scale_of_bits(hdr + kTowMaxW4));  // exact
 
   float4 av[NSLOT][2];
-  uint4 bv[NSLOT][2][3];
+  uint4 bv[NSLOT][2][2];
   auto load = [&](int i, int slot) {
     const float4* a = reinterpret_cast<const float4*>(ap + 16 * i);
     av[slot][0] = a[0];
     av[slot][1] = a[1];
-    const uint4* b = bp + (long long)i * 16 * 192;
+    const uint4* b = bp + (long long)i * 16 * 128;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int pt = 0; pt < 3; ++pt) bv[slot][t][pt] = b[t * 192 + 64 * pt];
+      for (int pt = 0; pt < 2; ++pt) bv[slot][t][pt] = b[t * 128 + 64 * pt];
   };
   f32x16 acc[2];
 #pragma unroll
@@ -89,14 +93,12 @@ void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w
       const int i = i0 + sl;
       if (i < ns) {
         if (i + D < ns) load(i + D, (sl + D) % NSLOT);
-        bf16x8 a[3];
-        tow_split8(av[sl][0], av[sl][1], a);
+        f16x8 a[2];
+        split2x8(av[sl][0], av[sl][1], sa, a[0], a[1]);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          bf16x8 b[3];
-#pragma unroll
-          for (int pt = 0; pt < 3; ++pt) b[pt] = __builtin_bit_cast(bf16x8, bv[sl][t][pt]);
-          acc[t] = mfma_x3(a, b, acc[t]);
+          const f16x8 b[2] = {as_f16x8(bv[sl][t][0]), as_f16x8(bv[sl][t][1])};
+          acc[t] = mfma_x2(a, b, acc[t]);
         }
       }
     }
@@ -107,17 +109,18 @@ void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rr = 32 * rt + tow_row(r, lane);
-      if (rr < B) out[(long long)rr * 512 + 32 * t] = acc[t][r];
+      if (rr < B) out[(long long)rr * 512 + 32 * t] = acc[t][r] * inv;
     }
 }
 
 // false when the shape is not one this kernel covers (the caller then uses gemm3)
+// hdr: the tower's bounds header (TowerPrep::HDR of the same prep)
 inline bool launch_fc4_roll(const float* a3, long long lda, int B, int K, const char* w4p, int nz, int chunk,
-                            float* part, hipStream_t s) {
+                            float* part, const unsigned* hdr, hipStream_t s) {
   if (chunk % 16 || K % 16 || (lda % 4) || ((uintptr_t)a3 % 16)) return false;
   const int cs = chunk / 16;
   const dim3 grid(nz * ((B + 31) / 32) * 2), blk(256);
-  hipLaunchKernelGGL(fc4_roll_kernel, grid, blk, 0, s, a3, lda, B, K, w4p, nz, cs, part);
+  hipLaunchKernelGGL(fc4_roll_kernel, grid, blk, 0, s, a3, lda, B, K, w4p, nz, cs, part, hdr);
   return true;
 }
 

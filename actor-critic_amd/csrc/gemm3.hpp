@@ -20,8 +20,14 @@
 // comments of sw_rows / sw_kc).
 // Column sums (COLSUM, i-contiguous B only) are summed in f32 from the staged
 // values at the commit and reduced across the k-row threads through LDS.
+//
+// F16 (launch_gemm3_f16): the same kernel on f16x2 split operands (f16x2.hpp) --
+// two f16 parts per operand scaled by the power of two of a published bound
+// (amax_a, amax_b: f32 bit patterns in device memory), three MFMAs per product
+// instead of six, the accumulators unscaled before the epilogue.
 #pragma once
 
+#include "f16x2.hpp"
 #include "gemm.hpp"
 #include "symred3.hpp"
 
@@ -53,27 +59,33 @@ __device__ __forceinline__ int sw_kc(int c, int i) {
   else return c ^ ((i >> 2) & 3);
 }
 
-template <int BM, int BN, int BK>
+template <int BM, int BN, int BK, int NP = 3>
 constexpr int gemm3_lds_bytes() {
-  return 2 * 3 * (BM + BN) * BK * 2;
+  return 2 * NP * (BM + BN) * BK * 2;
 }
-template <int BM, int BN, int BK>
+template <int BM, int BN, int BK, int NP = 3>
 constexpr int gemm3_blocks_per_cu() {
-  return std::min(8, 160 * 1024 / gemm3_lds_bytes<BM, BN, BK>());
+  return std::min(8, 160 * 1024 / gemm3_lds_bytes<BM, BN, BK, NP>());
 }
 
-// one operand's LDS image: write a staged float4 run, read 32-wide fragments
-template <bool KC, int BX, int BK>
+// one operand's LDS image: write a staged float4 run, read 32-wide fragments;
+// NP = 3: bf16 h/m/l parts, NP = 2: f16 h/l parts of the values times sc
+template <bool KC, int BX, int BK, int NP = 3>
 struct X3Image {
   static constexpr int PART = BX * BK * 2;  // bytes per part
-  static constexpr int BYTES = 3 * PART;
+  static constexpr int BYTES = NP * PART;
   static constexpr int RB = KC ? BK * 2 : BX * 2;  // bytes per LDS row
   // commit of run v at (k, x): KC -> 4 consecutive k of row x; else 4
   // consecutive x of k-row k
-  __device__ __forceinline__ static void write(char* s, int k, int x, const float4& f) {
+  __device__ __forceinline__ static void write(char* s, int k, int x, const float4& f, float sc = 1.f) {
     uint2 h, m, l;
-    split3(f.x, f.y, h.x, m.x, l.x);
-    split3(f.z, f.w, h.y, m.y, l.y);
+    if constexpr (NP == 3) {
+      split3(f.x, f.y, h.x, m.x, l.x);
+      split3(f.z, f.w, h.y, m.y, l.y);
+    } else {
+      split2(f.x, f.y, sc, h.x, m.x);
+      split2(f.z, f.w, sc, h.y, m.y);
+    }
     int off;
     if constexpr (KC) {
       off = x * RB + 16 * sw_kc<BK>(k >> 3, x) + 8 * ((k >> 2) & 1);
@@ -82,7 +94,7 @@ struct X3Image {
     }
     *reinterpret_cast<uint2*>(s + off) = h;
     *reinterpret_cast<uint2*>(s + PART + off) = m;
-    *reinterpret_cast<uint2*>(s + 2 * PART + off) = l;
+    if constexpr (NP == 3) *reinterpret_cast<uint2*>(s + 2 * PART + off) = l;
   }
   // byte offset (within a part) of lane's fragment for k-step ks (16 k) and the
   // 32-wide block starting at x0
@@ -106,14 +118,22 @@ struct X3Image {
 };
 
 template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM, class OpA, class OpB,
-          class Epi>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gemm3_blocks_per_cu<BM, BN, BK>())))
-void gemm3_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, int sym_cols) {
+          class Epi, bool F16 = false>
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(gemm3_blocks_per_cu<BM, BN, BK, F16 ? 2 : 3>())))
+void gemm3_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, int sym_cols,
+                  const unsigned* amax_a = nullptr, const unsigned* amax_b = nullptr) {
   using TL = Tile<BM, BN, BK, WTM, WTN>;
   static_assert(BK == 16 || BK == 32, "BK 16 or 32");
   static_assert(!COLSUM || !OpB::KCONTIG, "column sums need an i-contiguous B");
-  using IA = X3Image<OpA::KCONTIG, BM, BK>;
-  using IB = X3Image<OpB::KCONTIG, BN, BK>;
+  constexpr int NP = F16 ? 2 : 3;
+  using IA = X3Image<OpA::KCONTIG, BM, BK, NP>;
+  using IB = X3Image<OpB::KCONTIG, BN, BK, NP>;
+  float sa = 1.f, sb = 1.f;
+  if constexpr (F16) {
+    sa = f16x2_scale_of_bits(amax_a);
+    sb = f16x2_scale_of_bits(amax_b);
+  }
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
   if constexpr (SPLITK) {
     const int tx = (I + BM - 1) / BM, ty = (J + BN - 1) / BN;
@@ -237,9 +257,9 @@ void gemm3_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, i
       const int idx = tid + 256 * v;
       if constexpr (OpA::KCONTIG) {
         const int i = idx / (BK / 4);
-        IA::write(As, (idx - i * (BK / 4)) * 4, i, x);
+        IA::write(As, (idx - i * (BK / 4)) * 4, i, x, sa);
       } else {
-        IA::write(As, tid / TPRA + RSA * (v / RPRA), (tid % TPRA) * 4 + (v % RPRA) * TPRA * 4, x);
+        IA::write(As, tid / TPRA + RSA * (v / RPRA), (tid % TPRA) * 4 + (v % RPRA) * TPRA * 4, x, sa);
       }
     }
 #pragma unroll
@@ -248,7 +268,7 @@ void gemm3_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, i
       const int idx = tid + 256 * v;
       if constexpr (OpB::KCONTIG) {
         const int j = idx / (BK / 4);
-        IB::write(Bs, (idx - j * (BK / 4)) * 4, j, x);
+        IB::write(Bs, (idx - j * (BK / 4)) * 4, j, x, sb);
       } else {
         if constexpr (COLSUM) {
           const int u = v % RPRB;
@@ -257,7 +277,7 @@ void gemm3_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, i
           csum[4 * u + 2] += x.z;
           csum[4 * u + 3] += x.w;
         }
-        IB::write(Bs, tid / TPRB + RSB * (v / RPRB), (tid % TPRB) * 4 + (v % RPRB) * TPRB * 4, x);
+        IB::write(Bs, tid / TPRB + RSB * (v / RPRB), (tid % TPRB) * 4 + (v % RPRB) * TPRB * 4, x, sb);
       }
     }
   };
@@ -296,7 +316,7 @@ void gemm3_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, i
       for (int ks = 0; ks < BK / 16; ++ks) {
         bf16x8 a[WTM][3], b[WTN][3];
 #pragma unroll
-        for (int pt = 0; pt < 3; ++pt) {
+        for (int pt = 0; pt < NP; ++pt) {
 #pragma unroll
           for (int tm = 0; tm < WTM; ++tm) a[tm][pt] = IA::frag(As + pt * IA::PART, aoff[ks][tm]);
 #pragma unroll
@@ -305,7 +325,15 @@ void gemm3_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, i
 #pragma unroll
         for (int tm = 0; tm < WTM; ++tm)
 #pragma unroll
-          for (int tn = 0; tn < WTN; ++tn) acc[tm][tn] = mfma_x3(a[tm], b[tn], acc[tm][tn]);
+          for (int tn = 0; tn < WTN; ++tn) {
+            if constexpr (F16) {
+              const f16x8 ah[2] = {__builtin_bit_cast(f16x8, a[tm][0]), __builtin_bit_cast(f16x8, a[tm][1])};
+              const f16x8 bh[2] = {__builtin_bit_cast(f16x8, b[tn][0]), __builtin_bit_cast(f16x8, b[tn][1])};
+              acc[tm][tn] = mfma_x2(ah, bh, acc[tm][tn]);
+            } else {
+              acc[tm][tn] = mfma_x3(a[tm], b[tn], acc[tm][tn]);
+            }
+          }
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -347,6 +375,15 @@ void gemm3_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, i
     __syncthreads();
   }
 
+  if constexpr (F16) {
+    const float inv = 1.0f / (sa * sb);  // exact: powers of two
+#pragma unroll
+    for (int a = 0; a < WTM; ++a)
+#pragma unroll
+      for (int b = 0; b < WTN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[a][b][r] *= inv;
+  }
   if constexpr (has_ldst<Epi>::value && 2 * (IA::BYTES + IB::BYTES) >= 4 * 32 * 36 * 4) {
     __syncthreads();
     store_tile_lds<WTM, WTN>(epi, acc, i0 + wm * WTM * 32, j0 + wn * WTN * 32, lane,
@@ -363,7 +400,16 @@ inline void launch_gemm3(const OpA& a, const OpB& b, const Epi& e, int I, int J,
   dim3 grid(cdiv(I, BM), cdiv(J, BN), zdim);
   if (SPLITK) grid = dim3(live_tiles<BM, BN>(I, J, sym_cols) * zdim);
   hipLaunchKernelGGL((gemm3_kernel<BM, BN, BK, WTM, WTN, SPLITK, COLSUM, OpA, OpB, Epi>), grid,
-                     dim3(256), 0, s, a, b, e, I, J, K, k_chunk, sym_cols);
+                     dim3(256), 0, s, a, b, e, I, J, K, k_chunk, sym_cols, nullptr, nullptr);
+}
+
+// the f16x2 form (no split-K): amax_a / amax_b bound |A|, |B| (f32 bit patterns)
+template <int BM, int BN, int BK, int WTM, int WTN, class OpA, class OpB, class Epi>
+inline void launch_gemm3_f16(const OpA& a, const OpB& b, const Epi& e, int I, int J, int K,
+                             const unsigned* amax_a, const unsigned* amax_b, hipStream_t s) {
+  hipLaunchKernelGGL((gemm3_kernel<BM, BN, BK, WTM, WTN, false, false, OpA, OpB, Epi, true>),
+                     dim3(cdiv(I, BM), cdiv(J, BN), 1), dim3(256), 0, s, a, b, e, I, J, K, 0, 0, amax_a,
+                     amax_b);
 }
 
 // launch_gemm's interface, run on gemm3_kernel (bf16x3, K-tile BK3) in

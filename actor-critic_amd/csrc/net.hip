@@ -106,11 +106,21 @@ bool get_layout(int A, int C3, Layout* L) { return make_layout(A, C3, L); }
 // ---------------------------------------------------------------------------
 // d4 = (dhead [W_pi | w_v]^T) * relu'(a4): A+1 MACs per output, elementwise
 // over [B][512] (memory-bound); the k-ordered fmaf chain is the f32 MFMA's.
+// amax (nullable): max |d4| published for fc4's f16x2 input gradient (every
+// lane reaches the wave reduction; out-of-range lanes contribute 0)
+__device__ __forceinline__ void publish_max4(unsigned* amax, float4 r, bool ok) {
+  if (!amax) return;
+  float mx = ok ? fmaxf(fmaxf(fabsf(r.x), fabsf(r.y)), fmaxf(fabsf(r.z), fabsf(r.w))) : 0.f;
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(mx));
+}
+
 __global__ void heads_dx_kernel(const float* dhead, int ldh, int B, const float* wpi,
-                                const float* wv, int A, const float* a4, float* d4) {
+                                const float* wv, int A, const float* a4, float* d4, unsigned* amax) {
   // 4 consecutive outputs per thread (float4 a4 / d4)
-  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= (long long)B * 128) return;
+  const long long q0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ok = q0 < (long long)B * 128;
+  const long long q = ok ? q0 : 0;
   const int m = (int)(q >> 7), j0 = (int)(q & 127) * 4;
   const float* g = dhead + (long long)m * ldh;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -130,16 +140,18 @@ __global__ void heads_dx_kernel(const float* dhead, int ldh, int B, const float*
   o.y = acc[1] * (float)(x.y > 0.f);
   o.z = acc[2] * (float)(x.z > 0.f);
   o.w = acc[3] * (float)(x.w > 0.f);
-  *reinterpret_cast<float4*>(d4 + q * 4) = o;
+  if (ok) *reinterpret_cast<float4*>(d4 + q * 4) = o;
+  publish_max4(amax, o, ok);
 }
 
 // Breakout's A = 4 (16-byte aligned W_pi rows, dhead rows of ldh % 4 == 0): the
 // four W_pi rows and the dhead row as float4 loads (7 loads a thread instead of 26),
 // the same k-ordered fmaf chain per output
 __global__ void heads_dx4_kernel(const float* dhead, int ldh, int B, const float* wpi,
-                                 const float* wv, const float* a4, float* d4) {
-  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= (long long)B * 128) return;
+                                 const float* wv, const float* a4, float* d4, unsigned* amax) {
+  const long long q0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ok = q0 < (long long)B * 128;
+  const long long q = ok ? q0 : 0;
   const int m = (int)(q >> 7), j0 = (int)(q & 127) * 4;
   const float* g = dhead + (long long)m * ldh;
   const float4 g4 = *reinterpret_cast<const float4*>(g);
@@ -161,7 +173,8 @@ __global__ void heads_dx4_kernel(const float* dhead, int ldh, int B, const float
   r.y = o[1] * (float)(x.y > 0.f);
   r.z = o[2] * (float)(x.z > 0.f);
   r.w = o[3] * (float)(x.w > 0.f);
-  *reinterpret_cast<float4*>(d4 + q * 4) = r;
+  if (ok) *reinterpret_cast<float4*>(d4 + q * 4) = r;
+  publish_max4(amax, r, ok);
 }
 
 // conv/fc epilogue with an image remap so the rollout can write step t of an
@@ -366,11 +379,14 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // act_img_stride: images between consecutive batch rows in the activation
   // buffers (1 = contiguous; T = rollout step t of an env-major buffer).
   const long long st = act_img_stride;
-  // conv1 -> conv2 -> conv3 as one fused kernel per image (tower.hpp) in bf16x3
-  // mode; the per-layer kernels below in f32 mode or for unaligned images
-  const bool tower = g_gemm_mode == ACMI_GEMM_X3 && (uintptr_t)obs % 16 == 0 && img_stride % 16 == 0;
+  // conv1 -> conv2 -> conv3 as one fused kernel per image (tower.hpp, f16x2 on
+  // acmi_conv_prepare's fragments) in x3 mode; the per-layer kernels below in f32
+  // mode, without prepared weights or for unaligned images
+  const bool tower =
+      g_gemm_mode == ACMI_GEMM_X3 && prep && (uintptr_t)obs % 16 == 0 && img_stride % 16 == 0;
   ACMI_REQUIRE(tower || g_forward_mode == ACMI_FWD_F32, ACMI_ERR_ARG,
-               "bf16 forward needs the fused tower: 16-byte aligned observations and image stride");
+               "16-bit forward needs the fused tower: net->conv_prep and 16-byte aligned observations / image "
+               "stride");
   if (tower) {
     // the three convs fused per image (16-byte image loads)
     prof_begin(ACMI_PROF_CONV1_FWD, s);
@@ -424,7 +440,9 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     // the slabs in fixed order and applies bias + relu
     const char* w4p = prep ? static_cast<const char*>(prep) + TowerPrep<C3>::BYTES + CT2::BYTES : nullptr;
     if (!(g_gemm_mode == ACMI_GEMM_X3 && w4p &&
-          launch_fc4_roll(a->a3, st * K4, B, K4, w4p, nz, chunk, a->ws, s))) {
+          launch_fc4_roll(a->a3, st * K4, B, K4, w4p, nz, chunk, a->ws,
+                          reinterpret_cast<const unsigned*>(static_cast<const char*>(prep) + TowerPrep<C3>::HDR),
+                          s))) {
       EpiPartial epi{a->ws, B, 512};
       launch_mm<64, 128, 32, 1, 2, true, false, 16>(opA4, opB4, epi, B, 512, K4, nz, chunk, s);
     }
@@ -965,23 +983,41 @@ template <int C3>
 static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a,
                     const acmi_bwd_t* bw, const float* dhead, int ldh,
                     hipStream_t s, const char* prep = nullptr, float* gram_part = nullptr,
-                    bool* gram_done = nullptr, unsigned* amax_d3 = nullptr, unsigned* amax_d2 = nullptr) {
-  // amax_d3 / amax_d2 (nullable, zeroed by the caller): max |d3|, |d2| published by
-  // the producing epilogues for the band reductions' operand scales
+                    bool* gram_done = nullptr, unsigned* dxs = nullptr) {
+  // dxs: kBandScratch words of scratch (band.hpp layout): the dX epilogues publish
+  // max |d3|, |d2| there, the f16x2 consumers (convt2, the band reductions) scale
+  // by them
+  ACMI_REQUIRE(dxs, ACMI_ERR_ARG, "dx_chain: no scratch");
+  ACMI_REQUIRE(hipMemsetAsync(dxs, 0, kBandScratch * sizeof(unsigned), s) == hipSuccess, ACMI_ERR_HIP,
+               "dx_chain: scratch reset failed");
   if (gram_done) *gram_done = false;
   // heads -> d4 = (dhead W_h^T) * relu'(a4)
   if (L.A == 4 && ldh % 4 == 0 && (uintptr_t)(P + L.off[8]) % 16 == 0 && (uintptr_t)dhead % 16 == 0)
     hipLaunchKernelGGL(heads_dx4_kernel, dim3(cdiv((long long)B * 128, 256)), dim3(256), 0, s, dhead,
-                       ldh, B, P + L.off[8], P + L.off[10], a->a4, bw->d4);
+                       ldh, B, P + L.off[8], P + L.off[10], a->a4, bw->d4, dxs + kBsMaxD4);
   else
     hipLaunchKernelGGL(heads_dx_kernel, dim3(cdiv((long long)B * 128, 256)), dim3(256), 0, s, dhead,
-                       ldh, B, P + L.off[8], P + L.off[10], L.A, a->a4, bw->d4);
+                       ldh, B, P + L.off[8], P + L.off[10], L.A, a->a4, bw->d4, dxs + kBsMaxD4);
+  // max |W3|, |W4| for the f16x2 operands below: from the prepared weights'
+  // header, else computed here
+  const unsigned* hdr = prep ? reinterpret_cast<const unsigned*>(prep + TowerPrep<C3>::HDR) : nullptr;
+  const unsigned* w3max = hdr ? hdr + kTowMaxW3 : dxs + kBsMaxW3;
+  const unsigned* w4max = hdr ? hdr + kTowMaxW4 : dxs + kBsMaxW4;
+  if (!hdr && g_gemm_mode == ACMI_GEMM_X3) {
+    hipLaunchKernelGGL(absmax_kernel, dim3(16), dim3(256), 0, s, P + L.off[4], (long long)576 * C3,
+                       dxs + kBsMaxW3);
+    hipLaunchKernelGGL(absmax_kernel, dim3(64), dim3(256), 0, s, P + L.off[6], (long long)49 * C3 * 512,
+                       dxs + kBsMaxW4);
+  }
   {  // fc4 -> d3 = (d4 W4^T) * relu'(a3)
     const int K3 = 49 * C3;
     RowsAsK<DenseRows> opA{DenseRows{bw->d4, 512, B, 512}};
     MatTK<true> opB{P + L.off[6], 512, 512, K3};
-    EpiReluGrad epi{bw->d3, a->a3, K3, amax_d3};
-    launch_mm<64, 128, 32, 1, 2, false, false, 16>(opA, opB, epi, B, K3, 512, 1, 0, s);
+    EpiReluGrad epi{bw->d3, a->a3, K3, dxs + kBsMaxD3};
+    if (g_gemm_mode == ACMI_GEMM_X3)
+      launch_gemm3_f16<64, 128, 16, 1, 2>(opA, opB, epi, B, K3, 512, dxs + kBsMaxD4, w4max, s);
+    else
+      launch_mm<64, 128, 32, 1, 2, false, false, 16>(opA, opB, epi, B, K3, 512, 1, 0, s);
   }
   // conv input gradients as transposed products: rows = (phase, channel) of
   // the weights, columns = (super-)pixels gathering dY (EpiConvT, float4 rows)
@@ -990,9 +1026,10 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     using W = ConvTWeights<3, 3, 1, 64, C3>;
     W opA{P + L.off[4]};
     RowsAsK<Src> opB{Src{bw->d3, B * Src::L}};
-    EpiConvT<9, 9, 1, 64> epi{bw->d2, a->a2, amax_d2};
+    EpiConvT<9, 9, 1, 64> epi{bw->d2, a->a2, dxs + kBsMaxD2};
     if (g_gemm_mode == ACMI_GEMM_X3)
-      launch_convt_x3<9, 9, 3, 3, 1, 64, C3, 256>(P + L.off[4], bw->d3, B, epi, s);
+      // f16x2 operands: the scales of max |W3| and of max |d3| (the fc4 dX epilogue's)
+      launch_convt_x3<9, 9, 3, 3, 1, 64, C3, 256>(P + L.off[4], bw->d3, B, epi, w3max, dxs + kBsMaxD3, s);
     else
       launch_mm<64, 128, 16, 1, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
   }
@@ -1010,11 +1047,11 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
       // chain reduces d1 to its Gram partials instead of storing it
       if (gram_part) {
         hipLaunchKernelGGL(convt2_kernel<true>, dim3(convt2_gram_blocks(B)), dim3(256), 0, s, p2, bw->d2,
-                           a->a1, nullptr, B, gram_part);
+                           a->a1, nullptr, B, gram_part, dxs + kBsMaxD2);
         if (gram_done) *gram_done = true;
       } else {
-hipLaunchKernelGGL(convt2_kernel<false>, dim3(cdiv(B * CT2::L, CT2::TILE)), dim3(256), 0, s, p2,
-                           bw->d2, a->a1, bw->d1, B, nullptr);
+        hipLaunchKernelGGL(convt2_kernel<false>, dim3(cdiv(B * CT2::L, CT2::TILE)), dim3(256), 0, s, p2,
+                           bw->d2, a->a1, bw->d1, B, nullptr, dxs + kBsMaxD2);
       }
     } else
       launch_mm<128, 128, 16, 2, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
@@ -1041,11 +1078,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   const long long pcap_all = bwd_partial_cap(B, L.A, L.C3);
   unsigned* bscr = reinterpret_cast<unsigned*>(ws + pcap_all - kBandScratch);
   const bool band = band_on(st);
-  if (band)
-    ACMI_REQUIRE(hipMemsetAsync(bscr, 0, kBandScratch * sizeof(unsigned), s) == hipSuccess, ACMI_ERR_HIP,
-                 "acmi_backward: band scratch reset failed");
-  int rc = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s, prep, nullptr, nullptr,
-                        band ? bscr + kBsMaxD3 : nullptr, band ? bscr + kBsMaxD2 : nullptr);
+  int rc = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s, prep, nullptr, nullptr, bscr);
   if (rc) return rc;
   {
     hipEvent_t* ev = dx_done_event();
@@ -1153,12 +1186,14 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
   const int ldg = roundup4(L.A + 1) < 8 ? 8 : roundup4(L.A + 1);
   float* ghead = ws;  // [B][ldg]
   float* part = ws + (long long)B * ldg;
-  const long long cap = ws_cap - (long long)B * ldg;
+  // the dX chain's scratch (operand-scale maxima) in the workspace's last words
+  const long long cap = ws_cap - (long long)B * ldg - kBandScratch;
+  unsigned* dxs = reinterpret_cast<unsigned*>(ws + ws_cap - kBandScratch);
   hipLaunchKernelGGL(sampled_head_grad_kernel, dim3(cdiv(B, 128)), dim3(128), 0, s,
                      a->logits, a->ld_logits, B, L.A, seed, row0, ctr, ghead, ldg);
   bool g1_done = false;
   const bool g1_fits = (long long)convt2_gram_blocks(B) * 33 * 32 <= cap;
-  int rc = dx_chain<C3>(L, P, B, a, bw, ghead, ldg, s, prep, g1_fits ? part : nullptr, &g1_done);
+  int rc = dx_chain<C3>(L, P, B, a, bw, ghead, ldg, s, prep, g1_fits ? part : nullptr, &g1_done, dxs);
   if (rc) return rc;
   if (g1_done) {  // G of conv1's output from the conv2 dX kernel's per-block Gram partials
     hipLaunchKernelGGL(finalize_cov_kernel, dim3(cdiv(32 * 32, 4)), dim3(256), 0, s, part,
@@ -1309,13 +1344,24 @@ int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
   ACMI_REQUIRE(net && net->params && prep && make_layout(net->num_actions, net->conv3_filters, &L),
                ACMI_ERR_ARG, "acmi_conv_prepare: bad arguments");
   ACMI_REQUIRE((uintptr_t)prep % 16 == 0, ACMI_ERR_ARG, "acmi_conv_prepare: prep must be 16-byte aligned");
-  launch_tower_prep(net->params, L.off, L.C3, prep, (hipStream_t)stream);
   const long long o2 = L.C3 == 32 ? TowerPrep<32>::BYTES : TowerPrep<64>::BYTES;
+  const long long oh = L.C3 == 32 ? TowerPrep<32>::HDR : TowerPrep<64>::HDR;
+  // the tower's bounds header (atomicMax targets), then its f16x2 fragments
+  ACMI_REQUIRE(hipMemsetAsync(static_cast<char*>(prep) + oh, 0, 32, (hipStream_t)stream) == hipSuccess,
+               ACMI_ERR_HIP, "acmi_conv_prepare: memset failed");
+  launch_tower_prep(net->params, L.off, L.C3, prep, (hipStream_t)stream);
+  // conv2's input-gradient weights: max |W2| (the f16x2 scale), then the split
+  ACMI_REQUIRE(hipMemsetAsync(static_cast<char*>(prep) + o2 + CT2::FRAG_BYTES, 0, 16, (hipStream_t)stream) ==
+                   hipSuccess,
+               ACMI_ERR_HIP, "acmi_conv_prepare: memset failed");
+  hipLaunchKernelGGL(convt2_wmax_kernel, dim3(32), dim3(256), 0, (hipStream_t)stream, net->params + L.off[2],
+                     static_cast<char*>(prep) + o2);
   hipLaunchKernelGGL(convt2_prep_kernel, dim3(CT2::NKS * 4 * 64 / 256), dim3(256), 0, (hipStream_t)stream,
                      net->params + L.off[2], static_cast<char*>(prep) + o2);
   const int K4 = 49 * L.C3;
   hipLaunchKernelGGL(fc4_prep_kernel, dim3(K4 / 16 * 16 * 64 / 256), dim3(256), 0, (hipStream_t)stream,
-                     net->params + L.off[6], K4, static_cast<char*>(prep) + o2 + CT2::BYTES);
+                     net->params + L.off[6], K4, static_cast<char*>(prep) + o2 + CT2::BYTES,
+                     reinterpret_cast<const unsigned*>(static_cast<char*>(prep) + oh));
   ACMI_LAUNCH_CHECK("acmi_conv_prepare");
   return ACMI_OK;
 }

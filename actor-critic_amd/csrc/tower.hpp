@@ -7,16 +7,21 @@
 // for ~6 us of MFMA work each.  Here a block loads its u8 image once (28 KB),
 // keeps a1 (51 KB) in LDS for conv2 and a2 (21 KB, over the image) for conv3,
 // and streams only the weights: every lane loads its B fragment (8 k of one
-// output column) straight from global/L2 one k-step ahead -- already split into
-// bf16 h/m/l when the caller prepared the weights (acmi_conv_prepare, once per
-// parameter version), else split here -- no weight staging, so 79 KB of LDS and
-// two blocks (8 waves) per CU hold all 512 images of a rollout step at once.
+// output column) straight from global/L2 one k-step ahead, already split into
+// f16 h/l by acmi_conv_prepare (once per parameter version) -- no weight
+// staging, so 79 KB of LDS and two blocks (8 waves) per CU hold all 512 images
+// of a rollout step at once.  (Without prepared weights the forward runs the
+// per-layer kernels instead.)
 //
-// Arithmetic: conv1 as conv1_fwd_x3 (u8 pixels exact in bf16, three MFMAs per
-// k16 against the weights' h/m/l, scale 1/255 and bias in one fmaf); conv2 /
-// conv3 bf16x3 on both operands (mfma_x3, symred3.hpp) -- f32-accurate.  The
-// a1 / a2 LDS images use convfwd3.hpp's 16-byte chunk swizzle by pixel x, so
-// the lanes of a fragment read (consecutive output columns) hit distinct banks.
+// Arithmetic: f16x2 split operands (f16x2.hpp), each tensor scaled by a power of
+// two from a bound the prepare step computes (tower_stats_kernel): the weights'
+// max |W|, and the a1 / a2 bounds of band.hpp (ReLU outputs of [0,1] pixels
+// under the positive weight mass).  conv1: u8 pixels exact in f16, two MFMAs per
+// k16 against the weights' h/l (bf16x3 took three); conv2 / conv3: the a1 / a2
+// fragments split h/l from LDS, three MFMAs per product (bf16x3: six); the
+// accumulators unscaled in the epilogue's bias fma -- f32-accurate.  The a1 / a2
+// LDS images use convfwd3.hpp's 16-byte chunk swizzle by pixel x, so the lanes
+// of a fragment read (consecutive output columns) hit distinct banks.
 // Work per block: conv1 three row tiles per wave + the 13th by K halves on two
 // waves (roles rotated by block parity: equal per-SIMD load); conv2 the 3x2
 // tiles as one full tile + half the K of row tile 2 per wave (the halves summed
@@ -26,7 +31,7 @@
 #pragma once
 
 #include "conv1u8.hpp"
-#include "symred3.hpp"
+#include "f16x2.hpp"
 
 namespace acmi {
 
@@ -44,125 +49,162 @@ __device__ __forceinline__ int tow_pos(int p, int x, int ch) {
   return p * C * 4 + 16 * (ch ^ ((x / S) & (C / 4 - 1)));
 }
 
-__device__ __forceinline__ bf16x8 tow_bf16x8(const float4& x0, const float4& x1) {
-  uint4 h;
-  h.x = pk_bf16(x0.x, x0.y);
-  h.y = pk_bf16(x0.z, x0.w);
-  h.z = pk_bf16(x1.x, x1.y);
-  h.w = pk_bf16(x1.z, x1.w);
-  return __builtin_bit_cast(bf16x8, h);
-}
-
-__device__ __forceinline__ void tow_split8(const float4& x0, const float4& x1, bf16x8 (&o)[3]) {
-  uint4 h, m, l;
-  split3(x0.x, x0.y, h.x, m.x, l.x);
-  split3(x0.z, x0.w, h.y, m.y, l.y);
-  split3(x1.x, x1.y, h.z, m.z, l.z);
-  split3(x1.z, x1.w, h.w, m.w, l.w);
-  o[0] = __builtin_bit_cast(bf16x8, h);
-  o[1] = __builtin_bit_cast(bf16x8, m);
-  o[2] = __builtin_bit_cast(bf16x8, l);
-}
-
-// lane's B fragment of k16-step s, output columns c0 .. c0+31 of W [K][N]:
-// B[16s + 8(lane>>5) + e][c0 + (lane & 31)], e = 0..7
-template <int N>
-__device__ __forceinline__ void tow_bload(const float* w, int s, int c0, int lane, float4 (&x)[2]) {
-  const float* p = w + (16 * s + 8 * (lane >> 5)) * N + c0 + (lane & 31);
-  x[0] = make_float4(p[0], p[N], p[2 * N], p[3 * N]);
-  x[1] = make_float4(p[4 * N], p[5 * N], p[6 * N], p[7 * N]);
+// eight u8 pixels as f16 (exact)
+__device__ __forceinline__ f16x8 u8x8_to_f16(uint2 u) {
+  uint32_t w[4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t x = h ? u.y : u.x;
+    w[2 * h] = pk_f16((float)(x & 255u), (float)((x >> 8) & 255u));
+    w[2 * h + 1] = pk_f16((float)((x >> 16) & 255u), (float)(x >> 24));
+  }
+  return __builtin_bit_cast(f16x8, make_uint4(w[0], w[1], w[2], w[3]));
 }
 
 // Prepared weights (acmi_conv_prepare): conv1/conv2/conv3 weights split once
-// per parameter version into the bf16x3 parts of every lane's B fragment,
-// fragment-major -- [k16 step][32-col tile][part h,m,l][lane] x 16 B -- so the
+// per parameter version into the f16 h/l parts of every lane's B fragment,
+// fragment-major -- [k16 step][32-col tile][part h,l][lane] x 16 B -- so the
 // tower loads them with one 16-byte load per part instead of 8 scalar loads and
-// a split per k-step and wave (the split of each weight done once, not by every
-// wave of every block).
+// a split per k-step and wave; then a header of bounds (bit patterns, for the
+// atomicMax of tower_stats_kernel): max |W1|, |W2|, |W3|, the a1, a2 and a3
+// bounds, max |W4| (fc4roll.hpp's prepared fc4 reads the last two).
 template <int C3>
 struct TowerPrep {
-  static constexpr long long FRAG = 3 * 64 * 16;  // bytes per (k-step, col tile)
+  static constexpr long long FRAG = 2 * 64 * 16;  // bytes per (k-step, col tile)
   static constexpr long long O1 = 0, N1 = 16 * 1;             // conv1: 16 steps x 1 tile
   static constexpr long long O2 = O1 + N1 * FRAG, N2 = 32 * 2;  // conv2: 32 x 2
   static constexpr long long O3 = O2 + N2 * FRAG, N3 = 36 * (C3 / 32);
-  static constexpr long long BYTES = O3 + N3 * FRAG;
+  static constexpr long long HDR = O3 + N3 * FRAG;            // 8 words of bounds
+  static constexpr long long BYTES = HDR + 32;
 };
+enum { kTowMaxW1 = 0, kTowMaxW2 = 1, kTowMaxW3 = 2, kTowMaxA1 = 3, kTowMaxA2 = 4, kTowMaxA3 = 5, kTowMaxW4 = 6 };
 
-__global__ void tower_prep_kernel(const float* w1, const float* w2, const float* w3, int C3, char* out) {
+// the header's bounds (zeroed by the caller): 64 blocks of band.hpp's a1 / a2
+// bounds (block c' takes conv2's column c') plus max |W| over all four layers
+__global__ __launch_bounds__(256) void tower_stats_kernel(const float* w1, const float* b1, const float* w2,
+                                                         const float* b2, const float* w3, int n3,
+                                                         const float* w4, int n4, unsigned* hdr) {
+  __shared__ float part[8][32];
+  __shared__ float B1[32];
+  __shared__ float red[4];
+  const int t = threadIdx.x, co = blockIdx.x;
+  {
+    const int c = t & 31, q = t >> 5;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int k = q; k < 256; k += 8) acc += fmaxf(w1[k * 32 + c], 0.f);
+    part[q][c] = acc;
+  }
+  __syncthreads();
+  if (t < 32) {
+    float acc = fmaxf(b1[t], 0.f);
+    for (int q = 0; q < 8; ++q) acc += part[q][t];
+    B1[t] = acc;
+  }
+  __syncthreads();
+  const float v = fmaxf(w2[t * 64 + co], 0.f) * B1[t & 31] + fmaxf(w2[(t + 256) * 64 + co], 0.f) * B1[t & 31];
+  const float sum = wave_sum(v);
+  if ((t & 63) == 0) red[t >> 6] = sum;
+  // max |W| of the three layers over the grid
+  float m1 = 0.f, m2 = 0.f, m3 = 0.f, m4 = 0.f;
+  for (int i = co * 256 + t; i < 8192; i += 64 * 256) m1 = fmaxf(m1, fabsf(w1[i]));
+  for (int i = co * 256 + t; i < 32768; i += 64 * 256) m2 = fmaxf(m2, fabsf(w2[i]));
+  for (int i = co * 256 + t; i < n3; i += 64 * 256) m3 = fmaxf(m3, fabsf(w3[i]));
+  for (int i = co * 256 + t; i < n4; i += 64 * 256) m4 = fmaxf(m4, fabsf(w4[i]));
+  m1 = wave_max(m1);
+  m2 = wave_max(m2);
+  m3 = wave_max(m3);
+  m4 = wave_max(m4);
+  if ((t & 63) == 0) {
+    atomicMax(hdr + kTowMaxW1, __float_as_uint(m1));
+    atomicMax(hdr + kTowMaxW2, __float_as_uint(m2));
+    atomicMax(hdr + kTowMaxW3, __float_as_uint(m3));
+    atomicMax(hdr + kTowMaxW4, __float_as_uint(m4));
+  }
+  __syncthreads();
+  if (t == 0) {
+    atomicMax(hdr + kTowMaxA2, __float_as_uint(red[0] + red[1] + red[2] + red[3] + fmaxf(b2[co], 0.f)));
+    if (co == 0) {
+      float m = 0.f;
+      for (int c = 0; c < 32; ++c) m = fmaxf(m, B1[c]);
+      atomicMax(hdr + kTowMaxA1, __float_as_uint(m));
+    }
+  }
+}
+
+// the a3 bound from the final a2 bound: block co takes conv3's column co,
+// a3 <= sum_k max(W3[k][co], 0) * max a2 + max(b3[co], 0)
+__global__ __launch_bounds__(64) void tower_stats3_kernel(const float* w3, const float* b3, int C3,
+                                                          unsigned* hdr) {
+  const int co = blockIdx.x, t = threadIdx.x;
+  float acc = 0.f;
+  for (int k = t; k < 576; k += 64) acc += fmaxf(w3[k * C3 + co], 0.f);
+  acc = wave_sum(acc);
+  if (t == 0) atomicMax(hdr + kTowMaxA3, __float_as_uint(acc * __uint_as_float(hdr[kTowMaxA2]) + fmaxf(b3[co], 0.f)));
+}
+
+__global__ void tower_prep_kernel(const float* w1, const float* w2, const float* w3, int C3, char* out,
+                                  const unsigned* hdr) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;  // (layer, step, tile, lane)
   const int lane = g & 63;
   int f = g >> 6;  // fragment index over the three layers
   const int n3 = 36 * (C3 / 32);
   const float* w;
-  int N, s, ct;
+  int N, s, ct, layer;
   long long o;
   if (f < 16) {
-    w = w1, N = 32, s = f, ct = 0, o = 0;
+    w = w1, N = 32, s = f, ct = 0, o = 0, layer = 0;
   } else if ((f -= 16) < 64) {
-    w = w2, N = 64, s = f >> 1, ct = f & 1, o = 16LL * 3 * 1024;
+    w = w2, N = 64, s = f >> 1, ct = f & 1, o = 16LL * 2 * 1024, layer = 1;
   } else if ((f -= 64) < n3) {
-    w = w3, N = C3, s = f / (C3 / 32), ct = f % (C3 / 32), o = (16LL + 64) * 3 * 1024;
+    w = w3, N = C3, s = f / (C3 / 32), ct = f % (C3 / 32), o = (16LL + 64) * 2 * 1024, layer = 2;
   } else {
     return;
   }
+  const float sw = f16x2_scale_of_bits(hdr + layer);
   const float* p = w + (16 * s + 8 * (lane >> 5)) * N + 32 * ct + (lane & 31);
-  uint4 h, m, l;
-  split3(p[0], p[N], h.x, m.x, l.x);
-  split3(p[2 * N], p[3 * N], h.y, m.y, l.y);
-  split3(p[4 * N], p[5 * N], h.z, m.z, l.z);
-  split3(p[6 * N], p[7 * N], h.w, m.w, l.w);
-  uint4* d = reinterpret_cast<uint4*>(out + o + ((long long)(s * (N / 32) + ct) * 3) * 1024) + lane;
+  uint4 h, l;
+  split2(p[0], p[N], sw, h.x, l.x);
+  split2(p[2 * N], p[3 * N], sw, h.y, l.y);
+  split2(p[4 * N], p[5 * N], sw, h.z, l.z);
+  split2(p[6 * N], p[7 * N], sw, h.w, l.w);
+  uint4* d = reinterpret_cast<uint4*>(out + o + ((long long)(s * (N / 32) + ct) * 2) * 1024) + lane;
   d[0] = h;
-  d[64] = m;
-  d[128] = l;
-}
-
-// B fragment of k16-step s, column tile ct from the prepared weights
-__device__ __forceinline__ void tow_bprep(const char* base, int s, int nct, int ct, int lane, uint4 (&x)[3]) {
-  const uint4* p = reinterpret_cast<const uint4*>(base + ((long long)(s * nct + ct) * 3) * 1024) + lane;
-  x[0] = p[0];
-  x[1] = p[64];
-  x[2] = p[128];
+  d[64] = l;
 }
 
 // row of the 32x32 C/D fragment element r of `lane`
 __device__ __forceinline__ int tow_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
-// a layer's B fragments, two k-steps in flight (slot = k-step parity, always a
-// compile-time index): prepared bf16 parts (PREP) or f32 weights split here
-template <bool PREP, int N, bool BF16 = false>
+// a layer's B fragments from the prepared weights, two k-steps in flight (slot =
+// k-step parity, always a compile-time index); H16: the h part only
+template <int N, bool H16 = false>
 struct TowB {
-  const float* w;
   const char* prep;
-  uint4 q[2][3];
-  float4 f[2][2];
+  uint4 q[2][2];
   __device__ __forceinline__ void fetch(int s, int ct, int lane, int slot) {
-    if constexpr (PREP && BF16) {  // the h part only
-      q[slot][0] = reinterpret_cast<const uint4*>(prep + ((long long)(s * (N / 32) + ct) * 3) * 1024)[lane];
-    } else if constexpr (PREP) {
-      tow_bprep(prep, s, N / 32, ct, lane, q[slot]);
-    } else {
-      tow_bload<N>(w, s, 32 * ct, lane, f[slot]);
-    }
+    const uint4* p = reinterpret_cast<const uint4*>(prep + ((long long)(s * (N / 32) + ct) * 2) * 1024) + lane;
+    q[slot][0] = p[0];
+    if constexpr (!H16) q[slot][1] = p[64];
   }
-  __device__ __forceinline__ void get(int slot, bf16x8 (&b)[3]) {
-    if constexpr (PREP) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) b[i] = __builtin_bit_cast(bf16x8, q[slot][i]);
-    } else {
-      tow_split8(f[slot][0], f[slot][1], b);
-    }
+  __device__ __forceinline__ void get(int slot, f16x8 (&b)[2]) {
+    b[0] = as_f16x8(q[slot][0]);
+    if constexpr (!H16) b[1] = as_f16x8(q[slot][1]);
   }
 };
 
-// BF16 (acmi_set_forward_mode ACMI_FWD_BF16): one bf16 MFMA per product -- the
-// weights' h part and conv2/conv3 inputs rounded to bf16 (u8 pixels exact).
-template <int C3, bool PREP, bool BF16 = false>
+// H16 (acmi_set_forward_mode ACMI_FWD_BF16): one f16 MFMA per product on the h
+// parts alone -- every operand rounded once to f16 after its power-of-two scale
+// (11-bit significands, u8 pixels exact; a bf16 forward's precision or better).
+template <int C3, bool H16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, const float* b1,
-                  const float* w2, const float* b2, const float* w3, const float* b3, float* a1g,
-                  float* a2g, float* a3g, long long st, const char* prep) {
+void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, const float* b2,
+                  const float* b3, float* a1g, float* a2g, float* a3g, long long st, const char* prep) {
   using P = TowerPrep<C3>;
+  const unsigned* hdr = reinterpret_cast<const unsigned*>(prep + P::HDR);
+  const float sw1 = f16x2_scale_of_bits(hdr + kTowMaxW1), sw2 = f16x2_scale_of_bits(hdr + kTowMaxW2);
+  const float sw3 = f16x2_scale_of_bits(hdr + kTowMaxW3), sa1 = f16x2_scale_of_bits(hdr + kTowMaxA1);
+  const float sa2 = f16x2_scale_of_bits(hdr + kTowMaxA2);
   __shared__ __attribute__((aligned(16))) char lds[kTowLds + kTowScr];
   char* const imgL = lds;           // u8 image; later a2
   char* const a1L = lds + kTowObs;  // a1; later conv3 scratch
@@ -201,30 +243,27 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
-    TowB<PREP, 32, BF16> bw{w1, prep + P::O1};
+    TowB<32, H16> bw{prep + P::O1};
     bw.fetch(0, 0, lane, 0);
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       if (s + 1 < 16) bw.fetch(s + 1, 0, lane, (s + 1) & 1);
-      bf16x8 b[3];
+      f16x8 b[2];
       bw.get(s & 1, b);
       const int koff = (s >> 1) * 336 + 16 * (s & 1);  // kernel row kh = s/2, kw half
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (u == 3 && (w < 2 || (s >> 3) != w - 2)) continue;
-        const bf16x8 a = u8x8_to_bf16(*reinterpret_cast<const uint2*>(imgL + abase[u] + koff));
-        if constexpr (!BF16) {
-          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[2], acc[u], 0, 0, 0);
-          acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[1], acc[u], 0, 0, 0);
-        }
-        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[0], acc[u], 0, 0, 0);
+        const f16x8 a = u8x8_to_f16(*reinterpret_cast<const uint2*>(imgL + abase[u] + koff));
+        if constexpr (!H16) acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[1], acc[u], 0, 0, 0);
+        acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[0], acc[u], 0, 0, 0);
       }
     }
-    const float bias = b1[col];
+    const float bias = b1[col], inv1 = 1.0f / sw1;
     float* g = a1g + img * st * 12800;
     auto emit1 = [&](int p, float v) {
-      v = fmaxf(__builtin_fmaf(v, 1.0f / 255.0f, bias), 0.f);
+      v = fmaxf(__builtin_fmaf(v * inv1, 1.0f / 255.0f, bias), 0.f);
       *reinterpret_cast<float*>(a1L + tow_pos<32, 2>(p, p % 20, col >> 2) + 4 * (col & 3)) = v;
       g[p * 32 + col] = v;
     };
@@ -263,12 +302,12 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
     f32x16 accF, accH;
 #pragma unroll
     for (int r = 0; r < 16; ++r) accF[r] = accH[r] = 0.f;
-    TowB<PREP, 64, BF16> bw{w2, prep + P::O2};
+    TowB<64, H16> bw{prep + P::O2};
     bw.fetch(0, ct, lane, 0);
 #pragma unroll
     for (int s = 0; s < 32; ++s) {
       if (s + 1 < 32) bw.fetch(s + 1, ct, lane, (s + 1) & 1);
-      bf16x8 b[3];
+      f16x8 b[2];
       bw.get(s & 1, b);
       const int tap = s >> 1, kh = tap >> 2, kw = tap & 3;
       const int ch = 4 * (s & 1) + 2 * kh8;
@@ -278,16 +317,15 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
         const int p = pin[u] + kh * 20 + kw, x = px[u] + kw;
         const float4 x0 = *reinterpret_cast<const float4*>(a1L + tow_pos<32, 2>(p, x, ch));
         const float4 x1 = *reinterpret_cast<const float4*>(a1L + tow_pos<32, 2>(p, x, ch + 1));
-        bf16x8 a[3];
-        if constexpr (BF16) {
-          a[0] = tow_bf16x8(x0, x1);
-          if (u == 0) accF = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], accF, 0, 0, 0);
-          else accH = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], accH, 0, 0, 0);
+        f16x8 a[2];
+        split2x8(x0, x1, sa1, a[0], a[1]);
+        if constexpr (H16) {
+          if (u == 0) accF = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], accF, 0, 0, 0);
+          else accH = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], accH, 0, 0, 0);
           continue;
         }
-        tow_split8(x0, x1, a);
-        if (u == 0) accF = mfma_x3(a, b, accF);
-        else accH = mfma_x3(a, b, accH);
+        if (u == 0) accF = mfma_x2(a, b, accF);
+        else accH = mfma_x2(a, b, accH);
       }
     }
     // row tile 2: the second K half (waves 2, 3) through LDS to the first
@@ -301,10 +339,10 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
     }
     __syncthreads();
     const int c = 32 * ct + col;
-    const float bias = b2[c];
+    const float bias = b2[c], inv2 = 1.0f / (sa1 * sw2);  // exact: powers of two
     float* g = a2g + img * st * 5184;
     auto emit = [&](int p, float v) {
-      v = fmaxf(__builtin_fmaf(v, 1.0f, bias), 0.f);
+      v = fmaxf(__builtin_fmaf(v, inv2, bias), 0.f);
       *reinterpret_cast<float*>(imgL + tow_pos<64, 1>(p, p % 9, c >> 2) + 4 * (c & 3)) = v;
       g[p * 64 + c] = v;
     };
@@ -335,31 +373,31 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    TowB<PREP, C3, BF16> bw{w3, prep + P::O3};
+    TowB<C3, H16> bw{prep + P::O3};
     bw.fetch(s0, ct, lane, 0);
     for (int s = s0; s < s1; s += 2) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int ss = s + h;
         if (ss + 1 < s1) bw.fetch(ss + 1, ct, lane, h ^ 1);
-        bf16x8 b[3];
+        f16x8 b[2];
         bw.get(h, b);
         const int tap = ss >> 2, kh = tap / 3, kw = tap - kh * 3;
         const int ch = 4 * (ss & 3) + 2 * kh8;
         const int p = pin + kh * 9 + kw, x = ow + kw;
         const float4 x0 = *reinterpret_cast<const float4*>(imgL + tow_pos<64, 1>(p, x, ch));
         const float4 x1 = *reinterpret_cast<const float4*>(imgL + tow_pos<64, 1>(p, x, ch + 1));
-        bf16x8 a[3];
-        if constexpr (BF16) {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tow_bf16x8(x0, x1), b[0], acc, 0, 0, 0);
+        f16x8 a[2];
+        split2x8(x0, x1, sa2, a[0], a[1]);
+        if constexpr (H16) {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], acc, 0, 0, 0);
           continue;
         }
-        tow_split8(x0, x1, a);
-        acc = mfma_x3(a, b, acc);
+        acc = mfma_x2(a, b, acc);
       }
     }
     const int c = 32 * ct + col;
-    const float bias = b3[c];
+    const float bias = b3[c], inv3 = 1.0f / (sa2 * sw3);
     float* g = a3g + img * st * (49 * C3);
     if constexpr (C3 == 32) {  // the second K half (waves 2, 3) through LDS to the first
       float* scr = reinterpret_cast<float*>(a1L);  // [rt][32 rows][32]
@@ -373,7 +411,7 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
         for (int r = 0; r < 16; ++r) {
           const int p = 32 * rt + tow_row(r, lane);
           if (p < 49)
-            g[p * C3 + c] = fmaxf(__builtin_fmaf(acc[r] + scr[(rt * 32 + tow_row(r, lane)) * 32 + col], 1.0f,
+            g[p * C3 + c] = fmaxf(__builtin_fmaf(acc[r] + scr[(rt * 32 + tow_row(r, lane)) * 32 + col], inv3,
                                                  bias), 0.f);
         }
       }
@@ -381,31 +419,36 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* w1, con
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int p = 32 * rt + tow_row(r, lane);
-        if (p < 49) g[p * C3 + c] = fmaxf(__builtin_fmaf(acc[r], 1.0f, bias), 0.f);
+        if (p < 49) g[p * C3 + c] = fmaxf(__builtin_fmaf(acc[r], inv3, bias), 0.f);
       }
     }
   }
 }
 
+// prep: acmi_conv_prepare's fragments + bounds (required)
 template <int C3>
 inline void launch_tower(const uint8_t* obs, long long img_stride, int B, const float* P,
                          const long long* off, float* a1, float* a2, float* a3, long long st,
-                         const void* prep, hipStream_t s, bool bf16 = false) {
-#define ACMI_TOWER(PR, BF)                                                                            \
-  hipLaunchKernelGGL((tower_kernel<C3, PR, BF>), dim3(B), dim3(256), 0, s, obs, img_stride, P + off[0], \
-                     P + off[1], P + off[2], P + off[3], P + off[4], P + off[5], a1, a2, a3, st,       \
-                     static_cast<const char*>(prep))
-  if (prep && bf16) ACMI_TOWER(true, true);
-  else if (prep) ACMI_TOWER(true, false);
-  else if (bf16) ACMI_TOWER(false, true);
-  else ACMI_TOWER(false, false);
-#undef ACMI_TOWER
+                         const void* prep, hipStream_t s, bool h16 = false) {
+  const char* pp = static_cast<const char*>(prep);
+  if (h16)
+    hipLaunchKernelGGL((tower_kernel<C3, true>), dim3(B), dim3(256), 0, s, obs, img_stride, P + off[1],
+                       P + off[3], P + off[5], a1, a2, a3, st, pp);
+  else
+    hipLaunchKernelGGL((tower_kernel<C3, false>), dim3(B), dim3(256), 0, s, obs, img_stride, P + off[1],
+                       P + off[3], P + off[5], a1, a2, a3, st, pp);
 }
 
+// the header must be zero before the stats kernel's atomicMax (memset by the caller)
 inline void launch_tower_prep(const float* P, const long long* off, int C3, void* prep, hipStream_t s) {
+  const long long hdr = C3 == 32 ? TowerPrep<32>::HDR : TowerPrep<64>::HDR;
+  unsigned* h = reinterpret_cast<unsigned*>(static_cast<char*>(prep) + hdr);
+  hipLaunchKernelGGL(tower_stats_kernel, dim3(64), dim3(256), 0, s, P + off[0], P + off[1], P + off[2],
+                     P + off[3], P + off[4], 576 * C3, P + off[6], 49 * C3 * 512, h);
+  hipLaunchKernelGGL(tower_stats3_kernel, dim3(C3), dim3(64), 0, s, P + off[4], P + off[5], C3, h);
   const int frags = 16 + 64 + 36 * (C3 / 32);
   hipLaunchKernelGGL(tower_prep_kernel, dim3(frags * 64 / 256 + 1), dim3(256), 0, s, P + off[0], P + off[2],
-                     P + off[4], C3, static_cast<char*>(prep));
+                     P + off[4], C3, static_cast<char*>(prep), h);
 }
 
 }  // namespace acmi

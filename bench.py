@@ -39,6 +39,8 @@ BF16_MFMA_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA: 256 CUs x 4 SIMDs x 1024 FLOP
 # bf16x3 split operands: six bf16 MFMAs per f32-accurate product tile, so the
 # f32-equivalent ceiling of that arithmetic is the bf16 peak / 6
 X3_F32EQ_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
+# f16x2 split operands (f16x2.hpp): three f16 MFMAs (f16 dense peak = bf16's)
+F16X2_F32EQ_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
 HBM_PEAK_GBS = 8000.0
 PMC_PACKAGE = 'r02_final'  # profiles/<this>/: the current measurement package
 
@@ -247,7 +249,7 @@ def run(args):
         _lib.call('acmi_band_info', 1, C3, M, info)
         kern_flops = exec_flops = 2.0 * 64 * 64 * info[0] * M
         kern_name = ('conv2 band reduction: wgrad + K-FAC A factor over pixel-pair sub-tiles '
-                     '(bf16x3 split-operand MFMA, f32-accurate)')
+                     '(f16x2 split-operand MFMA, f32-accurate)')
     elif acktr:
         kern_flops = patch_flops
         exec_flops = 2.0 * 44 * 64 * 64 * rows
@@ -257,7 +259,9 @@ def run(args):
         kern_flops = 2.0 * 513 * 64 * rows
         exec_flops = 2.0 * 8 * 128 * 32 * rows
         kern_name = 'conv2 wgrad reduction GEMM (f32 MFMA)'
-    peak = X3_F32EQ_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
+    # MFMAs per f32-accurate product: 3 (f16x2, band), 6 (bf16x3), 1 (f32 MFMA)
+    nmf = 3 if band else 6 if x3 else 1
+    peak = F16X2_F32EQ_PEAK_TFLOPS if band else X3_F32EQ_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
     kern_ms = tot_ms.value / max(1, cnt.value)
     achieved = kern_flops / (kern_ms * 1e-3) / 1e12 if cnt.value else None
     executed = exec_flops / (kern_ms * 1e-3) / 1e12 if cnt.value else None
@@ -275,11 +279,14 @@ def run(args):
         # the replaced kernel would have needed to match
         roofline['patch_equivalent_tflops'] = patch_flops / (kern_ms * 1e-3) / 1e12
     if x3 and achieved:
-        # peak = bf16 dense peak / 6 (f32-equivalent); the same rate against the
-        # f32-input MFMA peak, and the bf16 MFMA work actually issued
+        # peak = 16-bit dense peak / nmf (f32-equivalent); the same rate against
+        # the f32-input MFMA peak and the bf16x3 ceiling, and the 16-bit MFMA work
+        # actually issued
+        roofline['mfma_per_product'] = nmf
         roofline['frac_of_f32_mfma_peak'] = achieved / FP32_MFMA_PEAK_TFLOPS
-        roofline['executed_bf16_tflops'] = 6 * executed
-        roofline['executed_frac_of_bf16_peak'] = 6 * executed / BF16_MFMA_PEAK_TFLOPS
+        roofline['frac_of_bf16x3_ceiling'] = achieved / X3_F32EQ_PEAK_TFLOPS
+        roofline['executed_16bit_tflops'] = nmf * executed
+        roofline['executed_frac_of_16bit_peak'] = nmf * executed / BF16_MFMA_PEAK_TFLOPS
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -51,16 +51,19 @@ int acmi_get_gemm_mode(void);
 /* Precision of the forward's conv tower (rollout and update forward; BASELINE
  * configs[4] "bf16 forward / fp32 K-FAC factors" -- an extension, the
  * reference computes in fp32):
- *   ACMI_FWD_F32   bf16x3 split operands, f32-accurate (default)
- *   ACMI_FWD_BF16  one bf16 MFMA per product: weights and conv2/conv3 inputs
- *                  rounded to bf16 (u8 pixels exact), f32 accumulation
+ *   ACMI_FWD_F32   f16x2 split operands (scaled f16 h + l, three MFMAs per
+ *                  product), f32-accurate (default)
+ *   ACMI_FWD_BF16  one 16-bit MFMA per product: weights and conv2/conv3 inputs
+ *                  scaled by powers of two and rounded once to f16 (11-bit
+ *                  significands -- at least bf16's precision; u8 pixels exact),
+ *                  f32 accumulation
  * The backward, the K-FAC statistics and the optimizers stay f32-accurate; they
  * read the activations the forward produced.  Initial mode from ACMI_FORWARD
  * ("bf16" / "f32").  Not stream-ordered: set it between launches.
- * The bf16 arithmetic lives in the fused conv tower only: setting ACMI_FWD_BF16
- * fails (ACMI_ERR_ARG) in ACMI_GEMM_F32 mode, and a forward
- * in that mode fails on observations or an image stride that are not 16-byte
- * aligned -- the mode is never silently ignored. */
+ * The 16-bit arithmetic lives in the fused conv tower only: setting
+ * ACMI_FWD_BF16 fails (ACMI_ERR_ARG) in ACMI_GEMM_F32 mode, and a forward in
+ * that mode fails without net->conv_prep or on observations / an image stride
+ * that are not 16-byte aligned -- the mode is never silently ignored. */
 #define ACMI_FWD_F32 0
 #define ACMI_FWD_BF16 1
 int acmi_set_forward_mode(int mode);
@@ -110,15 +113,19 @@ typedef struct acmi_net {
                             caller re-prepares after every parameter change) */
 } acmi_net_t;
 
-/* The forward's conv tower (bf16x3 mode), fc4 at rollout batches (split-K
- * slabs with a forward workspace) and the backward's conv2 input gradient
- * (acmi_backward, acmi_kfac_output_stats) read their weights as pre-split bf16
- * MFMA fragments when net->conv_prep is set: acmi_conv_prepare writes them
- * (stream-ordered, three small kernels) -- once per parameter version, not per
- * rollout step or update.  With conv_prep == NULL the tower splits the weights
- * itself and fc4 / the conv2 input gradient run on the generic split-per-block
- * GEMM (same results, bit for bit; the sampled-loss chain then stores its
- * conv1-output gradient and reduces its G factor separately). */
+/* The forward's fused conv tower (x3 gemm mode), fc4 at rollout batches
+ * (split-K slabs with a forward workspace) and the backward's conv2 input
+ * gradient (acmi_backward, acmi_kfac_output_stats) read their weights as
+ * pre-split f16x2 MFMA fragments -- scaled f16 (h, l) pairs, with a header of
+ * power-of-two scale bounds (max |W| per layer, weight-derived activation
+ * bounds) -- when net->conv_prep is set: acmi_conv_prepare writes them
+ * (stream-ordered, a few small kernels) -- once per parameter version, not per
+ * rollout step or update.  With conv_prep == NULL the forward runs the
+ * per-layer conv kernels and fc4 / the conv2 input gradient the generic
+ * split-per-block bf16x3 GEMM: f32-class like the prepared path, not
+ * bit-identical to it (the sampled-loss chain then stores its conv1-output
+ * gradient and reduces its G factor separately); the 16-bit forward
+ * (ACMI_FWD_BF16) needs conv_prep. */
 int64_t acmi_conv_prep_bytes(int conv3_filters);
 int acmi_conv_prepare(const acmi_net_t* net, void* conv_prep, acmi_stream_t stream);
 

@@ -5,9 +5,10 @@ in KB), written as the profiles/<round>/pmc_traffic.json that bench.py reads.
 
   python scripts/pmc_traffic.py gpurun_out/pmc_bench3 profiles/r01/pmc_traffic.json [band GRID]
 
-With `band GRID` the kernel is the conv2 band reduction (symred6_kernel with
-EpiBand; the conv3 one has another grid size, GRID = groups x chunks x 512 of
-conv2, acmi_band_info).
+With `band` the kernel is the conv2 band reduction (band.hpp band_kernel; the
+conv3 launch of the same kernel has another grid size: the dispatches are
+grouped by grid size and the group with the larger mean FETCH_SIZE -- conv2 reads
+a1, 2.5x conv3's a2 -- is taken; `band GRID` pins the grid size in threads).
 """
 import collections
 import csv
@@ -23,20 +24,31 @@ ALGO_INPUT_BYTES = 736624640  # a1 patches source + d2 read once (DESIGN.md Roof
 
 
 BAND_KERNEL = ('conv2 band reduction: wgrad + K-FAC A factor over pixel-pair sub-tiles '
-               '(bf16x3 split-operand MFMA, f32-accurate)')
-BAND_MATCH = 'EpiBand'
+               '(f16x2 split-operand MFMA, f32-accurate)')
+BAND_MATCH = 'band_kernel'
+BAND = False
 GRID = None
 
 
 def per_dispatch(d, counter):
     vals = collections.defaultdict(float)
-    for f in glob.glob(os.path.join(d, '*', '*_counter_collection.csv')):
+    grids = {}
+    for f in glob.glob(os.path.join(d, '**', '*_counter_collection.csv'), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if row['Counter_Name'] == counter and MATCH in row['Kernel_Name']:
-                    if GRID is not None and int(row.get('Grid_Size') or row.get('Grid_Size_X')) != GRID:
+                    g = int(row.get('Grid_Size') or row.get('Grid_Size_X'))
+                    if GRID is not None and g != GRID:
                         continue
-                    vals[row['Dispatch_Id']] += float(row['Counter_Value'])
+                    key = (f, row['Dispatch_Id'])
+                    vals[key] += float(row['Counter_Value'])
+                    grids[key] = g
+    if BAND and GRID is None and vals:
+        by = collections.defaultdict(list)
+        for k, v in vals.items():
+            by[grids[k]].append(v)
+        best = max(by, key=lambda g: sum(by[g]) / len(by[g]))
+        return by[best]
     return list(vals.values())
 
 
@@ -67,6 +79,7 @@ def main(d, out):
 
 
 if __name__ == '__main__':
-    if len(sys.argv) > 4 and sys.argv[3] == 'band':
-        KERNEL, MATCH, GRID = BAND_KERNEL, BAND_MATCH, int(sys.argv[4])
+    if len(sys.argv) > 3 and sys.argv[3] == 'band':
+        KERNEL, MATCH, BAND = BAND_KERNEL, BAND_MATCH, True
+        GRID = int(sys.argv[4]) if len(sys.argv) > 4 else None
     main(sys.argv[1], sys.argv[2])

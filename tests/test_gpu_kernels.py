@@ -372,9 +372,11 @@ def test_kfac_eigvals_match_numpy(lib, cuda):
 
 
 @pytest.mark.parametrize('C3', [32, 64])
-def test_conv_prep_forward_bit_identical(lib, cuda, C3):
-    """The conv tower with pre-split weights (acmi_conv_prepare) gives the same
-    activations, bit for bit, as the tower splitting the weights itself."""
+def test_conv_prep_tower_matches_layer_kernels(lib, cuda, C3):
+    """The fused conv tower on acmi_conv_prepare's f16x2 fragments (tower.hpp) and
+    the per-layer kernels a net without conv_prep runs agree to f32 accuracy: every
+    activation within 2e-6 of the other relative to its range, both within 1e-5
+    of the float64 forward."""
     A, B = 4, 37
     params = rand_params(A, C3, cuda, seed=4)
     obs = torch.randint(0, 256, (B, 84, 84, 4), generator=torch.Generator().manual_seed(6),
@@ -390,16 +392,21 @@ def test_conv_prep_forward_bit_identical(lib, cuda, C3):
                   _lib.stream_handle())
         torch.cuda.synchronize()
         outs.append({k: v.cpu() for k, v in t.items()})
+    rel = lambda x, y: ((x.double() - y.double()).abs().max() / max(1e-6, y.double().abs().max())).item()
     for k in outs[0]:
-        assert torch.equal(outs[0][k], outs[1][k]), k
+        assert rel(outs[1][k], outs[0][k]) < 2e-6, (k, rel(outs[1][k], outs[0][k]))
+    ref = torch_forward(params, obs.cpu(), A, C3)
+    for name, r in zip(['a1', 'a2', 'a3', 'a4', 'logits', 'value'], ref):
+        for o in outs:
+            assert rel(o[name].reshape(r.shape), r) < 1e-5, name
 
 
 @pytest.mark.parametrize('C3,B', [(32, 37), (32, 512), (64, 512)])
-def test_fc4_rollout_bit_identical(lib, cuda, C3, B):
-    """fc4's split-K slabs at rollout batches on the pre-split W4 (fc4roll.hpp,
-    used when the net carries conv_prep and a forward workspace) are bit-identical
-    to the staged gemm3 split-K launch (same chunks, same bf16x3 split, same MFMA
-    order), and the forward still matches float64 within 1e-5."""
+def test_fc4_rollout_matches_gemm3(lib, cuda, C3, B):
+    """fc4's split-K slabs at rollout batches on the pre-split f16x2 W4
+    (fc4roll.hpp, used when the net carries conv_prep and a forward workspace)
+    agree with the staged bf16x3 gemm3 split-K launch to f32 accuracy (2e-6 of
+    each tensor's range), and the forward matches float64 within 1e-5."""
     A = 4
     params = rand_params(A, C3, cuda, seed=21)
     obs = torch.randint(0, 256, (B, 84, 84, 4), generator=torch.Generator().manual_seed(22),
@@ -418,7 +425,8 @@ def test_fc4_rollout_bit_identical(lib, cuda, C3, B):
         torch.cuda.synchronize()
         outs.append({k: v.cpu() for k, v in t.items()})
     for k in ('a4', 'logits', 'value'):
-        assert torch.equal(outs[0][k], outs[1][k]), k
+        d = ((outs[1][k].double() - outs[0][k].double()).abs().max() / outs[0][k].double().abs().max()).item()
+        assert d < 2e-6, (k, d)
     ref = torch_forward(params, obs.cpu(), A, C3)
     for name, r in zip(['a1', 'a2', 'a3', 'a4', 'logits', 'value'], ref):
         got = outs[1][name].double().reshape(r.shape)
@@ -428,13 +436,14 @@ def test_fc4_rollout_bit_identical(lib, cuda, C3, B):
 
 @pytest.mark.parametrize('B', [37, 1000])
 def test_convt2_matches_gemm3_path(lib, cuda, B):
-    """conv2's input gradient on pre-split weights (convt2.hpp, used when the net
-    carries conv_prep) is bit-identical to the gemm3 path (same k order, same six
-    bf16 MFMAs per 32x32x16), the parameter gradients and A factors of the whole
-    backward are unchanged, and the sampled-loss chain's conv1 G factor -- reduced
-    from the masked d1 tiles inside the kernel instead of stored and re-read -- is
-    within 2e-6 of float64 d1^T d1 / rows over the stored d1 (B = 1000: some blocks
-    of the Gram grid take two column tiles)."""
+    """conv2's input gradient on pre-split f16x2 weights (convt2.hpp, used when the
+    net carries conv_prep) agrees with the bf16x3 gemm3 path to f32 accuracy (both
+    are f32-class: d1 within 2e-6 of each other relative to max |d1|), so do the
+    parameter gradients and A factors of the whole backward (2e-6), and the
+    sampled-loss chain's conv1 G factor -- reduced from the masked d1 tiles inside
+    the kernel instead of stored and re-read -- is within 2e-6 of float64
+    d1^T d1 / rows over the stored d1 (B = 1000: some blocks of the Gram grid take
+    two column tiles)."""
     A, C3 = 4, 32
     params = rand_params(A, C3, cuda, seed=12)
     g = torch.Generator().manual_seed(13)
@@ -472,25 +481,30 @@ def test_convt2_matches_gemm3_path(lib, cuda, B):
         torch.cuda.synchronize()
         out[use_prep] = (d1_loss.cpu(), grads.cpu(), astat.cpu(), gstat.cpu(), ds[0].cpu())
     (d1a, ga, aa, sa, d1s), (d1b, gb, ab, sb, _) = out[False], out[True]
-    assert torch.equal(d1a, d1b)
-    assert torch.equal(ga, gb)
-    assert torch.equal(aa, ab)
+    rel = lambda x, y: ((x.double() - y.double()).abs().max() / y.double().abs().max()).item()
+    assert rel(d1b, d1a) < 2e-6, rel(d1b, d1a)
+    off, n = _layout(A, C3)
+    ends = off[1:] + [n]
+    for o, e in zip(off, ends):
+        assert rel(gb[o:e], ga[o:e]) < 2e-6, (o, rel(gb[o:e], ga[o:e]))
+    assert rel(ab, aa) < 2e-6
     # G factors: conv1's from the kernel's Gram, the rest unchanged
     o0 = so[5]
     ref = (d1s.double().reshape(-1, 32).t() @ d1s.double().reshape(-1, 32)) / (400 * B)
     got = sb[o0:o0 + 32 * 32].double().reshape(32, 32)
-    rel = (got - ref).abs().max().item() / ref.abs().max().item()
-    assert rel < 2e-6, rel
+    err = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
     assert torch.equal(got, got.t())
-    assert torch.equal(sa[so[6]:], sb[so[6]:])
+    assert rel(sb[so[6]:], sa[so[6]:]) < 2e-6
 
 
 @pytest.mark.parametrize('A,C3,B', [(4, 32, 29), (18, 64, 29), (18, 32, 1024)],
                          ids=['breakout', 'full-actions-c64', 'configs4-shard-1024x18'])
 def test_bf16_forward_mode(lib, cuda, A, C3, B):
     """acmi_set_forward_mode(ACMI_FWD_BF16) (BASELINE configs[4] "bf16 forward"):
-    the conv tower with one bf16 MFMA per product stays within bf16 accuracy of the
-    float64 forward (max error <= 1e-2 of each tensor's range; measured ~2e-3), and
+    the conv tower with one 16-bit MFMA per product (the scaled f16 h parts alone)
+    stays within bf16 accuracy of the float64 forward (max error <= 1e-2 of each
+    tensor's range), and
     switching back restores the f32-accurate tower bit for bit.  The last case is
     the configs[4] shard itself: 1024 images per launch, the full 18-action set,
     C3 = 32 (ACKTR)."""
