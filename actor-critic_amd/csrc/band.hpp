@@ -144,8 +144,12 @@ inline void band_chunks(long long rows, int ngroups, int* nc, int* ch) {
 // zeroed before the dX chain): the bit patterns of max |d3|, |d2| (published by
 // the dX epilogues, gemm.hpp has_amax) and of the a1 / a2 bounds
 // (band_bounds_kernel); the kernels turn them into their operand scales
-constexpr int kBandScratch = 64;
-enum { kBsMaxA1 = 0, kBsMaxA2 = 1, kBsMaxD2 = 2, kBsMaxD3 = 3, kBsMaxW3 = 4, kBsMaxD4 = 5, kBsMaxW4 = 6 };
+// published maxima (kAmaxSlots words each, common.hpp)
+enum {
+  kBsMaxA1 = 0 * kAmaxWords, kBsMaxA2 = 1 * kAmaxWords, kBsMaxD2 = 2 * kAmaxWords, kBsMaxD3 = 3 * kAmaxWords,
+  kBsMaxW3 = 4 * kAmaxWords, kBsMaxD4 = 5 * kAmaxWords, kBsMaxW4 = 6 * kAmaxWords
+};
+constexpr int kBandScratch = 8 * kAmaxWords;
 
 inline long long band_ws_floats(const BandPlan* p, long long rows) {
   if (!p) return 0;
@@ -186,11 +190,11 @@ __global__ __launch_bounds__(256) void band_bounds_kernel(const float* w1, const
   __syncthreads();
   if (t == 0) {
     const float b2c = red[0] + red[1] + red[2] + red[3] + fmaxf(b2[co], 0.f);
-    atomicMax(scr + kBsMaxA2, __float_as_uint(b2c));
+    amax_update(scr + kBsMaxA2, b2c);
     if (co == 0) {
       float m = 0.f;
       for (int c = 0; c < 32; ++c) m = fmaxf(m, B1[c]);
-      atomicMax(scr + kBsMaxA1, __float_as_uint(m));
+      amax_update(scr + kBsMaxA1, m);
     }
   }
 }

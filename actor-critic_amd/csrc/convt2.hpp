@@ -42,7 +42,7 @@ struct CT2 {
   static constexpr int NKS = 16;                    // k16 steps: 4 taps x 64 channels
   static constexpr int STEP_BYTES = 4 * 2 * 1024;   // 4 phases x 2 parts x 64 lanes x 16 B
   static constexpr int FRAG_BYTES = NKS * STEP_BYTES;  // 131,072 B of prepared weights
-  static constexpr int BYTES = FRAG_BYTES + 16;     // + max |W2| (bit pattern) and padding
+  static constexpr int BYTES = FRAG_BYTES + 4 * kAmaxWords;  // + max |W2| (published, common.hpp)
   static constexpr int TILE = 128;                  // columns per block tile (4 waves x 32)
 };
 
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void convt2_wmax_kernel(const float* w2, char*
   for (int i = blockIdx.x * 256 + threadIdx.x; i < 16 * CT2::CIN * CT2::COUT; i += gridDim.x * 256)
     m = fmaxf(m, fabsf(w2[i]));
   m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(out + CT2::FRAG_BYTES), __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) amax_update(reinterpret_cast<unsigned*>(out + CT2::FRAG_BYTES), m);
 }
 
 // prepared weights: fragment (ks, phase) lane l holds W[py+2a][px+2b][ci][co..co+7],

@@ -31,8 +31,9 @@ __device__ __forceinline__ float f16x2_scale(float mx) {
   (void)frexpf(mx, &e);  // mx < 2^e
   return ldexpf(1.f, 14 - e);
 }
+// the scale of a published bound (common.hpp amax_read: all 64 lanes active)
 __device__ __forceinline__ float f16x2_scale_of_bits(const unsigned* mx) {
-  return f16x2_scale(__uint_as_float(*mx));
+  return f16x2_scale(amax_read(mx));
 }
 
 __device__ __forceinline__ uint32_t pk_f16(float a, float b) {
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* x, long long n
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
     m = fmaxf(m, fabsf(x[i]));
   m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) amax_update(out, m);
 }
 
 }  // namespace acmi

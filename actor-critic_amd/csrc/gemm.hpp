@@ -76,8 +76,8 @@ struct has_vec4<T, std::void_t<decltype(T::VEC4)>> : std::integral_constant<bool
 
 // Epilogues with a member `unsigned* amax` (nullable) also publish the largest
 // |value| they stored: store/store4 return what they wrote, each wave takes the
-// max of its lanes and one lane atomicMax-es its bit pattern (non-negative floats
-// order as their bits) into *amax, zeroed by the caller before the launch.  The
+// max of its lanes and one lane publishes it (amax_update: atomicMax of the bit
+// pattern when larger) into *amax, zeroed by the caller before the launch.  The
 // band reductions and the f16x2 operand splits scale a tensor by it (band.hpp).
 template <class T, class = void>
 struct has_amax : std::false_type {};
@@ -86,7 +86,7 @@ struct has_amax<T, std::void_t<decltype(std::declval<T&>().amax)>> : std::true_t
 
 __device__ __forceinline__ void amax_publish(unsigned* amax, float m, int lane) {
   m = wave_max(m);
-  if (amax && lane == 0) atomicMax(amax, __float_as_uint(m));
+  if (amax && lane == 0) amax_update(amax, m);
 }
 __device__ __forceinline__ float absmax4(float m, float4 v) {
   return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));

@@ -106,17 +106,23 @@ bool get_layout(int A, int C3, Layout* L) { return make_layout(A, C3, L); }
 // ---------------------------------------------------------------------------
 // d4 = (dhead [W_pi | w_v]^T) * relu'(a4): A+1 MACs per output, elementwise
 // over [B][512] (memory-bound); the k-ordered fmaf chain is the f32 MFMA's.
-// amax (nullable): max |d4| published for fc4's f16x2 input gradient (every
-// lane reaches the wave reduction; out-of-range lanes contribute 0)
-__device__ __forceinline__ void publish_max4(unsigned* amax, float4 r, bool ok) {
-  if (!amax) return;
-  float mx = ok ? fmaxf(fmaxf(fabsf(r.x), fabsf(r.y)), fmaxf(fabsf(r.z), fabsf(r.w))) : 0.f;
-  mx = wave_max(mx);
-  if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(mx));
+// amax (nullable): max |d4| published for fc4's f16x2 input gradient, once per
+// block (common.hpp amax_update; every thread reaches the block reduction,
+// out-of-range ones contribute 0)
+__device__ __forceinline__ void block_amax256(unsigned* amax, float m) {
+  __shared__ float red[4];
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) amax_update(amax, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+__device__ __forceinline__ float absmax4f(float4 r) {
+  return fmaxf(fmaxf(fabsf(r.x), fabsf(r.y)), fmaxf(fabsf(r.z), fabsf(r.w)));
 }
 
-__global__ void heads_dx_kernel(const float* dhead, int ldh, int B, const float* wpi,
-                                const float* wv, int A, const float* a4, float* d4, unsigned* amax) {
+__global__ __launch_bounds__(256) void heads_dx_kernel(const float* dhead, int ldh, int B, const float* wpi,
+                                                       const float* wv, int A, const float* a4, float* d4,
+                                                       unsigned* amax) {
   // 4 consecutive outputs per thread (float4 a4 / d4)
   const long long q0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool ok = q0 < (long long)B * 128;
@@ -141,14 +147,15 @@ __global__ void heads_dx_kernel(const float* dhead, int ldh, int B, const float*
   o.z = acc[2] * (float)(x.z > 0.f);
   o.w = acc[3] * (float)(x.w > 0.f);
   if (ok) *reinterpret_cast<float4*>(d4 + q * 4) = o;
-  publish_max4(amax, o, ok);
+  if (amax) block_amax256(amax, ok ? absmax4f(o) : 0.f);
 }
 
 // Breakout's A = 4 (16-byte aligned W_pi rows, dhead rows of ldh % 4 == 0): the
 // four W_pi rows and the dhead row as float4 loads (7 loads a thread instead of 26),
 // the same k-ordered fmaf chain per output
-__global__ void heads_dx4_kernel(const float* dhead, int ldh, int B, const float* wpi,
-                                 const float* wv, const float* a4, float* d4, unsigned* amax) {
+__global__ __launch_bounds__(256) void heads_dx4_kernel(const float* dhead, int ldh, int B, const float* wpi,
+                                                        const float* wv, const float* a4, float* d4,
+                                                        unsigned* amax) {
   const long long q0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool ok = q0 < (long long)B * 128;
   const long long q = ok ? q0 : 0;
@@ -174,7 +181,7 @@ __global__ void heads_dx4_kernel(const float* dhead, int ldh, int B, const float
   r.z = o[2] * (float)(x.z > 0.f);
   r.w = o[3] * (float)(x.w > 0.f);
   if (ok) *reinterpret_cast<float4*>(d4 + q * 4) = r;
-  publish_max4(amax, r, ok);
+  if (amax) block_amax256(amax, ok ? absmax4f(r) : 0.f);
 }
 
 // conv/fc epilogue with an image remap so the rollout can write step t of an
@@ -1347,11 +1354,13 @@ int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
   const long long o2 = L.C3 == 32 ? TowerPrep<32>::BYTES : TowerPrep<64>::BYTES;
   const long long oh = L.C3 == 32 ? TowerPrep<32>::HDR : TowerPrep<64>::HDR;
   // the tower's bounds header (atomicMax targets), then its f16x2 fragments
-  ACMI_REQUIRE(hipMemsetAsync(static_cast<char*>(prep) + oh, 0, 32, (hipStream_t)stream) == hipSuccess,
+  ACMI_REQUIRE(hipMemsetAsync(static_cast<char*>(prep) + oh, 0, TowerPrep<32>::HDR_BYTES, (hipStream_t)stream) ==
+                   hipSuccess,
                ACMI_ERR_HIP, "acmi_conv_prepare: memset failed");
   launch_tower_prep(net->params, L.off, L.C3, prep, (hipStream_t)stream);
   // conv2's input-gradient weights: max |W2| (the f16x2 scale), then the split
-  ACMI_REQUIRE(hipMemsetAsync(static_cast<char*>(prep) + o2 + CT2::FRAG_BYTES, 0, 16, (hipStream_t)stream) ==
+  ACMI_REQUIRE(hipMemsetAsync(static_cast<char*>(prep) + o2 + CT2::FRAG_BYTES, 0, CT2::BYTES - CT2::FRAG_BYTES,
+                              (hipStream_t)stream) ==
                    hipSuccess,
                ACMI_ERR_HIP, "acmi_conv_prepare: memset failed");
   hipLaunchKernelGGL(convt2_wmax_kernel, dim3(32), dim3(256), 0, (hipStream_t)stream, net->params + L.off[2],

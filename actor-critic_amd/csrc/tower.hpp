@@ -74,10 +74,14 @@ struct TowerPrep {
   static constexpr long long O1 = 0, N1 = 16 * 1;             // conv1: 16 steps x 1 tile
   static constexpr long long O2 = O1 + N1 * FRAG, N2 = 32 * 2;  // conv2: 32 x 2
   static constexpr long long O3 = O2 + N2 * FRAG, N3 = 36 * (C3 / 32);
-  static constexpr long long HDR = O3 + N3 * FRAG;            // 8 words of bounds
-  static constexpr long long BYTES = HDR + 32;
+  static constexpr long long HDR = O3 + N3 * FRAG;  // 8 published bounds (common.hpp)
+  static constexpr long long HDR_BYTES = 8 * 4 * kAmaxWords;
+  static constexpr long long BYTES = HDR + HDR_BYTES;
 };
-enum { kTowMaxW1 = 0, kTowMaxW2 = 1, kTowMaxW3 = 2, kTowMaxA1 = 3, kTowMaxA2 = 4, kTowMaxA3 = 5, kTowMaxW4 = 6 };
+enum {
+  kTowMaxW1 = 0 * kAmaxWords, kTowMaxW2 = 1 * kAmaxWords, kTowMaxW3 = 2 * kAmaxWords, kTowMaxA1 = 3 * kAmaxWords,
+  kTowMaxA2 = 4 * kAmaxWords, kTowMaxA3 = 5 * kAmaxWords, kTowMaxW4 = 6 * kAmaxWords
+};
 
 // the header's bounds (zeroed by the caller): 64 blocks of band.hpp's a1 / a2
 // bounds (block c' takes conv2's column c') plus max |W| over all four layers
@@ -116,18 +120,18 @@ __global__ __launch_bounds__(256) void tower_stats_kernel(const float* w1, const
   m3 = wave_max(m3);
   m4 = wave_max(m4);
   if ((t & 63) == 0) {
-    atomicMax(hdr + kTowMaxW1, __float_as_uint(m1));
-    atomicMax(hdr + kTowMaxW2, __float_as_uint(m2));
-    atomicMax(hdr + kTowMaxW3, __float_as_uint(m3));
-    atomicMax(hdr + kTowMaxW4, __float_as_uint(m4));
+    amax_update(hdr + kTowMaxW1, m1);
+    amax_update(hdr + kTowMaxW2, m2);
+    amax_update(hdr + kTowMaxW3, m3);
+    amax_update(hdr + kTowMaxW4, m4);
   }
   __syncthreads();
   if (t == 0) {
-    atomicMax(hdr + kTowMaxA2, __float_as_uint(red[0] + red[1] + red[2] + red[3] + fmaxf(b2[co], 0.f)));
+    amax_update(hdr + kTowMaxA2, red[0] + red[1] + red[2] + red[3] + fmaxf(b2[co], 0.f));
     if (co == 0) {
       float m = 0.f;
       for (int c = 0; c < 32; ++c) m = fmaxf(m, B1[c]);
-      atomicMax(hdr + kTowMaxA1, __float_as_uint(m));
+      amax_update(hdr + kTowMaxA1, m);
     }
   }
 }
@@ -140,7 +144,8 @@ __global__ __launch_bounds__(64) void tower_stats3_kernel(const float* w3, const
   float acc = 0.f;
   for (int k = t; k < 576; k += 64) acc += fmaxf(w3[k * C3 + co], 0.f);
   acc = wave_sum(acc);
-  if (t == 0) atomicMax(hdr + kTowMaxA3, __float_as_uint(acc * __uint_as_float(hdr[kTowMaxA2]) + fmaxf(b3[co], 0.f)));
+  const float a2 = amax_read(hdr + kTowMaxA2);
+  if (t == 0) amax_update(hdr + kTowMaxA3, acc * a2 + fmaxf(b3[co], 0.f));
 }
 
 __global__ void tower_prep_kernel(const float* w1, const float* w2, const float* w3, int C3, char* out,
@@ -161,7 +166,7 @@ __global__ void tower_prep_kernel(const float* w1, const float* w2, const float*
   } else {
     return;
   }
-  const float sw = f16x2_scale_of_bits(hdr + layer);
+  const float sw = f16x2_scale_of_bits(hdr + layer * kAmaxWords);  // (f, so layer, is wave-uniform)
   const float* p = w + (16 * s + 8 * (lane >> 5)) * N + 32 * ct + (lane & 31);
   uint4 h, l;
   split2(p[0], p[N], sw, h.x, l.x);
