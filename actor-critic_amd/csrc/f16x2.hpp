@@ -17,7 +17,7 @@
 // bound of a ReLU activation (band.hpp band_bounds_kernel).
 #pragma once
 
-#include "symred3.hpp"  // f32x2v, s16x4/8, ds_tr16
+#include "split16.hpp"  // f32x2v, s16x4/8, ds_tr16
 
 namespace acmi {
 
@@ -73,7 +73,7 @@ __device__ __forceinline__ f32x16 mfma_x2(const f16x8 (&a)[2], const f16x8 (&b)[
 
 // max |x| over n floats (a weight matrix) into *out (zeroed by the caller):
 // grid-stride loads, one atomicMax per wave
-__global__ __launch_bounds__(256) void absmax_kernel(const float* x, long long n, unsigned* out) {
+static __global__ __launch_bounds__(256) void absmax_kernel(const float* x, long long n, unsigned* out) {
   float m = 0.f;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
     m = fmaxf(m, fabsf(x[i]));

@@ -120,7 +120,10 @@ struct X3Image {
 template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM, class OpA, class OpB,
           class Epi, bool F16 = false>
 __global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(gemm3_blocks_per_cu<BM, BN, BK, F16 ? 2 : 3>())))
+// (occupancy of the three-part LDS image in both forms: the two-part image would
+// allow more blocks, but its register budget then spills -- measured 30-390 VGPRs
+// of spill and 1.4-3x the time at 64x128 .. 128x256)
+__attribute__((amdgpu_waves_per_eu(gemm3_blocks_per_cu<BM, BN, BK, 3>())))
 void gemm3_kernel(OpA opA, OpB opB, Epi epi, int I, int J, int K, int k_chunk, int sym_cols,
                   const unsigned* amax_a = nullptr, const unsigned* amax_b = nullptr) {
   using TL = Tile<BM, BN, BK, WTM, WTN>;

@@ -857,7 +857,7 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
                        int ldy, int cout, bool with_stats, float* part,
                        long long part_cap, float* gradA, int nsplit,
                        float* gradB, float* astat, hipStream_t s, int site = 0,
-                       float wscale = 1.f) {
+                       float wscale = 1.f, const unsigned* pmax = nullptr, const unsigned* ymax = nullptr) {
   constexpr bool kU8 = !std::is_same<typename Src::elem_t, float>::value;
   const int mode = g_gemm_mode;
   const WgradPlan pl = wgrad_plan(K, cout, with_stats, rows, kU8, mode);
@@ -871,8 +871,8 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
   EpiPartial epi{part, I, J};
   prof_begin(site, s);
   if constexpr (std::is_same<typename Src::elem_t, float>::value) {
-    if (pl.six)  // six-slab groups, bf16x3 split operands
-      launch_symred6(opB, epi, pl.sp6, I, J, (int)rows, nc, ch, s);
+    if (pl.six)  // six-slab groups, bf16x3 split operands (f16x2 with published bounds)
+      launch_symred6(opB, epi, pl.sp6, I, J, (int)rows, nc, ch, s, pmax, ymax, kp);
     else if (pl.slabs && mode == ACMI_GEMM_X3)  // slab groups, bf16x3 split operands
       launch_symred3(opB, epi, pl.sp, I, J, (int)rows, nc, ch, s);
     else if (pl.slabs)  // slab groups over the upper triangle of P^T P and the dY columns
@@ -1021,8 +1021,10 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     RowsAsK<DenseRows> opA{DenseRows{bw->d4, 512, B, 512}};
     MatTK<true> opB{P + L.off[6], 512, 512, K3};
     EpiReluGrad epi{bw->d3, a->a3, K3, dxs + kBsMaxD3};
+    // f16x2 on 128 x 64 tiles, BK = 32 (per launch at M = 10240: 89.8 us; 64 x 128
+    // 107, 128 x 128 96.6, 64 x 128 / BK 32 97.1, 256 x 128 127.7; bf16x3 64 x 128 132)
     if (g_gemm_mode == ACMI_GEMM_X3)
-      launch_gemm3_f16<64, 128, 16, 1, 2>(opA, opB, epi, B, K3, 512, dxs + kBsMaxD4, w4max, s);
+      launch_gemm3_f16<128, 64, 32, 2, 1>(opA, opB, epi, B, K3, 512, dxs + kBsMaxD4, w4max, s);
     else
       launch_mm<64, 128, 32, 1, 2, false, false, 16>(opA, opB, epi, B, K3, 512, 1, 0, s);
   }
@@ -1114,10 +1116,13 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
                    part, ws_cap, grads + L.off[8], L.A, grads + L.off[10],
                    st ? astat + L.stat_off[4] : nullptr, s);
   if (rc) return rc;
-  // fc4: X = a3 flat
+  // fc4: X = a3 flat; f16x2 with the prepared weights' a3 bound and max |d4|
+  // (published by the dX chain's heads kernel)
+  const unsigned* a3b =
+      prep ? reinterpret_cast<const unsigned*>(prep + TowerPrep<C3>::HDR) + kTowMaxA3 : nullptr;
   rc = wgrad_layer(DenseRows{a->a3, 49 * C3, B, 49 * C3}, 49 * C3, B, bw->d4, 512, 512, st,
                    part, ws_cap, grads + L.off[6], 512, nullptr,
-                   st ? astat + L.stat_off[3] : nullptr, s);
+                   st ? astat + L.stat_off[3] : nullptr, s, 0, 1.f, a3b, a3b ? bscr + kBsMaxD4 : nullptr);
   if (rc) return rc;
   // conv3 / conv2: pixel-pair band reductions over the dense activation rows
   // (band.hpp), or the patches of a2 / a1

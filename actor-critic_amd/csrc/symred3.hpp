@@ -42,53 +42,10 @@
 #include <random>
 #include <vector>
 
+#include "f16x2.hpp"  // split3, mfma_x3, ds_tr16, cat8 (split16.hpp); split2, mfma_x2
 #include "symred.hpp"
 
 namespace acmi {
-
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-
-// (a, b) -> packed bf16 pair, round-to-nearest-even (v_cvt_pk_bf16_f32)
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
-  const f32x2v v = {a, b};
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
-}
-
-// three-term split of the pair (a, b): h + m + l == (a, b) to 2^-24 relative
-__device__ __forceinline__ void split3(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
-  h = pk_bf16(a, b);
-  const float ra = a - __uint_as_float(h << 16);
-  const float rb = b - __uint_as_float(h & 0xffff0000u);
-  m = pk_bf16(ra, rb);
-  const float sa = ra - __uint_as_float(m << 16);
-  const float sb = rb - __uint_as_float(m & 0xffff0000u);
-  l = pk_bf16(sa, sb);
-}
-
-__device__ __forceinline__ s16x4 ds_tr16(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s16x4*)(p));
-}
-
-__device__ __forceinline__ bf16x8 cat8(s16x4 a, s16x4 b) {
-  const s16x8 v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// six-product bf16x3 step on one accumulator
-__device__ __forceinline__ f32x16 mfma_x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
-  return c;
-}
 
 constexpr int kX3Rows = 16;                 // k-rows per stage
 constexpr int kX3RowBytes = 512;            // 256 bf16 columns
@@ -254,280 +211,6 @@ void symred3_kernel(Op op, Epi epi, SymPlan plan, int I, int J, int K, int k_chu
     for (int r = 0; r < 8; ++r) t += cs[r * 256 + col];
     if (jb + lane < J) epi.colsum(jb + lane, t);
   }
-}
-
-// ---------------------------------------------------------------------------
-// Wide groups: two 64x64 sub-tiles per wave, eight per block from the same
-// four staged slabs.  The split-K reduction streams every staged row from L2
-// once per group, and with one sub-tile per wave the load rate it needs to keep
-// the MFMAs busy (~10 TB/s chip-wide at conv2's shape) is about twice what the
-// gather sustains (the no-MFMA probe: 0.87 ms of 1.5); eight sub-tiles per
-// staged byte halve the groups (conv2 11 -> 6, conv3 14 -> 7).  Accumulators
-// 2 x 64 registers -> 2 waves per SIMD, 2 blocks per CU.
-// ---------------------------------------------------------------------------
-struct SymGroup2 {
-  int16_t base[4];  // first [P | dY] column of each staged slab (-1: none)
-  int8_t ra[4][2];  // per wave and tile: staged slab of the rows (-1: no tile)
-  int8_t cb[4][2];  // per wave and tile: staged slab of the columns
-};
-constexpr int kSym2MaxGroups = 48;
-struct SymPlan2 {
-  int ngroups;
-  SymGroup2 g[kSym2MaxGroups];
-};
-
-// Greedy cover of the needed sub-tiles -- (a, b), a <= b < nb over the P slabs
-// and (a, dY) -- by groups of <= 4 slabs and <= 8 sub-tiles: each round takes
-// the slab set that covers the most remaining sub-tiles.  Within a wave the
-// dY sub-tile (possibly a half slab) comes second, so the kernel needs only
-// the (1 or 2 tiles) x (second tile half or not) loop variants.  K % 64 == 0.
-inline bool sym_plan2(int K, int cout_pad, SymPlan2* p) {
-  if (K % 64 != 0 || cout_pad > 64 || cout_pad <= 0) return false;
-  const int nb = K / 64, ns = nb + 1;  // slab nb = dY
-  if (ns > 16) return false;
-  bool need[16][16] = {};
-  int left = 0;
-  for (int a = 0; a < nb; ++a)
-    for (int b = a; b < ns; ++b) need[a][b] = true, ++left;
-  int n = 0;
-  while (left > 0) {
-    if (n >= kSym2MaxGroups) return false;
-    int best = -1, bestc = 0, bs[4] = {0, 0, 0, 0};
-    for (int s0 = 0; s0 < ns; ++s0)
-      for (int s1 = s0 + 1; s1 < ns; ++s1)
-        for (int s2 = s1 + 1; s2 < ns; ++s2)
-          for (int s3 = s2 + 1; s3 <= ns; ++s3) {  // s3 == ns: three slabs
-            const int sl[4] = {s0, s1, s2, s3 < ns ? s3 : -1};
-            int c = 0;
-            for (int x = 0; x < 4; ++x)
-              for (int y = x; y < 4; ++y)
-                if (sl[x] >= 0 && sl[y] >= 0 && need[sl[x]][sl[y]]) ++c;
-            c = std::min(c, 8);
-            if (c > bestc) {
-              bestc = c;
-              best = 1;
-              for (int x = 0; x < 4; ++x) bs[x] = sl[x];
-            }
-          }
-    if (best < 0) {  // fewer than 3 slabs' worth left (e.g. only (0,0) with nb == 1)
-      for (int a = 0; a < nb && best < 0; ++a)
-        for (int b = a; b < ns && best < 0; ++b)
-          if (need[a][b]) {
-            bs[0] = a;
-            bs[1] = b != a ? b : -1;
-            bs[2] = bs[3] = -1;
-            best = 1;
-          }
-    }
-    // collect up to 8 tiles of this slab set: P x P first, dY tiles last
-    int ta[8], tb[8], nt = 0;
-    for (int pass = 0; pass < 2; ++pass)
-      for (int x = 0; x < 4; ++x)
-        for (int y = 0; y < 4; ++y) {
-          if (bs[x] < 0 || bs[y] < 0 || nt >= 8) continue;
-          const int a = bs[x], b = bs[y];
-          if (a > b || !need[a][b] || (b == nb) != (pass == 1)) continue;
-          need[a][b] = false;
-          --left;
-          ta[nt] = x;
-          tb[nt] = y;
-          ++nt;
-        }
-    // waves take tiles in pairs; P x P tiles fill first-tile slots, so a dY
-    // tile is a wave's second tile unless both of its tiles are dY tiles
-    SymGroup2& G = p->g[n++];
-    for (int x = 0; x < 4; ++x) G.base[x] = (int16_t)(bs[x] < 0 ? -1 : (bs[x] == nb ? K : 64 * bs[x]));
-    for (int w = 0; w < 4; ++w)
-      for (int t = 0; t < 2; ++t) G.ra[w][t] = G.cb[w][t] = -1;
-    // order: the P x P tiles (first nt_p), then dY tiles; wave w gets tiles
-    // w and w + 4 so dY tiles (the tail) land in second slots first
-    for (int i = 0; i < nt; ++i) {
-      const int w = i % 4, t = i / 4;
-      G.ra[w][t] = (int8_t)ta[i];
-      G.cb[w][t] = (int8_t)tb[i];
-    }
-    // a wave with only a dY tile in slot 0 is fine (variant 1 tile, half)
-  }
-  p->ngroups = n;
-  return true;
-}
-
-template <class Op, class Epi>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-void symred3w_kernel(Op op, Epi epi, SymPlan2 plan, int I, int J, int K, int k_chunk) {
-  constexpr int BK = kX3Rows;
-  constexpr int NR = BK / 8;
-  __shared__ __attribute__((aligned(16))) char lds[2 * kX3Buf];
-
-  const int total = gridDim.x;
-  const int b = blockIdx.x;
-  const int xcd = b & 7, base8 = total >> 3, rem = total & 7;
-  const int l = xcd * base8 + min(xcd, rem) + (b >> 3);
-  const int ng = plan.ngroups;
-  const int bz = l / ng;
-  const SymGroup2& G = plan.g[l - bz * ng];
-  set_z(epi, bz);
-  const int kbeg = bz * k_chunk;
-  const int kend = min(K, kbeg + k_chunk);
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int c16 = tid & 31;
-  const int scol = c16 * 8;
-  const int sbase = G.base[scol >> 6];
-  const int jcol = sbase >= 0 ? sbase + (scol & 63) : J;
-  const typename Op::CB c0 = op.col_base(jcol), c1 = op.col_base(jcol + 4);
-  typename Op::St ra[NR][2];
-  float csum[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) csum[e] = 0.f;
-  typename Op::It it[NR];
-#pragma unroll
-  for (int rr = 0; rr < NR; ++rr) it[rr] = op.iter(kbeg + (tid >> 5) + 8 * rr);
-
-  auto fetch = [&](int k0) {
-#pragma unroll
-    for (int rr = 0; rr < NR; ++rr) {
-      const int k = k0 + (tid >> 5) + 8 * rr;
-      ra[rr][0] = op.stage_it(it[rr], c0, k < kend);
-      ra[rr][1] = op.stage_it(it[rr], c1, k < kend);
-      op.template advance<BK>(it[rr]);
-    }
-  };
-  auto commit = [&](int buf) {
-    char* s = lds + buf * kX3Buf;
-#pragma unroll
-    for (int rr = 0; rr < NR; ++rr) {
-      const int k = (tid >> 5) + 8 * rr;
-      const float4 x0 = finish(ra[rr][0]);
-      const float4 x1 = finish(ra[rr][1]);
-      csum[0] += x0.x;
-      csum[1] += x0.y;
-      csum[2] += x0.z;
-      csum[3] += x0.w;
-      csum[4] += x1.x;
-      csum[5] += x1.y;
-      csum[6] += x1.z;
-      csum[7] += x1.w;
-      uint4 h, m, lo;
-      split3(x0.x, x0.y, h.x, m.x, lo.x);
-      split3(x0.z, x0.w, h.y, m.y, lo.y);
-      split3(x1.x, x1.y, h.z, m.z, lo.z);
-      split3(x1.z, x1.w, h.w, m.w, lo.w);
-      const int off = k * kX3RowBytes + 16 * (c16 ^ (4 * (k & 3)));
-      *reinterpret_cast<uint4*>(s + off) = h;
-      *reinterpret_cast<uint4*>(s + kX3Part + off) = m;
-      *reinterpret_cast<uint4*>(s + 2 * kX3Part + off) = lo;
-    }
-  };
-
-  const int q = (lane >> 2) & 3, p = lane & 3, g = (lane >> 4) & 1, kh = lane >> 5;
-  auto slot_off = [&](int colblock) {
-    const int slot = (colblock >> 2) + 4 * g + p;
-    return (8 * kh + q) * kX3RowBytes + 8 * (slot ^ (8 * q));
-  };
-  int ib[2], jb[2], aoff[2][2], boff[2][2];
-  bool half[2];
-  const int ntile = (G.ra[wave][0] >= 0) + (G.ra[wave][1] >= 0);
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int sa = G.ra[wave][t] < 0 ? 0 : G.ra[wave][t];
-    const int sb = G.cb[wave][t] < 0 ? 0 : G.cb[wave][t];
-    ib[t] = G.base[sa];
-    jb[t] = G.base[sb];
-    half[t] = jb[t] + 32 >= J;
-    aoff[t][0] = slot_off(64 * sa);
-    aoff[t][1] = slot_off(64 * sa + 32);
-    boff[t][0] = slot_off(64 * sb);
-    boff[t][1] = slot_off(64 * sb + 32);
-  }
-
-  f32x16 acc[2][2][2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int y = 0; y < 2; ++y)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][x][y][r] = 0.f;
-
-  if (nk > 0) {
-    fetch(kbeg);
-    commit(0);
-  }
-  __syncthreads();
-
-  auto tile = [&](const char* s, int t, auto NTc) {
-    constexpr int NT = decltype(NTc)::value;
-    bf16x8 a[2][3], bb[2][3];
-#pragma unroll
-    for (int pt = 0; pt < 3; ++pt) {
-      const char* sp = s + pt * kX3Part;
-      a[0][pt] = cat8(ds_tr16(sp + aoff[t][0]), ds_tr16(sp + aoff[t][0] + 4 * kX3RowBytes));
-      a[1][pt] = cat8(ds_tr16(sp + aoff[t][1]), ds_tr16(sp + aoff[t][1] + 4 * kX3RowBytes));
-      bb[0][pt] = cat8(ds_tr16(sp + boff[t][0]), ds_tr16(sp + boff[t][0] + 4 * kX3RowBytes));
-      if constexpr (NT == 2)
-        bb[1][pt] = cat8(ds_tr16(sp + boff[t][1]), ds_tr16(sp + boff[t][1] + 4 * kX3RowBytes));
-    }
-#pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-      for (int tn = 0; tn < NT; ++tn) acc[t][tm][tn] = mfma_x3(a[tm], bb[tn], acc[t][tm][tn]);
-  };
-  // NTILE tiles, N0 / N1 column blocks in tile 0 / 1 (wave-uniform variants)
-  auto step = [&](int kt, int cur, auto NTILE, auto N0, auto N1) {
-    constexpr int nt = decltype(NTILE)::value;
-    fetch(kbeg + (kt + 1) * BK);
-    __builtin_amdgcn_sched_barrier(0);
-    const char* s = lds + cur * kX3Buf;
-    if constexpr (nt >= 1) tile(s, 0, N0);
-    if constexpr (nt >= 2) tile(s, 1, N1);
-    __builtin_amdgcn_sched_barrier(0);
-    commit(cur ^ 1);
-    __syncthreads();
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  auto run = [&](auto NTILE, auto N0, auto N1) {
-    for (int kt = 0; kt < nk; ++kt) step(kt, kt & 1, NTILE, N0, N1);
-  };
-  if (ntile == 0) run(I0{}, I2{}, I2{});
-  else if (ntile == 1) {
-    if (half[0]) run(I1{}, I1{}, I2{});
-    else run(I1{}, I2{}, I2{});
-  } else {
-    if (half[0]) run(I2{}, I1{}, I1{});  // both tiles are dY tiles
-    else if (half[1]) run(I2{}, I2{}, I1{});
-    else run(I2{}, I2{}, I2{});
-  }
-
-  float* cs = reinterpret_cast<float*>(lds);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) cs[(tid >> 5) * 256 + scol + e] = csum[e];
-  __syncthreads();
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    if (t >= ntile) break;
-    store_tile<2, 2>(epi, acc[t], ib[t], jb[t], lane, I, J);
-    if (ib[t] == 0) {  // the (0, b) sub-tile is unique: its wave writes column sums of slab b
-      const int col = 64 * G.cb[wave][t] + lane;
-      float v = 0.f;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) v += cs[r * 256 + col];
-      if (jb[t] + lane < J) epi.colsum(jb[t] + lane, v);
-    }
-  }
-}
-
-template <class Op, class Epi>
-inline void launch_symred3w(const Op& op, const Epi& e, const SymPlan2& plan, int I, int J, int K,
-                            int nchunk, int k_chunk, hipStream_t s) {
-  hipLaunchKernelGGL((symred3w_kernel<Op, Epi>), dim3(plan.ngroups * nchunk), dim3(256), 0, s, op, e,
-                     plan, I, J, K, k_chunk);
 }
 
 // ---------------------------------------------------------------------------
@@ -750,11 +433,22 @@ inline bool sym_plan6_greedy(int K, int cout_pad, SymPlan6* p) {
 // MFMA pipe idles through every commit.
 // The plan (by value) covers the upper triangle with groups; dense partials
 // [chunk][I+1][J] through store_tile.
-template <class Op, class Epi, bool PIPE = false>
+// F16: f16x2 split operands (f16x2.hpp, three MFMAs per product): the P columns
+// [0, kp) scaled by the power of two of the published bound pmax, the dY
+// columns by ymax's; parts h, l in the first two thirds of each LDS buffer; the
+// accumulators unscaled per column before the store (rows are P columns).
+template <class Op, class Epi, bool PIPE = false, bool F16 = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_chunk) {
+void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_chunk,
+                    const unsigned* pmax = nullptr, const unsigned* ymax = nullptr, int kp = 0) {
   constexpr int BK = kX3Rows;
+  constexpr int NP = F16 ? 2 : 3;
   __shared__ __attribute__((aligned(16))) char lds[2 * kSixBuf];
+  float sp = 1.f, sy = 1.f;
+  if constexpr (F16) {
+    sp = f16x2_scale_of_bits(pmax);
+    sy = f16x2_scale_of_bits(ymax);
+  }
 
   const int total = gridDim.x;
   const int b = blockIdx.x;
@@ -776,11 +470,13 @@ void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_ch
   const int srow = tid >> 5;
   const int scol = 12 * (tid & 31);
   typename Op::CB cbs[3];
+  float scu[3];  // F16: the scale of each staged run's columns
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
     const int c = scol + 4 * u;
     const int base = G.base[c >> 6];
     cbs[u] = op.col_base(base >= 0 ? base + (c & 63) : J);
+    scu[u] = base + (c & 63) < kp ? sp : sy;
   }
   typename Op::It it = op.iter(kbeg + srow);
   typename Op::St ra[PIPE ? 2 : 1][3];
@@ -807,12 +503,17 @@ void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_ch
       csum[4 * u + 2] += x.z;
       csum[4 * u + 3] += x.w;
       uint2 h, m, lo;
-      split3(x.x, x.y, h.x, m.x, lo.x);
-      split3(x.z, x.w, h.y, m.y, lo.y);
+      if constexpr (F16) {
+        split2(x.x, x.y, scu[u], h.x, m.x);
+        split2(x.z, x.w, scu[u], h.y, m.y);
+      } else {
+        split3(x.x, x.y, h.x, m.x, lo.x);
+        split3(x.z, x.w, h.y, m.y, lo.y);
+      }
       const int off = 8 * (((scol >> 2) + u) ^ q8);
       *reinterpret_cast<uint2*>(s + off) = h;
       *reinterpret_cast<uint2*>(s + kSixPart + off) = m;
-      *reinterpret_cast<uint2*>(s + 2 * kSixPart + off) = lo;
+      if constexpr (!F16) *reinterpret_cast<uint2*>(s + 2 * kSixPart + off) = lo;
     }
   };
 
@@ -860,7 +561,7 @@ void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_ch
     constexpr int NT = decltype(NTc)::value;
     bf16x8 a[2][3], bb[2][3];
 #pragma unroll
-    for (int pt = 0; pt < 3; ++pt) {
+    for (int pt = 0; pt < NP; ++pt) {
       const char* sp = s + pt * kSixPart;
       a[0][pt] = cat8(ds_tr16(sp + aoff[t][0]), ds_tr16(sp + aoff[t][0] + 4 * kSixRowBytes));
       a[1][pt] = cat8(ds_tr16(sp + aoff[t][1]), ds_tr16(sp + aoff[t][1] + 4 * kSixRowBytes));
@@ -871,7 +572,15 @@ void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_ch
 #pragma unroll
     for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
-      for (int tn = 0; tn < NT; ++tn) acc[t][tm][tn] = mfma_x3(a[tm], bb[tn], acc[t][tm][tn]);
+      for (int tn = 0; tn < NT; ++tn) {
+        if constexpr (F16) {
+          const f16x8 ah[2] = {__builtin_bit_cast(f16x8, a[tm][0]), __builtin_bit_cast(f16x8, a[tm][1])};
+          const f16x8 bh[2] = {__builtin_bit_cast(f16x8, bb[tn][0]), __builtin_bit_cast(f16x8, bb[tn][1])};
+          acc[t][tm][tn] = mfma_x2(ah, bh, acc[t][tm][tn]);
+        } else {
+          acc[t][tm][tn] = mfma_x3(a[tm], bb[tn], acc[t][tm][tn]);
+        }
+      }
   };
   // SN: register set holding tile kt+1 (PIPE) / receiving it (plain)
   auto step = [&](int kt, int cur, auto NTILE, auto N0, auto N1, auto SN) {
@@ -883,9 +592,9 @@ void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_ch
       if constexpr (nt >= 1) {
         tile(s, 0, N0);
         if (kt + 1 < nk) commit(cur ^ 1, SN);
-        constexpr int nm = 6 * 2 * decltype(N0)::value;
+        constexpr int nm = (F16 ? 3 : 6) * 2 * decltype(N0)::value;
         __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);             // the loads
-        __builtin_amdgcn_sched_group_barrier(0x100, 6 * (2 + decltype(N0)::value), 0);  // fragments
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * NP * (2 + decltype(N0)::value), 0);  // fragments
 #pragma unroll
         for (int i = 0; i < nm; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -939,6 +648,16 @@ void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_ch
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       if (t >= ntile) break;
+      if constexpr (F16) {  // unscale: rows are P columns (sp), column j by its own scale
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+          const float inv = 1.f / (sp * (jb[t] + 32 * tn + (lane & 31) < kp ? sp : sy));
+#pragma unroll
+          for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][tm][tn][r] *= inv;
+        }
+      }
       store_tile<2, 2>(epi, acc[t], ib[t], jb[t], lane, I, J);
       if (ib[t] == 0) {  // the (0, b) sub-tile is unique: its wave writes slab b's column sums
         const int col = 64 * G.cb[wave][t] + lane;
@@ -951,11 +670,18 @@ void symred6_kernel(Op op, Epi epi, SymPlan6 plan, int I, int J, int K, int k_ch
   }
 }
 
+// pmax / ymax (both or neither): the f16x2 form, P columns [0, kp) and dY
+// columns bounded by the published maxima
 template <class Op, class Epi>
 inline void launch_symred6(const Op& op, const Epi& e, const SymPlan6& plan, int I, int J, int K,
-                           int nchunk, int k_chunk, hipStream_t s) {
-  hipLaunchKernelGGL((symred6_kernel<Op, Epi, true>), dim3(plan.ngroups * nchunk), dim3(512), 0, s, op, e,
-                     plan, I, J, K, k_chunk);
+                           int nchunk, int k_chunk, hipStream_t s, const unsigned* pmax = nullptr,
+                           const unsigned* ymax = nullptr, int kp = 0) {
+  if (pmax && ymax)
+    hipLaunchKernelGGL((symred6_kernel<Op, Epi, true, true>), dim3(plan.ngroups * nchunk), dim3(512), 0, s, op,
+                       e, plan, I, J, K, k_chunk, pmax, ymax, kp);
+  else
+    hipLaunchKernelGGL((symred6_kernel<Op, Epi, true>), dim3(plan.ngroups * nchunk), dim3(512), 0, s, op, e,
+                       plan, I, J, K, k_chunk, nullptr, nullptr, 0);
 }
 
 // Six-slab groups (symred6_kernel, loads two K-tiles ahead) where sym_plan6 has
