@@ -238,8 +238,8 @@ def run(args):
     M = N * T
     rows = 81 * M
     lib = _lib.load()
-    x3 = acktr and lib.acmi_get_gemm_mode() == _lib.GEMM_X3
-    band = x3 and lib.acmi_get_conv_stats_mode() == _lib.CONV_STATS_BAND
+    x3 = lib.acmi_get_gemm_mode() == _lib.GEMM_X3
+    band = acktr and x3 and lib.acmi_get_conv_stats_mode() == _lib.CONV_STATS_BAND
     patch_flops = 2.0 * (513 * 514 / 2 + 513 * 64) * rows  # the patch-row sums it replaces
     if band:
         # pixel-pair band reduction (band.hpp): the needed 64x64 sub-tiles of
@@ -258,7 +258,8 @@ def run(args):
     else:
         kern_flops = 2.0 * 513 * 64 * rows
         exec_flops = 2.0 * 8 * 128 * 32 * rows
-        kern_name = 'conv2 wgrad reduction GEMM (f32 MFMA)'
+        kern_name = ('conv2 wgrad reduction GEMM (bf16x3 split-operand MFMA, f32-accurate)' if x3
+                     else 'conv2 wgrad reduction GEMM (f32 MFMA)')
     # MFMAs per f32-accurate product: 3 (f16x2, band), 6 (bf16x3), 1 (f32 MFMA)
     nmf = 3 if band else 6 if x3 else 1
     peak = F16X2_F32EQ_PEAK_TFLOPS if band else X3_F32EQ_PEAK_TFLOPS if x3 else FP32_MFMA_PEAK_TFLOPS
