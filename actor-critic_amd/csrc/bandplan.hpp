@@ -291,6 +291,18 @@ inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 3) 
     p.xcd_groups[x].push_back((int)i);
     acc += work(p.groups[i]);
   }
+  // within a region, the groups with the most sub-tiles first (spatial order among
+  // equals): the blocks an XCD runs side by side then advance through the chunk's
+  // rows at about the same pace, so the rows one of them pulls into L2 are still
+  // there when the others reach them (conv2 band 0.654 -> 0.602 ms per launch)
+  auto ntile = [&](int gi) {
+    int t = 0;
+    for (int w = 0; w < 8; ++w) t += (p.groups[gi].ra[w][0] >= 0) + (p.groups[gi].ra[w][1] >= 0);
+    return t;
+  };
+  for (int x = 0; x < 8; ++x)
+    std::stable_sort(p.xcd_groups[x].begin(), p.xcd_groups[x].end(),
+                     [&](int a, int b) { return ntile(a) > ntile(b); });
   // tile ids (group-major), column-sum owners (first group staging the slab)
   p.tile_of.assign((size_t)ns * ns, -1);
   std::vector<char> csdone(ns, 0);
