@@ -19,7 +19,7 @@
 #include <algorithm>
 
 #include "common.hpp"
-#include "symred3.hpp"  // split3, pk_bf16, ds_tr16, cat8, stage_f4 (fused conv1 wgrad)
+#include "symred3.hpp"  // split2, u8x8_to_f16, ds_tr16, cat8h, f16x2 scales (fused conv1 wgrad)
 
 namespace acmi {
 
@@ -204,236 +204,17 @@ __global__ __launch_bounds__(256) void conv1_afactor_i8_kernel(const uint8_t* ob
   if (diag && tid < 128) colsum[(long long)chunk * 256 + 128 * ta + tid] = csum;
 }
 
-// One block per chunk for the whole upper triangle (ACMI_GEMM_X3 mode; the
-// 3-block form above stages each row's patch bytes 4 times over its tile pairs
-// -- 512 bytes per row -- and is bound by that gather): 8 waves, all 256 patch
-// columns staged once per 64-row stage (256 bytes per row), 36 upper-triangle
-// 32x32 tiles dealt as rows (r, 7-r) to wave pairs, at most two distinct row
-// blocks per wave (kTri).  Same partial layout, so conv1_afactor_finalize is
-// shared.  40 KB of LDS, 5 x 16 accumulator registers.
-__constant__ int8_t kTri[8][5][2] = {
-    {{0, 0}, {0, 1}, {0, 2}, {0, 3}, {0, 4}}, {{0, 5}, {0, 6}, {0, 7}, {7, 7}, {-1, -1}},
-    {{1, 1}, {1, 2}, {1, 3}, {1, 4}, {1, 5}}, {{1, 6}, {1, 7}, {6, 6}, {6, 7}, {-1, -1}},
-    {{2, 2}, {2, 3}, {2, 4}, {2, 5}, {2, 6}}, {{2, 7}, {5, 5}, {5, 6}, {5, 7}, {-1, -1}},
-    {{3, 3}, {3, 4}, {3, 5}, {3, 6}, {3, 7}}, {{4, 4}, {4, 5}, {4, 6}, {4, 7}, {-1, -1}}};
-
-// WG: also the conv1 weight gradient [P;1]^T d1 from the same staged patch bytes
-// (fused with the A factor: the u8 patch gather is shared).  d1 rows are staged
-// next to them, split three ways into a [part][row][32] bf16 image (as
-// conv1_wgrad_x3_kernel's), the patch bytes enter the bf16 MFMAs exactly
-// (u = x ^ 0x80); wave w owns patch columns 32w..32w+31 x all 32 channels.
-// Per-chunk partials [chunk][257][32] (row 256: the bias gradient), reduced by
-// finalize_wgrad_kernel like the separate kernel's.  24 KB more LDS; two waves
-// per SIMD (one block per CU) for the extra registers.
-template <bool WG>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WG ? 2 : 4))) void conv1_afactor_i8_tri_kernel(const uint8_t* obs,
-                                                                   long long img_stride, int rows,
-                                                                   int chunk_rows, int* part,
-                                                                   int* colsum, const float* d1,
-                                                                   float* wpart) {
-  const int total = gridDim.x, b = blockIdx.x;
-  const int xcd = b & 7, base_l = total >> 3, rem = total & 7;
-  const int chunk = xcd * base_l + min(xcd, rem) + (b >> 3);
-  const int r_begin = chunk * chunk_rows;
-  const int r_end = min(rows, r_begin + chunk_rows);
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2][256 * AF_LINE];
-  constexpr int DRA = 64;              // d1 image row bytes: 32 channels x bf16
-  constexpr int DPART = AF_BK * DRA;   // 4 KB per split part
-  __shared__ __attribute__((aligned(16))) char dimg[WG ? 2 : 1][WG ? 3 * DPART : 16];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  // d1 staging (WG): 8 threads per row (one float4 each), 64 rows
-  const int drow = tid >> 3, dcol = (tid & 7) * 4;
-  StF4 rd = make_float4(0.f, 0.f, 0.f, 0.f);
-  double dsum[4] = {0.0, 0.0, 0.0, 0.0};  // bias gradient: ~8000 rows per thread column
-  // staging map: 4 rows (4*q4 .. +3) x 8 columns (8*cg .. +7) per thread, cg < 32
-  const int q4 = tid & 15;
-  const int cg = tid >> 4;
-  const int c = 8 * cg;
-  const int coff = (((c >> 5) * AF_OBS_W) + ((c & 31) >> 2)) * 4;  // (kh, kw0) of the 8 bytes
-
-  uint2 ra[4];
-  const uint8_t* x0 = reinterpret_cast<const uint8_t*>(kX0Run);
-  const uint32_t istride = (uint32_t)img_stride;
-  auto fetch = [&](int r0) {
-    const int r = r0 + 4 * q4;
-    const bool ok = r < r_end;
-    const uint32_t rr = ok ? (uint32_t)r : (uint32_t)r_begin;
-    const uint32_t img = rr / 400u;
-    const uint32_t p = rr - img * 400u;
-    const uint32_t oh = p / 20u;
-    const uint32_t ow = p - oh * 20u;
-    const uint32_t off = img * istride + (oh * 4 * AF_OBS_W + ow * 4) * 4;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      ra[q] = *reinterpret_cast<const uint2*>(ok ? obs + (off + (uint32_t)(coff + 16 * q)) : x0);
-    if constexpr (WG) {
-      const int k = r0 + drow;
-      const bool dok = k < r_end;
-      rd = stage_f4(d1 + (long long)(dok ? k : 0) * 32 + dcol, dok);
-    }
-  };
-  auto transpose4 = [](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t* out) {
-    const uint32_t p01l = __builtin_amdgcn_perm(w1, w0, 0x05010400u);
-    const uint32_t p01h = __builtin_amdgcn_perm(w1, w0, 0x07030602u);
-    const uint32_t p23l = __builtin_amdgcn_perm(w3, w2, 0x05010400u);
-    const uint32_t p23h = __builtin_amdgcn_perm(w3, w2, 0x07030602u);
-    out[0] = __builtin_amdgcn_perm(p23l, p01l, 0x05040100u);
-    out[1] = __builtin_amdgcn_perm(p23l, p01l, 0x07060302u);
-    out[2] = __builtin_amdgcn_perm(p23h, p01h, 0x05040100u);
-    out[3] = __builtin_amdgcn_perm(p23h, p01h, 0x07060302u);
-  };
-  auto commit = [&](int buf) {
-    constexpr uint32_t F = 0x80808080u;
-    uint32_t cols[8];
-    transpose4(ra[0].x ^ F, ra[1].x ^ F, ra[2].x ^ F, ra[3].x ^ F, cols);
-    transpose4(ra[0].y ^ F, ra[1].y ^ F, ra[2].y ^ F, ra[3].y ^ F, cols + 4);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      *reinterpret_cast<uint32_t*>(lds[buf] + (c + j) * AF_LINE + 4 * q4) = cols[j];
-    if constexpr (WG) {
-      dsum[0] += (double)rd.x;
-      dsum[1] += (double)rd.y;
-      dsum[2] += (double)rd.z;
-      dsum[3] += (double)rd.w;
-      uint2 h, m, l;
-      split3(rd.x, rd.y, h.x, m.x, l.x);
-      split3(rd.z, rd.w, h.y, m.y, l.y);
-      char* ds = dimg[buf] + drow * DRA + 2 * dcol;
-      *reinterpret_cast<uint2*>(ds) = h;
-      *reinterpret_cast<uint2*>(ds + DPART) = m;
-      *reinterpret_cast<uint2*>(ds + 2 * DPART) = l;
-    }
-  };
-
-  int ti[5], tj[5];
-  const int wu = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the table in SGPRs
-#pragma unroll
-  for (int t = 0; t < 5; ++t) {
-    ti[t] = kTri[wu][t][0];
-    tj[t] = kTri[wu][t][1];
-  }
-  const int ntile = tj[4] >= 0 ? 5 : 4;
-  const int row0 = ti[0];
-  int row1 = row0;  // the wave's other row block (if any)
-#pragma unroll
-  for (int t = 1; t < 5; ++t)
-    if (tj[t] >= 0 && ti[t] != row0) row1 = ti[t];
-
-  v16i acc[5];
-#pragma unroll
-  for (int t = 0; t < 5; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0;
-  int csum = 0;
-  f32x16 wacc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) wacc[r] = 0.f;
-  // d1 fragment offset in the [k][32] image (conv1_wgrad_x3_kernel's map)
-  const int daoff = (8 * (lane >> 5) + ((lane >> 2) & 3)) * DRA + 8 * (4 * ((lane >> 4) & 1) + (lane & 3));
-
-  const int nst = r_end > r_begin ? (r_end - r_begin + AF_BK - 1) / AF_BK : 0;
-  if (nst > 0) {
-    fetch(r_begin);
-    commit(0);
-  }
-  __syncthreads();
-  const int half = lane >> 5;
-  auto stage = [&](int st, auto NTc) {
-    constexpr int NT = decltype(NTc)::value;
-    const int cur = st & 1;
-    fetch(r_begin + (st + 1) * AF_BK);
-    __builtin_amdgcn_sched_barrier(0);
-    const uint8_t* S = lds[cur] + (lane & 31) * AF_LINE + 16 * half;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const v4i a0 = *reinterpret_cast<const v4i*>(S + row0 * 32 * AF_LINE + 32 * s);
-      const v4i a1 = *reinterpret_cast<const v4i*>(S + row1 * 32 * AF_LINE + 32 * s);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const v4i bb = *reinterpret_cast<const v4i*>(S + tj[t] * 32 * AF_LINE + 32 * s);
-        acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ti[t] == row0 ? a0 : a1, bb, acc[t], 0, 0, 0);
-      }
-    }
-    if constexpr (WG) {
-      // weight gradient: C^T[channel][patch column] over this stage's 64 rows
-      const char* dsb = dimg[cur];
-      const uint8_t* pc = lds[cur] + (32 * wave + (lane & 31)) * AF_LINE + 8 * (lane >> 5);
-#pragma unroll
-      for (int ks = 0; ks < AF_BK / 16; ++ks) {
-        bf16x8 a[3];
-#pragma unroll
-        for (int pt = 0; pt < 3; ++pt) {
-          const char* ap = dsb + pt * DPART + 16 * ks * DRA + daoff;
-          a[pt] = cat8(ds_tr16(ap), ds_tr16(ap + 4 * DRA));
-        }
-        const uint2 xb = *reinterpret_cast<const uint2*>(pc + 16 * ks);
-        const uint32_t u0 = xb.x ^ 0x80808080u, u1 = xb.y ^ 0x80808080u;  // back to u
-        const uint4 pb = make_uint4(pk_bf16((float)(u0 & 255u), (float)((u0 >> 8) & 255u)),
-                                    pk_bf16((float)((u0 >> 16) & 255u), (float)(u0 >> 24)),
-                                    pk_bf16((float)(u1 & 255u), (float)((u1 >> 8) & 255u)),
-                                    pk_bf16((float)((u1 >> 16) & 255u), (float)(u1 >> 24)));
-        const bf16x8 bb = __builtin_bit_cast(bf16x8, pb);
-        wacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bb, wacc, 0, 0, 0);
-        wacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb, wacc, 0, 0, 0);
-        wacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb, wacc, 0, 0, 0);
-      }
-    }
-    if (tid < 256) {  // column sums of x over the staged rows
-      const uint32_t* line = reinterpret_cast<const uint32_t*>(lds[cur] + tid * AF_LINE);
-#pragma unroll
-      for (int w = 0; w < AF_BK / 4; ++w) csum = __builtin_amdgcn_sdot4((int)line[w], 0x01010101, csum, false);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    commit(cur ^ 1);
-    __syncthreads();
-  };
-  if (ntile == 5)
-    for (int st = 0; st < nst; ++st) stage(st, std::integral_constant<int, 5>{});
-  else
-    for (int st = 0; st < nst; ++st) stage(st, std::integral_constant<int, 4>{});
-
-  int* out = part + (long long)chunk * 65536;
-#pragma unroll
-  for (int t = 0; t < 5; ++t) {
-    if (t >= ntile) break;
-    const int col = 32 * tj[t] + (lane & 31);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = 32 * ti[t] + (r & 3) + 8 * (r >> 2) + 4 * half;
-      out[row * 256 + col] = acc[t][r];
-    }
-  }
-  if (tid < 256) colsum[(long long)chunk * 256 + tid] = csum;
-  if constexpr (WG) {
-    // wacc[r]: channel (r&3) + 8(r>>2) + 4(lane>>5), patch column 32w + (lane&31)
-    float* wout = wpart + (long long)chunk * 257 * 32;
-    const int i = 32 * wave + (lane & 31);
-#pragma unroll
-    for (int gq = 0; gq < 4; ++gq)
-      *reinterpret_cast<float4*>(wout + i * 32 + 8 * gq + 4 * (lane >> 5)) =
-          make_float4(wacc[4 * gq], wacc[4 * gq + 1], wacc[4 * gq + 2], wacc[4 * gq + 3]);
-    // bias gradient (row 256): the 64 row-threads of each channel group through LDS
-    double* cs = reinterpret_cast<double*>(&lds[0][0]);  // free after the last stage's barrier
-#pragma unroll
-    for (int e = 0; e < 4; ++e) cs[drow * 32 + dcol + e] = dsum[e];
-    __syncthreads();
-    if (tid < 32) {
-      double t = 0.0;
-      for (int r = 0; r < AF_BK; ++r) t += cs[r * 32 + tid];
-      wout[256 * 32 + tid] = (float)t;
-    }
-  }
-}
-
-// Role-split form of the fused kernel (the default for A factor + weight
-// gradient; ACMI_AF_ROLES=0 selects the kernel above).  The form above deals the
-// 36 A-factor tiles and the 8 weight-gradient tiles to all 8 waves, so every
-// wave reads its row fragments, its B fragments and the whole split d1 operand
-// from LDS -- about 230 KB of LDS reads per 64-row stage, the column sums'
-// 80-byte-strided dword reads 8-way bank conflicted.  Here:
+// One block per chunk for the whole upper triangle AND the conv1 weight gradient
+// (ACMI_GEMM_X3 mode; the 3-block form above stages each row's patch bytes 4
+// times over its tile pairs -- 512 bytes per row -- and is bound by that
+// gather): all 256 patch columns staged once per 64-row stage (256 bytes per
+// row), d1 rows staged beside them, so the u8 gather is shared by the A factor
+// and the weight gradient [P;1]^T d1.  Same A partial layout, so
+// conv1_afactor_finalize is shared; weight-gradient partials [chunk][257][32]
+// (row 256: the bias gradient) reduced by finalize_wgrad_kernel.  Roles (an
+// earlier form dealt the 36 A-factor tiles and the 8 weight-gradient tiles to
+// all 8 waves, so every wave read the whole split d1 operand -- about 230 KB of
+// LDS reads per stage, the column sums 8-way bank conflicted):
 //  * waves 0-3 own the A factor on column-block quarters, 9 tiles each: wave 0
 //    the upper triangle of blocks 0-3 but (3,3) (from 4 fragments), wave 1 that
 //    of blocks 4-7 but (7,7), waves 2 / 3 blocks 0-3 x 4-5 / 6-7 plus (3,3) /
@@ -442,8 +223,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WG ? 2 : 4)
 //    one read of the split d1 operand serves two tiles, and the column sums
 //    (v_dot4 of the patch bytes they read anyway);
 //  * the gather runs two stages ahead (two register sets).
-// Integer partials are exact and each weight-gradient tile accumulates in the
-// same order as above: the results are identical bit for bit.
+// Weight-gradient arithmetic: f16x2 (f16x2.hpp) -- d1 scaled by the power of two
+// of max |d1| (published by conv2's input-gradient epilogue, d1max) and split
+// into f16 h, l at the commit; the patch bytes u enter as the f16 subnormals
+// u * 2^-24 (exact; tower.hpp u8x8_to_f16); two MFMAs per k16 and tile, the
+// partials unscaled by 2^24 / s when stored.  Integer A partials are exact.
 __device__ __forceinline__ void af_transpose4(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
                                               uint32_t* out) {
   const uint32_t p01l = __builtin_amdgcn_perm(w1, w0, 0x05010400u);
@@ -469,16 +253,17 @@ struct AfRegs {  // one stage's gather: 4 rows x 8 patch bytes, one float4 of d1
 
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void conv1_afactor_roles_kernel(
     const uint8_t* obs, long long img_stride, int rows, int chunk_rows, int* part, int* colsum,
-    const float* d1, float* wpart) {
+    const float* d1, float* wpart, const unsigned* d1max) {
   const int total = gridDim.x, b = blockIdx.x;
   const int xcd = b & 7, base_l = total >> 3, rem = total & 7;
   const int chunk = xcd * base_l + min(xcd, rem) + (b >> 3);
   const int r_begin = chunk * chunk_rows;
   const int r_end = min(rows, r_begin + chunk_rows);
   __shared__ __attribute__((aligned(16))) uint8_t lds[2][256 * AF_LINE];
-  constexpr int DRA = 64;             // d1 image row bytes: 32 channels x bf16
-  constexpr int DPART = AF_BK * DRA;  // 4 KB per split part
-  __shared__ __attribute__((aligned(16))) char dimg[2][3 * DPART];
+  constexpr int DRA = 64;             // d1 image row bytes: 32 channels x f16
+  constexpr int DPART = AF_BK * DRA;  // 4 KB per split part (h, l)
+  __shared__ __attribute__((aligned(16))) char dimg[2][2 * DPART];
+  const float sd = f16x2_scale_of_bits(d1max);  // (every lane: before the role branch)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -531,7 +316,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     fp = wrap ? fp - 400u : fp;
     fimg = wrap ? fimg + istride : fimg;
   };
-  double dsum[4] = {0.0, 0.0, 0.0, 0.0};  // bias gradient (as above)
+  double dsum[4] = {0.0, 0.0, 0.0, 0.0};  // bias gradient: ~8000 rows per thread column
   uint32_t sink = 0;
   auto commit = [&](const AfRegs& R, int buf) {
     if constexpr (AF_PROBE == 3 || AF_PROBE == 4) {
@@ -549,13 +334,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     dsum[1] += (double)R.d.y;
     dsum[2] += (double)R.d.z;
     dsum[3] += (double)R.d.w;
-    uint2 h, m, l;
-    split3(R.d.x, R.d.y, h.x, m.x, l.x);
-    split3(R.d.z, R.d.w, h.y, m.y, l.y);
+    uint2 h, l;
+    split2(R.d.x, R.d.y, sd, h.x, l.x);
+    split2(R.d.z, R.d.w, sd, h.y, l.y);
     char* ds = dimg[buf] + drow * DRA + 2 * dcol;
     *reinterpret_cast<uint2*>(ds) = h;
-    *reinterpret_cast<uint2*>(ds + DPART) = m;
-    *reinterpret_cast<uint2*>(ds + 2 * DPART) = l;
+    *reinterpret_cast<uint2*>(ds + DPART) = l;
   };
 
   const int fb = wave == 1 ? 4 : 0;  // tri roles: first of the 4 column blocks
@@ -625,19 +409,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
       } else {
         // weight gradient: C^T[channel][patch column] over this stage's 64 rows.
         // Software-pipelined: every LDS operand of the stage is read up front,
-        // and the u8 -> bf16 conversion of k-step ks + 1 (VALU) is interleaved
-        // with the six MFMAs of k-step ks (one wave issues both in order).
+        // and the u8 -> f16 conversion of k-step ks + 1 (VALU) is interleaved
+        // with the four MFMAs of k-step ks (one wave issues both in order).
         const char* dsb = dimg[cur];
         const uint8_t* pc = lds[cur] + (64 * (wave - 4) + (lane & 31)) * AF_LINE + 8 * half;
         constexpr int NK = AF_BK / 16;
-        bf16x8 a[NK][3];
+        f16x8 a[NK][2];
         uint2 xb[NK][2];
 #pragma unroll
         for (int ks = 0; ks < NK; ++ks) {
 #pragma unroll
-          for (int pt = 0; pt < 3; ++pt) {
+          for (int pt = 0; pt < 2; ++pt) {
             const char* ap = dsb + pt * DPART + 16 * ks * DRA + daoff;
-            a[ks][pt] = cat8(ds_tr16(ap), ds_tr16(ap + 4 * DRA));
+            a[ks][pt] = cat8h(ds_tr16(ap), ds_tr16(ap + 4 * DRA));
           }
 #pragma unroll
           for (int tt = 0; tt < 2; ++tt) xb[ks][tt] = *reinterpret_cast<const uint2*>(pc + tt * 32 * AF_LINE + 16 * ks);
@@ -645,33 +429,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         auto convert = [&](const uint2& x, int tt) {
           csum[tt] = __builtin_amdgcn_sdot4((int)x.x, 0x01010101, csum[tt], false);
           csum[tt] = __builtin_amdgcn_sdot4((int)x.y, 0x01010101, csum[tt], false);
-          const uint32_t u0 = x.x ^ 0x80808080u, u1 = x.y ^ 0x80808080u;  // back to u
-          const uint4 pb = make_uint4(pk_bf16((float)(u0 & 255u), (float)((u0 >> 8) & 255u)),
-                                      pk_bf16((float)((u0 >> 16) & 255u), (float)(u0 >> 24)),
-                                      pk_bf16((float)(u1 & 255u), (float)((u1 >> 8) & 255u)),
-                                      pk_bf16((float)((u1 >> 16) & 255u), (float)(u1 >> 24)));
-          return __builtin_bit_cast(bf16x8, pb);
+          return u8x8_to_f16(make_uint2(x.x ^ 0x80808080u, x.y ^ 0x80808080u));  // back to u
         };
         f32x16 w0 = __builtin_bit_cast(f32x16, acc[0]);
         f32x16 w1 = __builtin_bit_cast(f32x16, acc[1]);
-        bf16x8 b0 = convert(xb[0][0], 0), b1 = convert(xb[0][1], 1);
+        f16x8 b0 = convert(xb[0][0], 0), b1 = convert(xb[0][1], 1);
 #pragma unroll
         for (int ks = 0; ks < NK; ++ks) {
-          bf16x8 n0 = b0, n1 = b1;
+          f16x8 n0 = b0, n1 = b1;
           if (ks + 1 < NK) {
             n0 = convert(xb[ks + 1][0], 0);
             n1 = convert(xb[ks + 1][1], 1);
           }
 #pragma unroll
-          for (int pt = 2; pt >= 0; --pt) {  // l, m, h: the order of the kernel above
-            w0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][pt], b0, w0, 0, 0, 0);
-            w1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks][pt], b1, w1, 0, 0, 0);
+          for (int pt = 1; pt >= 0; --pt) {  // l, then h
+            w0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][pt], b0, w0, 0, 0, 0);
+            w1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[ks][pt], b1, w1, 0, 0, 0);
           }
           if (ks + 1 < NK)
 #pragma unroll
-            for (int i = 0; i < 6; ++i) {  // one MFMA, then a share of the next conversion
+            for (int i = 0; i < 4; ++i) {  // one MFMA, then a share of the next conversion
               __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-              __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
             }
           b0 = n0;
           b1 = n1;
@@ -727,11 +506,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         const int v = csum[tt] + __shfl_xor(csum[tt], 32);
         if (half == 0) colsum[(long long)chunk * 256 + 64 * (wave - 4) + 32 * tt + lane] = v;
       }
-      // acc[tt][r]: channel (r&3) + 8(r>>2) + 4(lane>>5), patch column i
+      // acc[tt][r]: channel (r&3) + 8(r>>2) + 4(lane>>5), patch column i;
+      // unscaled: the subnormal pixels' 2^-24 and d1's scale (exact)
       float* wout = wpart + (long long)chunk * 257 * 32;
+      const float unscale = 16777216.0f / sd;
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
-        const f32x16 w = __builtin_bit_cast(f32x16, acc[tt]);
+        const f32x16 w = __builtin_bit_cast(f32x16, acc[tt]) * unscale;
         const int i = 64 * (wave - 4) + 32 * tt + (lane & 31);
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq)
@@ -758,12 +539,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     for (int r = 0; r < AF_BK; ++r) t += cs[r * 32 + tid];
     wpart[(long long)chunk * 257 * 32 + 256 * 32 + tid] = (float)t;
   }
-}
-
-// read per call (tests switch it in-process; one getenv per 400 us launch)
-static int af_roles() {
-  const char* e = getenv("ACMI_AF_ROLES");
-  return e ? atoi(e) : 1;
 }
 
 // chunks for the one-block-per-chunk kernel: 2 blocks per CU resident
@@ -850,10 +625,11 @@ int conv1_afactor_fused_chunks(long long rows) {
 }
 
 int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* astat, int* ws,
-                     long long ws_ints, hipStream_t s, const float* d1, float** wpart_out) {
+                     long long ws_ints, hipStream_t s, const float* d1, float** wpart_out, const unsigned* d1max) {
   const long long rows = 400LL * B;
   const bool tri = g_gemm_mode == ACMI_GEMM_X3;
-  ACMI_REQUIRE(!d1 || tri, ACMI_ERR_ARG, "fused conv1 weight gradient needs the bf16x3 mode");
+  ACMI_REQUIRE(tri == (d1 != nullptr) && (!d1 || d1max), ACMI_ERR_ARG,
+               "conv1 A factor: the x3 mode fuses the weight gradient (d1 and its published max needed)");
   int nchunk, chunk;
   if (tri)
     af_plan_tri(rows, &nchunk, &chunk);
@@ -871,18 +647,13 @@ int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* ast
   // fused weight-gradient partials after the int64 sums (16-byte aligned)
   float* wpart = reinterpret_cast<float*>(((uintptr_t)(sums + 65536 + 256) + 15) & ~(uintptr_t)15);
   if (wpart_out) *wpart_out = d1 ? wpart : nullptr;
-  // the role-split kernel's buffer offsets: frames and d1 within 2^32 bytes
-  const bool roles = af_roles() && (long long)B * img_stride <= (1LL << 32) - 64 && rows * 128 < (1LL << 32);
-  if (tri && d1 && roles)
+  if (tri) {
+    // buffer-resource offsets: frames and d1 within 2^32 bytes (152K frames)
+    ACMI_REQUIRE((long long)B * img_stride <= (1LL << 32) - 64 && rows * 128 < (1LL << 32), ACMI_ERR_ARG,
+                 "conv1 A factor: batch too large for 32-bit buffer offsets (B=%d)", B);
     hipLaunchKernelGGL(conv1_afactor_roles_kernel, dim3(nchunk), dim3(512), 0, s, obs, img_stride,
-                       (int)rows, chunk, part, colsum, d1, wpart);
-  else if (tri && d1)
-    hipLaunchKernelGGL(conv1_afactor_i8_tri_kernel<true>, dim3(nchunk), dim3(512), 0, s, obs, img_stride,
-                       (int)rows, chunk, part, colsum, d1, wpart);
-  else if (tri)
-    hipLaunchKernelGGL(conv1_afactor_i8_tri_kernel<false>, dim3(nchunk), dim3(512), 0, s, obs,
-                       img_stride, (int)rows, chunk, part, colsum, nullptr, nullptr);
-  else
+                       (int)rows, chunk, part, colsum, d1, wpart, d1max);
+  } else
     hipLaunchKernelGGL(conv1_afactor_i8_kernel, dim3(3 * nchunk), dim3(256), 0, s, obs, img_stride,
                        (int)rows, chunk, part, colsum);
   hipLaunchKernelGGL(conv1_afactor_reduce, dim3(65536 / 64 + 4), dim3(256), 0, s, part, colsum, nchunk,

@@ -147,7 +147,7 @@ inline void band_chunks(long long rows, int ngroups, int* nc, int* ch) {
 // published maxima (kAmaxSlots words each, common.hpp)
 enum {
   kBsMaxA1 = 0 * kAmaxWords, kBsMaxA2 = 1 * kAmaxWords, kBsMaxD2 = 2 * kAmaxWords, kBsMaxD3 = 3 * kAmaxWords,
-  kBsMaxW3 = 4 * kAmaxWords, kBsMaxD4 = 5 * kAmaxWords, kBsMaxW4 = 6 * kAmaxWords
+  kBsMaxW3 = 4 * kAmaxWords, kBsMaxD4 = 5 * kAmaxWords, kBsMaxW4 = 6 * kAmaxWords, kBsMaxD1 = 7 * kAmaxWords
 };
 constexpr int kBandScratch = 8 * kAmaxWords;
 

@@ -133,8 +133,8 @@ long long conv1_afactor_ws_ints(long long rows);
 // [chunk][257][32] are computed in the same pass (*wpart_out, in ws;
 // conv1_afactor_fused_chunks chunks)
 int conv1_afactor_u8(const uint8_t* obs, long long img_stride, int B, float* astat, int* ws,
-                     long long ws_ints, hipStream_t s, const float* d1 = nullptr,
-                     float** wpart_out = nullptr);
+                     long long ws_ints, hipStream_t s, const float* d1, float** wpart_out,
+                     const unsigned* d1max);
 int conv1_afactor_fused_chunks(long long rows);
 
 }  // namespace acmi

@@ -79,7 +79,8 @@ __global__ void convt2_prep_kernel(const float* w2, char* out) {
 template <bool GRAM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* __restrict__ a1,
-                   float* __restrict__ d1, int B, float* __restrict__ gpart, const unsigned* d2max) {
+                   float* __restrict__ d1, int B, float* __restrict__ gpart, const unsigned* d2max,
+                   unsigned* d1max) {
   // 16 KB ring; the epilogue's transpose scratch (4 x 32 x 36 floats) reuses it
   __shared__ __attribute__((aligned(16))) char lds[std::max(2 * CT2::STEP_BYTES, 4 * 32 * 36 * 4)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -203,7 +204,7 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
     if constexpr (!GRAM) {
       // ReLU'-masked d1 through the LDS transpose: each store instruction writes
       // 8 whole 128-byte pixel rows (gemm.hpp store_tile_lds, EpiConvT addressing)
-      store_tile_lds<4, 1>(EpiConvT<20, 20, 2, 32>{d1, a1}, reinterpret_cast<const f32x16(&)[4][1]>(acc), 0,
+      store_tile_lds<4, 1>(EpiConvT<20, 20, 2, 32>{d1, a1, d1max}, reinterpret_cast<const f32x16(&)[4][1]>(acc), 0,
                            tile * CT2::TILE + 32 * wave, lane, scr, 4 * CT2::CIN, J);
     } else {
 #pragma unroll

@@ -63,6 +63,15 @@ __device__ __forceinline__ f16x8 cat8h(s16x4 a, s16x4 b) {
 }
 __device__ __forceinline__ f16x8 as_f16x8(const uint4& u) { return __builtin_bit_cast(f16x8, u); }
 
+// eight u8 pixels n as the f16 SUBNORMALS n * 2^-24 (exact; one byte permute per
+// two: the byte is the significand, the exponent field zero) -- the products'
+// 2^-24 is taken out with the other operand's scale when they are stored
+__device__ __forceinline__ f16x8 u8x8_to_f16(uint2 u) {
+  const uint32_t w0 = __builtin_amdgcn_perm(0u, u.x, 0x0c010c00u), w1 = __builtin_amdgcn_perm(0u, u.x, 0x0c030c02u);
+  const uint32_t w2 = __builtin_amdgcn_perm(0u, u.y, 0x0c010c00u), w3 = __builtin_amdgcn_perm(0u, u.y, 0x0c030c02u);
+  return __builtin_bit_cast(f16x8, make_uint4(w0, w1, w2, w3));
+}
+
 // three-product f16x2 step on one accumulator: a = {h, l}, b = {h, l}
 __device__ __forceinline__ f32x16 mfma_x2(const f16x8 (&a)[2], const f16x8 (&b)[2], f32x16 c) {
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], c, 0, 0, 0);

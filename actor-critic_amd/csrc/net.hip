@@ -1048,7 +1048,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     using W = ConvTWeights<4, 4, 2, 32, 64>;
     W opA{P + L.off[2]};
     RowsAsK<Src> opB{Src{bw->d2, B * Src::L}};
-    EpiConvT<20, 20, 2, 32> epi{bw->d1, a->a1};
+    EpiConvT<20, 20, 2, 32> epi{bw->d1, a->a1, dxs + kBsMaxD1};  // max |d1|: conv1's f16x2 weight gradient
     prof_begin(ACMI_PROF_CONV2_DX, s);
     const char* p2 = prep ? prep + TowerPrep<C3>::BYTES : nullptr;
     if (p2 && g_gemm_mode == ACMI_GEMM_X3) {
@@ -1056,11 +1056,11 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
       // chain reduces d1 to its Gram partials instead of storing it
       if (gram_part) {
         hipLaunchKernelGGL(convt2_kernel<true>, dim3(convt2_gram_blocks(B)), dim3(256), 0, s, p2, bw->d2,
-                           a->a1, nullptr, B, gram_part, dxs + kBsMaxD2);
+                           a->a1, nullptr, B, gram_part, dxs + kBsMaxD2, nullptr);
         if (gram_done) *gram_done = true;
       } else {
         hipLaunchKernelGGL(convt2_kernel<false>, dim3(cdiv(B * CT2::L, CT2::TILE)), dim3(256), 0, s, p2,
-                           bw->d2, a->a1, bw->d1, B, nullptr, dxs + kBsMaxD2);
+                           bw->d2, a->a1, bw->d1, B, nullptr, dxs + kBsMaxD2, dxs + kBsMaxD1);
       }
     } else
       launch_mm<128, 128, 16, 2, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
@@ -1099,7 +1099,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
     float* wpart = nullptr;
     const int rc0 = conv1_afactor_u8(obs, img_stride, B, astat + L.stat_off[0],
                                      reinterpret_cast<int*>(ws + pcap), afactor_ws_floats(B), s,
-                                     fuse_c1 ? bw->d1 : nullptr, &wpart);
+                                     fuse_c1 ? bw->d1 : nullptr, &wpart, bscr + kBsMaxD1);
     prof_end(ACMI_PROF_CONV1_AFACTOR, s);
     if (rc0) return rc0;
     if (fuse_c1) {  // the conv1 weight gradient came with the A factor: reduce its chunks

@@ -16,12 +16,13 @@
 // Arithmetic: f16x2 split operands (f16x2.hpp), each tensor scaled by a power of
 // two from a bound the prepare step computes (tower_stats_kernel): the weights'
 // max |W|, and the a1 / a2 bounds of band.hpp (ReLU outputs of [0,1] pixels
-// under the positive weight mass).  conv1: u8 pixels exact in f16, two MFMAs per
-// k16 against the weights' h/l (bf16x3 took three); conv2 / conv3: the a1 / a2
-// fragments split h/l from LDS, three MFMAs per product (bf16x3: six); the
-// accumulators unscaled in the epilogue's bias fma -- f32-accurate.  The a1 / a2
-// LDS images use convfwd3.hpp's 16-byte chunk swizzle by pixel x, so the lanes
-// of a fragment read (consecutive output columns) hit distinct banks.
+// under the positive weight mass).  conv1: u8 pixels exact as f16 subnormals
+// (one byte permute per two), two MFMAs per k16 against the weights' h/l (bf16x3
+// took three); conv2 / conv3: the a1 / a2 images in LDS hold the activations
+// already split (h, l written once by the producing epilogue, tow_put), three
+// MFMAs per product (bf16x3: six); the accumulators unscaled in the epilogue's
+// bias fma -- f32-accurate.  The LDS images use convfwd3.hpp's 16-byte chunk
+// swizzle by pixel x, so the lanes of a fragment read hit distinct banks.
 // Work per block: conv1 three row tiles per wave + the 13th by K halves on two
 // waves (roles rotated by block parity: equal per-SIMD load); conv2 the 3x2
 // tiles as one full tile + half the K of row tile 2 per wave (the halves summed
@@ -42,24 +43,32 @@ constexpr int kTowScr = 16 * 32 * 4;       // conv1's 13th row tile, second K ha
 static_assert(2 * (kTowLds + kTowScr) <= 160 * 1024, "two blocks per CU");
 static_assert(81 * 64 * 4 + 2 * 17 * 32 * 4 <= kTowObs, "a2 + conv2 scratch fit the image region");
 
-// byte offset of 16-byte channel chunk `ch` of pixel p (x = its column) in an
-// f32 [pixel][C] LDS image read with stride S (convfwd3.hpp chunk_pos)
+// The a1 / a2 LDS images hold each activation already split (h, l f16 parts of
+// the scaled value, written once by the producing layer's epilogue) instead of
+// the f32 value split again by every wave that reads it (a1 pixels feed up to 4
+// conv2 taps x 4 waves, a2 pixels up to 9 conv3 taps): per pixel [part][C] f16
+// = C * 4 bytes, the 16-byte chunk c (8 channels of one part; c < C/8: h, else
+// l) at chunk position c ^ (x / S) % (C/4) -- the fragment reads of one
+// instruction (consecutive output columns, pixel x stepping by S) land on
+// distinct chunk positions (convfwd3.hpp chunk_pos).
 template <int C, int S>
-__device__ __forceinline__ int tow_pos(int p, int x, int ch) {
-  return p * C * 4 + 16 * (ch ^ ((x / S) & (C / 4 - 1)));
+__device__ __forceinline__ int tow_pos(int p, int x, int c) {
+  return p * C * 4 + 16 * (c ^ ((x / S) & (C / 4 - 1)));
+}
+// byte offset of channel ch's part (0: h, 1: l) of pixel p
+template <int C, int S>
+__device__ __forceinline__ int tow_elem(int p, int x, int ch, int part) {
+  return tow_pos<C, S>(p, x, part * (C / 8) + (ch >> 3)) + 2 * (ch & 7);
+}
+// the split of v (scaled by s) into the image
+template <int C, int S>
+__device__ __forceinline__ void tow_put(char* img, int p, int x, int ch, float v, float s) {
+  const _Float16 h = (_Float16)(v * s);
+  const _Float16 l = (_Float16)fmaf(v, s, -(float)h);
+  *reinterpret_cast<_Float16*>(img + tow_elem<C, S>(p, x, ch, 0)) = h;
+  *reinterpret_cast<_Float16*>(img + tow_elem<C, S>(p, x, ch, 1)) = l;
 }
 
-// eight u8 pixels as f16 (exact)
-__device__ __forceinline__ f16x8 u8x8_to_f16(uint2 u) {
-  uint32_t w[4];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const uint32_t x = h ? u.y : u.x;
-    w[2 * h] = pk_f16((float)(x & 255u), (float)((x >> 8) & 255u));
-    w[2 * h + 1] = pk_f16((float)((x >> 16) & 255u), (float)(x >> 24));
-  }
-  return __builtin_bit_cast(f16x8, make_uint4(w[0], w[1], w[2], w[3]));
-}
 
 // Prepared weights (acmi_conv_prepare): conv1/conv2/conv3 weights split once
 // per parameter version into the f16 h/l parts of every lane's B fragment,
@@ -265,11 +274,11 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
         acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[0], acc[u], 0, 0, 0);
       }
     }
-    const float bias = b1[col], inv1 = 1.0f / sw1;
+    const float bias = b1[col], inv1 = 16777216.0f / sw1;  // 2^24 (subnormal pixels) / scale: exact
     float* g = a1g + img * st * 12800;
     auto emit1 = [&](int p, float v) {
       v = fmaxf(__builtin_fmaf(v * inv1, 1.0f / 255.0f, bias), 0.f);
-      *reinterpret_cast<float*>(a1L + tow_pos<32, 2>(p, p % 20, col >> 2) + 4 * (col & 3)) = v;
+      tow_put<32, 2>(a1L, p, p % 20, col, v, sa1);
       g[p * 32 + col] = v;
     };
 #pragma unroll
@@ -315,15 +324,14 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
       f16x8 b[2];
       bw.get(s & 1, b);
       const int tap = s >> 1, kh = tap >> 2, kw = tap & 3;
-      const int ch = 4 * (s & 1) + 2 * kh8;
+      const int c8 = 2 * (s & 1) + kh8;  // the 8 channels of this k-step and lane half
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         if (u == 1 && (s < hk0 || s >= hk0 + 16)) continue;
         const int p = pin[u] + kh * 20 + kw, x = px[u] + kw;
-        const float4 x0 = *reinterpret_cast<const float4*>(a1L + tow_pos<32, 2>(p, x, ch));
-        const float4 x1 = *reinterpret_cast<const float4*>(a1L + tow_pos<32, 2>(p, x, ch + 1));
         f16x8 a[2];
-        split2x8(x0, x1, sa1, a[0], a[1]);
+        a[0] = *reinterpret_cast<const f16x8*>(a1L + tow_pos<32, 2>(p, x, c8));
+        if constexpr (!H16) a[1] = *reinterpret_cast<const f16x8*>(a1L + tow_pos<32, 2>(p, x, 4 + c8));
         if constexpr (H16) {
           if (u == 0) accF = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], accF, 0, 0, 0);
           else accH = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], accH, 0, 0, 0);
@@ -348,7 +356,7 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
     float* g = a2g + img * st * 5184;
     auto emit = [&](int p, float v) {
       v = fmaxf(__builtin_fmaf(v, inv2, bias), 0.f);
-      *reinterpret_cast<float*>(imgL + tow_pos<64, 1>(p, p % 9, c >> 2) + 4 * (c & 3)) = v;
+      tow_put<64, 1>(imgL, p, p % 9, c, v, sa2);
       g[p * 64 + c] = v;
     };
 #pragma unroll
@@ -388,12 +396,11 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
         f16x8 b[2];
         bw.get(h, b);
         const int tap = ss >> 2, kh = tap / 3, kw = tap - kh * 3;
-        const int ch = 4 * (ss & 3) + 2 * kh8;
+        const int c8 = 2 * (ss & 3) + kh8;
         const int p = pin + kh * 9 + kw, x = ow + kw;
-        const float4 x0 = *reinterpret_cast<const float4*>(imgL + tow_pos<64, 1>(p, x, ch));
-        const float4 x1 = *reinterpret_cast<const float4*>(imgL + tow_pos<64, 1>(p, x, ch + 1));
         f16x8 a[2];
-        split2x8(x0, x1, sa2, a[0], a[1]);
+        a[0] = *reinterpret_cast<const f16x8*>(imgL + tow_pos<64, 1>(p, x, c8));
+        if constexpr (!H16) a[1] = *reinterpret_cast<const f16x8*>(imgL + tow_pos<64, 1>(p, x, 8 + c8));
         if constexpr (H16) {
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], acc, 0, 0, 0);
           continue;

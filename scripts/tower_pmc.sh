@@ -3,7 +3,6 @@
 root="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$root"
 timeout -k 10 60 python scripts/kbench.py forward 512 || exit $?
-ACMI_TOWER=0 timeout -k 10 60 python scripts/kbench.py forward 512 || exit $?
-PASSES="sq lds" bash scripts/pmc.sh pmc_tower scripts/kbench.py forward 512 || exit $?
+PASSES="${PASSES:-sq lds}" bash scripts/pmc.sh pmc_tower scripts/kbench.py forward 512 || exit $?
 python3 scripts/pmc_table.py gpurun_out/pmc_tower > gpurun_out/pmc_tower/table.txt 2>&1
 exit 0
