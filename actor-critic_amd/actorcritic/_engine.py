@@ -93,6 +93,11 @@ class Activations(object):
         self.a4 = z(B, 512)
         self.logits = z(B, layout.A)
         self.value = z(B)
+        # ReLU' bit masks (acmi_acts_t m1..m3): one uint32 per 32 channels of a pixel
+        zi = lambda *s: torch.zeros(*s, dtype=torch.int32, device=device)
+        self.m1 = zi(B, 400)
+        self.m2 = zi(B, 81 * 2)
+        self.m3 = zi(B, 49 * (layout.C3 // 32))
         self.ws = None
         self.struct = self.view(0, 1)
 
@@ -107,7 +112,7 @@ class Activations(object):
             self.ws = torch.zeros(max(need, 1), dtype=torch.float32, device=self.a1.device)
         return _lib.Acts(el(self.a1, 400 * 32), el(self.a2, 81 * 64), el(self.a3, self.a3[0].numel()),
                          el(self.a4, 512), el(self.logits, A), el(self.value, 1), A, self.ws.data_ptr(),
-                         self.ws.numel())
+                         self.ws.numel(), el(self.m1, 400), el(self.m2, 162), el(self.m3, self.m3.shape[1]))
 
 
 class UpdateState(object):

@@ -32,7 +32,7 @@ class Net(ctypes.Structure):
 class Acts(ctypes.Structure):
     _fields_ = [('a1', c_vp), ('a2', c_vp), ('a3', c_vp), ('a4', c_vp),
                 ('logits', c_vp), ('value', c_vp), ('ld_logits', c_int),
-                ('ws', c_vp), ('ws_floats', c_i64)]
+                ('ws', c_vp), ('ws_floats', c_i64), ('m1', c_vp), ('m2', c_vp), ('m3', c_vp)]
 
 
 class Bwd(ctypes.Structure):

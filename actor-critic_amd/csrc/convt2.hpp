@@ -76,7 +76,8 @@ __global__ void convt2_prep_kernel(const float* w2, char* out) {
   d[64] = l;
 }
 
-template <bool GRAM>
+// MASK: a1 is the ReLU' bit words (acmi_acts_t m1) instead of the f32 activation
+template <bool GRAM, bool MASK = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* __restrict__ a1,
                    float* __restrict__ d1, int B, float* __restrict__ gpart, const unsigned* d2max,
@@ -204,7 +205,7 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
     if constexpr (!GRAM) {
       // ReLU'-masked d1 through the LDS transpose: each store instruction writes
       // 8 whole 128-byte pixel rows (gemm.hpp store_tile_lds, EpiConvT addressing)
-      store_tile_lds<4, 1>(EpiConvT<20, 20, 2, 32>{d1, a1, d1max}, reinterpret_cast<const f32x16(&)[4][1]>(acc), 0,
+      store_tile_lds<4, 1>(EpiConvT<20, 20, 2, 32, MASK>{d1, a1, d1max}, reinterpret_cast<const f32x16(&)[4][1]>(acc), 0,
                            tile * CT2::TILE + 32 * wave, lane, scr, 4 * CT2::CIN, J);
     } else {
 #pragma unroll
@@ -215,7 +216,13 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int ci = 8 * g + 4 * hl;
-          const float4 x = *reinterpret_cast<const float4*>(jok ? a1 + pix * CT2::CIN + ci : zero);
+          float4 x;
+          if constexpr (MASK) {  // ReLU' bits: word pix, channels ci .. ci + 3 (zero run past the end)
+            const uint32_t b = *reinterpret_cast<const uint32_t*>(jok ? a1 + pix : zero) >> ci;
+            x = make_float4((float)(b & 1u), (float)((b >> 1) & 1u), (float)((b >> 2) & 1u), (float)((b >> 3) & 1u));
+          } else {
+            x = *reinterpret_cast<const float4*>(jok ? a1 + pix * CT2::CIN + ci : zero);
+          }
           const int c = lane & 31;
           scr[(ci + 0) * 36 + c] = x.x > 0.f ? acc[p][4 * g + 0] : 0.f;
           scr[(ci + 1) * 36 + c] = x.y > 0.f ? acc[p][4 * g + 1] : 0.f;

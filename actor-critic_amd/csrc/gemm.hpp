@@ -565,12 +565,21 @@ struct EpiBiasAct {
 };
 
 // out = v * (act > 0)   (ReLU derivative from the stored post-ReLU output)
+// MASK: the activation's ReLU' bits (acmi_acts_t m1..m3: bit e of word e / 32 =
+// act[e] > 0) read instead of the f32 activation -- 1/32 of its bytes.  A
+// compile-time choice: a runtime one put the epilogue's loads under a branch
+// (fc4 dX 91 -> 119 us).
+template <bool MASK = false>
 struct EpiReluGrad {
   float* out;
-  const float* act;
+  const float* act;  // MASK: the uint32 bit words
   long long ld;
   unsigned* amax = nullptr;  // nullable: max |out| (has_amax)
-  __device__ __forceinline__ float aux(int i, int j) const { return act[(long long)i * ld + j]; }
+  __device__ __forceinline__ float aux(int i, int j) const {
+    const long long e = (long long)i * ld + j;
+    if constexpr (MASK) return (float)((reinterpret_cast<const uint32_t*>(act)[e >> 5] >> (e & 31)) & 1u);
+    else return act[e];
+  }
   __device__ __forceinline__ float store(int i, int j, float v, float x) const {
     const float o = x > 0.f ? v : 0.f;
     out[(long long)i * ld + j] = o;
@@ -583,13 +592,13 @@ struct EpiReluGrad {
 // NHWC pixel (S*ih'+ph, S*iw'+pw), channel ci; masked by ReLU'.  Four
 // consecutive rows are four consecutive channels of one pixel (VEC4), written
 // after the LDS transpose (LDS_T) as whole 128-byte channel runs.
-template <int IH, int IW, int S, int CIN>
+template <int IH, int IW, int S, int CIN, bool MASK = false>
 struct EpiConvT {
   static constexpr bool VEC4 = true;
   static constexpr bool LDS_T = true;
   static_assert(CIN % 4 == 0, "channel runs of 4");
   float* out;
-  const float* act;
+  const float* act;  // MASK: its ReLU' bit words (EpiReluGrad)
   unsigned* amax = nullptr;  // nullable: max |out| (has_amax)
   __device__ __forceinline__ long long offset(int i, int j) const {
     constexpr int PH = IH / S, PW = IW / S, L = PH * PW;
@@ -604,7 +613,14 @@ struct EpiConvT {
     return (((long long)img * IH + (S * ihp + ph)) * IW + (S * iwp + pw)) * CIN + ci;
   }
   __device__ __forceinline__ float4 aux4(int i0, int j) const {
-    return *reinterpret_cast<const float4*>(act + offset(i0, j));
+    const long long e = offset(i0, j);
+    if constexpr (MASK) {  // 4 consecutive channels: 4 bits of one word (CIN % 32 == 0)
+      static_assert(CIN % 32 == 0, "mask words of 32 channels");
+      const uint32_t b = reinterpret_cast<const uint32_t*>(act)[e >> 5] >> (e & 31);
+      return make_float4((float)(b & 1u), (float)((b >> 1) & 1u), (float)((b >> 2) & 1u), (float)((b >> 3) & 1u));
+    } else {
+      return *reinterpret_cast<const float4*>(act + e);
+    }
   }
   __device__ __forceinline__ float4 store4(int i0, int j, float4 v, float4 x) const {
     float4 o;

@@ -184,6 +184,27 @@ __global__ __launch_bounds__(256) void heads_dx4_kernel(const float* dhead, int 
   if (amax) block_amax256(amax, ok ? absmax4f(r) : 0.f);
 }
 
+// acmi_acts_t's masks: all three or none
+static bool masks_ok(const acmi_acts_t* a) { return (a->m1 && a->m2 && a->m3) || (!a->m1 && !a->m2 && !a->m3); }
+
+// ReLU' bit masks from the f32 activations, for the per-layer forward (the tower
+// writes them itself): word k of image b (wpi words per image, one per 32
+// channels) = bits (act > 0) of its 32 floats; images st apart in both buffers
+__global__ void act_mask_kernel(const float* act, int B, int wpi, long long st, uint32_t* mask) {
+  const long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= (long long)B * wpi) return;
+  const long long b = w / wpi, k = w - b * wpi;
+  const float4* src = reinterpret_cast<const float4*>(act + (b * st * wpi + k) * 32);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 v = src[q];
+    bits |= (uint32_t)(v.x > 0.f) << (4 * q) | (uint32_t)(v.y > 0.f) << (4 * q + 1) |
+            (uint32_t)(v.z > 0.f) << (4 * q + 2) | (uint32_t)(v.w > 0.f) << (4 * q + 3);
+  }
+  mask[b * st * wpi + k] = bits;
+}
+
 // conv/fc epilogue with an image remap so the rollout can write step t of an
 // env-major [N][T][rows] activation buffer in place.
 struct EpiAct {
@@ -398,7 +419,7 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     // the three convs fused per image (16-byte image loads)
     prof_begin(ACMI_PROF_CONV1_FWD, s);
     launch_tower<C3>(obs, img_stride, B, P, L.off, a->a1, a->a2, a->a3, st, prep, s,
-                     g_forward_mode == ACMI_FWD_BF16);
+                     g_forward_mode == ACMI_FWD_BF16, a->m1, a->m2, a->m3);
     prof_end(ACMI_PROF_CONV1_FWD, s);
   } else {
   {  // conv1: [B,84,84,4]u8 -> [B,20,20,32]; the u8 patches stay bytes in LDS
@@ -432,6 +453,12 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
       launch_gemm<128, 32, 32, 1, 1, false, false>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
     else
       launch_mm<128, 64, 32, 2, 1, false, false, 16>(opA, opB, epi, B * 49, C3, 576, 1, 0, s);
+  }
+  if (a->m1) {  // the ReLU' masks the tower would have written
+    hipLaunchKernelGGL(act_mask_kernel, dim3(cdiv((long long)B * 400, 256)), dim3(256), 0, s, a->a1, B, 400, st, a->m1);
+    hipLaunchKernelGGL(act_mask_kernel, dim3(cdiv((long long)B * 162, 256)), dim3(256), 0, s, a->a2, B, 162, st, a->m2);
+    hipLaunchKernelGGL(act_mask_kernel, dim3(cdiv((long long)B * 49 * C3 / 32, 256)), dim3(256), 0, s, a->a3, B,
+                       49 * C3 / 32, st, a->m3);
   }
   }  // per-layer convs
   // fc4: [B,49*C3] -> [B,512]
@@ -1020,13 +1047,17 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     const int K3 = 49 * C3;
     RowsAsK<DenseRows> opA{DenseRows{bw->d4, 512, B, 512}};
     MatTK<true> opB{P + L.off[6], 512, 512, K3};
-    EpiReluGrad epi{bw->d3, a->a3, K3, dxs + kBsMaxD3};
     // f16x2 on 128 x 64 tiles, BK = 32 (per launch at M = 10240: 89.8 us; 64 x 128
     // 107, 128 x 128 96.6, 64 x 128 / BK 32 97.1, 256 x 128 127.7; bf16x3 64 x 128 132)
-    if (g_gemm_mode == ACMI_GEMM_X3)
-      launch_gemm3_f16<128, 64, 32, 2, 1>(opA, opB, epi, B, K3, 512, dxs + kBsMaxD4, w4max, s);
-    else
-      launch_mm<64, 128, 32, 1, 2, false, false, 16>(opA, opB, epi, B, K3, 512, 1, 0, s);
+    auto run = [&](auto epi) {
+      if (g_gemm_mode == ACMI_GEMM_X3)
+        launch_gemm3_f16<128, 64, 32, 2, 1>(opA, opB, epi, B, K3, 512, dxs + kBsMaxD4, w4max, s);
+      else
+        launch_mm<64, 128, 32, 1, 2, false, false, 16>(opA, opB, epi, B, K3, 512, 1, 0, s);
+    };
+    // ReLU'(a3) from the mask bits when the forward wrote them
+    if (a->m3) run(EpiReluGrad<true>{bw->d3, reinterpret_cast<const float*>(a->m3), K3, dxs + kBsMaxD3});
+    else run(EpiReluGrad<false>{bw->d3, a->a3, K3, dxs + kBsMaxD3});
   }
   // conv input gradients as transposed products: rows = (phase, channel) of
   // the weights, columns = (super-)pixels gathering dY (EpiConvT, float4 rows)
@@ -1035,12 +1066,15 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     using W = ConvTWeights<3, 3, 1, 64, C3>;
     W opA{P + L.off[4]};
     RowsAsK<Src> opB{Src{bw->d3, B * Src::L}};
-    EpiConvT<9, 9, 1, 64> epi{bw->d2, a->a2, dxs + kBsMaxD2};
-    if (g_gemm_mode == ACMI_GEMM_X3)
-      // f16x2 operands: the scales of max |W3| and of max |d3| (the fc4 dX epilogue's)
-      launch_convt_x3<9, 9, 3, 3, 1, 64, C3, 256>(P + L.off[4], bw->d3, B, epi, w3max, dxs + kBsMaxD3, s);
-    else
-      launch_mm<64, 128, 16, 1, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
+    auto run = [&](auto epi) {
+      if (g_gemm_mode == ACMI_GEMM_X3)
+        // f16x2 operands: the scales of max |W3| and of max |d3| (the fc4 dX epilogue's)
+        launch_convt_x3<9, 9, 3, 3, 1, 64, C3, 256>(P + L.off[4], bw->d3, B, epi, w3max, dxs + kBsMaxD3, s);
+      else
+        launch_mm<64, 128, 16, 1, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
+    };
+    if (a->m2) run(EpiConvT<9, 9, 1, 64, true>{bw->d2, reinterpret_cast<const float*>(a->m2), dxs + kBsMaxD2});
+    else run(EpiConvT<9, 9, 1, 64>{bw->d2, a->a2, dxs + kBsMaxD2});
   }
   {  // conv2 -> d1 (stride 2: the four phases of a 2x2 super-pixel are the
      // 4 x 32 rows of one product over the 10x10 super-pixels)
@@ -1048,22 +1082,39 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     using W = ConvTWeights<4, 4, 2, 32, 64>;
     W opA{P + L.off[2]};
     RowsAsK<Src> opB{Src{bw->d2, B * Src::L}};
-    EpiConvT<20, 20, 2, 32> epi{bw->d1, a->a1, dxs + kBsMaxD1};  // max |d1|: conv1's f16x2 weight gradient
+    // (max |d1|: conv1's f16x2 weight gradient; ReLU'(a1) from the mask bits when written)
+    const float* act1 = a->m1 ? reinterpret_cast<const float*>(a->m1) : a->a1;
     prof_begin(ACMI_PROF_CONV2_DX, s);
     const char* p2 = prep ? prep + TowerPrep<C3>::BYTES : nullptr;
     if (p2 && g_gemm_mode == ACMI_GEMM_X3) {
       // pre-split weights, four phases per wave (convt2.hpp); the sampled-loss
       // chain reduces d1 to its Gram partials instead of storing it
+      auto go = [&](auto GRAMc, auto MASKc) {
+        constexpr bool GR = decltype(GRAMc)::value, MK = decltype(MASKc)::value;
+        if (GR)
+          hipLaunchKernelGGL((convt2_kernel<GR, MK>), dim3(convt2_gram_blocks(B)), dim3(256), 0, s, p2, bw->d2,
+                             act1, nullptr, B, gram_part, dxs + kBsMaxD2, nullptr);
+        else
+          hipLaunchKernelGGL((convt2_kernel<GR, MK>), dim3(cdiv(B * CT2::L, CT2::TILE)), dim3(256), 0, s, p2,
+                             bw->d2, act1, bw->d1, B, nullptr, dxs + kBsMaxD2, dxs + kBsMaxD1);
+      };
+      using T = std::true_type;
+      using F = std::false_type;
       if (gram_part) {
-        hipLaunchKernelGGL(convt2_kernel<true>, dim3(convt2_gram_blocks(B)), dim3(256), 0, s, p2, bw->d2,
-                           a->a1, nullptr, B, gram_part, dxs + kBsMaxD2, nullptr);
+        if (a->m1) go(T{}, T{});
+        else go(T{}, F{});
         if (gram_done) *gram_done = true;
       } else {
-        hipLaunchKernelGGL(convt2_kernel<false>, dim3(cdiv(B * CT2::L, CT2::TILE)), dim3(256), 0, s, p2,
-                           bw->d2, a->a1, bw->d1, B, nullptr, dxs + kBsMaxD2, dxs + kBsMaxD1);
+        if (a->m1) go(F{}, T{});
+        else go(F{}, F{});
       }
-    } else
-      launch_mm<128, 128, 16, 2, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
+    } else if (a->m1) {
+      launch_mm<128, 128, 16, 2, 2, false, false, 16>(
+          opA, opB, EpiConvT<20, 20, 2, 32, true>{bw->d1, act1, dxs + kBsMaxD1}, W::N, B * Src::L, Src::COLS, 1, 0, s);
+    } else {
+      launch_mm<128, 128, 16, 2, 2, false, false, 16>(opA, opB, EpiConvT<20, 20, 2, 32>{bw->d1, act1, dxs + kBsMaxD1},
+                                                      W::N, B * Src::L, Src::COLS, 1, 0, s);
+    }
     prof_end(ACMI_PROF_CONV2_DX, s);
   }
   ACMI_LAUNCH_CHECK("dx_chain");
@@ -1331,6 +1382,7 @@ static int forward_dispatch(const acmi_net_t* net, const uint8_t* obs, int64_t i
   ACMI_REQUIRE(acts->a1 && acts->a2 && acts->a3 && acts->a4 && acts->logits &&
                    acts->ld_logits >= net->num_actions && (!want_value || acts->value),
                ACMI_ERR_ARG, "acmi_forward: bad activation buffers");
+  ACMI_REQUIRE(masks_ok(acts), ACMI_ERR_ARG, "acmi_forward: ReLU masks m1..m3 must be all set or all NULL");
   ACMI_REQUIRE(act_stride >= 1, ACMI_ERR_ARG, "bad activation stride");
   ACMI_REQUIRE(spans32(B, img_stride, 84 * 84 * 4) && spans32(B, act_stride * 400 * 32, 400 * 32),
                ACMI_ERR_ARG, "acmi_forward: batch spans >= 2^31 elements (B=%d)", B);
@@ -1427,6 +1479,7 @@ int acmi_backward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride,
   Layout L;
   ACMI_REQUIRE(net && acts && bwd && grads && ws && obs, ACMI_ERR_ARG,
                "acmi_backward: null argument");
+  ACMI_REQUIRE(masks_ok(acts), ACMI_ERR_ARG, "acmi_backward: ReLU masks m1..m3 must be all set or all NULL");
   ACMI_REQUIRE(make_layout(net->num_actions, net->conv3_filters, &L), ACMI_ERR_ARG,
                "acmi_backward: bad net");
   ACMI_REQUIRE(B > 0 && img_stride >= 84 * 84 * 4 && img_stride % 4 == 0, ACMI_ERR_ARG,
@@ -1459,6 +1512,7 @@ int acmi_kfac_output_stats(const acmi_net_t* net, int B, const acmi_acts_t* acts
                "acmi_kfac_output_stats: null argument");
   ACMI_REQUIRE(make_layout(net->num_actions, net->conv3_filters, &L), ACMI_ERR_ARG, "bad net");
   ACMI_REQUIRE(B > 0 && spans32(B, 400 * 32, 400 * 32), ACMI_ERR_ARG, "bad B");
+  ACMI_REQUIRE(masks_ok(acts), ACMI_ERR_ARG, "acmi_kfac_output_stats: ReLU masks m1..m3 must be all set or all NULL");
   const long long cap = acmi_backward_ws_floats(B, net->num_actions, net->conv3_filters);
   hipStream_t s = (hipStream_t)stream;
   if (L.C3 == 32)

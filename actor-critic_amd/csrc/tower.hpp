@@ -190,12 +190,17 @@ __global__ void tower_prep_kernel(const float* w1, const float* w2, const float*
 // row of the 32x32 C/D fragment element r of `lane`
 __device__ __forceinline__ int tow_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
-// a layer's B fragments from the prepared weights, two k-steps in flight (slot =
-// k-step parity, always a compile-time index); H16: the h part only
+// a layer's B fragments from the prepared weights, kTowDepth k-steps ahead of
+// the one computed (slot = k-step mod kTowDepth + 1, a compile-time index in the
+// unrolled loops); H16: the h part only
+#ifndef ACMI_TOW_DEPTH
+#define ACMI_TOW_DEPTH 2
+#endif
+constexpr int kTowDepth = ACMI_TOW_DEPTH, kTowSlots = kTowDepth + 1;
 template <int N, bool H16 = false>
 struct TowB {
   const char* prep;
-  uint4 q[2][2];
+  uint4 q[kTowSlots][2];
   __device__ __forceinline__ void fetch(int s, int ct, int lane, int slot) {
     const uint4* p = reinterpret_cast<const uint4*>(prep + ((long long)(s * (N / 32) + ct) * 2) * 1024) + lane;
     q[slot][0] = p[0];
@@ -213,7 +218,8 @@ struct TowB {
 template <int C3, bool H16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, const float* b2,
-                  const float* b3, float* a1g, float* a2g, float* a3g, long long st, const char* prep) {
+                  const float* b3, float* a1g, float* a2g, float* a3g, long long st, const char* prep,
+                  uint32_t* m1g, uint32_t* m2g, uint32_t* m3g) {
   using P = TowerPrep<C3>;
   const unsigned* hdr = reinterpret_cast<const unsigned*>(prep + P::HDR);
   const float sw1 = f16x2_scale_of_bits(hdr + kTowMaxW1), sw2 = f16x2_scale_of_bits(hdr + kTowMaxW2);
@@ -258,13 +264,14 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
     TowB<32, H16> bw{prep + P::O1};
-    bw.fetch(0, 0, lane, 0);
+#pragma unroll
+    for (int i = 0; i < kTowDepth; ++i) bw.fetch(i, 0, lane, i);
     __syncthreads();
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      if (s + 1 < 16) bw.fetch(s + 1, 0, lane, (s + 1) & 1);
+      if (s + kTowDepth < 16) bw.fetch(s + kTowDepth, 0, lane, (s + kTowDepth) % kTowSlots);
       f16x8 b[2];
-      bw.get(s & 1, b);
+      bw.get(s % kTowSlots, b);
       const int koff = (s >> 1) * 336 + 16 * (s & 1);  // kernel row kh = s/2, kw half
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -276,10 +283,15 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
     }
     const float bias = b1[col], inv1 = 16777216.0f / sw1;  // 2^24 (subnormal pixels) / scale: exact
     float* g = a1g + img * st * 12800;
+    uint32_t* mg = m1g ? m1g + img * st * 400 : nullptr;
+    // (the callers' active lanes are whole 32-lane halves: lanes 0 / 32 write the
+    // ReLU' word of their half's pixel)
     auto emit1 = [&](int p, float v) {
       v = fmaxf(__builtin_fmaf(v * inv1, 1.0f / 255.0f, bias), 0.f);
       tow_put<32, 2>(a1L, p, p % 20, col, v, sa1);
       g[p * 32 + col] = v;
+      const unsigned long long bal = __ballot(v > 0.f);
+      if (mg && col == 0) mg[p] = (uint32_t)(bal >> (lane & 32));
     };
 #pragma unroll
     for (int u = 0; u < 3; ++u)
@@ -317,12 +329,13 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
 #pragma unroll
     for (int r = 0; r < 16; ++r) accF[r] = accH[r] = 0.f;
     TowB<64, H16> bw{prep + P::O2};
-    bw.fetch(0, ct, lane, 0);
+#pragma unroll
+    for (int i = 0; i < kTowDepth; ++i) bw.fetch(i, ct, lane, i);
 #pragma unroll
     for (int s = 0; s < 32; ++s) {
-      if (s + 1 < 32) bw.fetch(s + 1, ct, lane, (s + 1) & 1);
+      if (s + kTowDepth < 32) bw.fetch(s + kTowDepth, ct, lane, (s + kTowDepth) % kTowSlots);
       f16x8 b[2];
-      bw.get(s & 1, b);
+      bw.get(s % kTowSlots, b);
       const int tap = s >> 1, kh = tap >> 2, kw = tap & 3;
       const int c8 = 2 * (s & 1) + kh8;  // the 8 channels of this k-step and lane half
 #pragma unroll
@@ -354,10 +367,13 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
     const int c = 32 * ct + col;
     const float bias = b2[c], inv2 = 1.0f / (sa1 * sw2);  // exact: powers of two
     float* g = a2g + img * st * 5184;
+    uint32_t* mg = m2g ? m2g + img * st * 162 : nullptr;
     auto emit = [&](int p, float v) {
       v = fmaxf(__builtin_fmaf(v, inv2, bias), 0.f);
       tow_put<64, 1>(imgL, p, p % 9, c, v, sa2);
       g[p * 64 + c] = v;
+      const unsigned long long bal = __ballot(v > 0.f);
+      if (mg && col == 0) mg[2 * p + ct] = (uint32_t)(bal >> (lane & 32));
     };
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -379,7 +395,7 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
     constexpr int NS = 36;  // k16 steps (576 / 16)
     const int rt = wave & 1;
     const int ct = C3 == 64 ? (wave >> 1) : 0;
-    const int s0 = C3 == 64 ? 0 : 18 * (wave >> 1), s1 = C3 == 64 ? NS : s0 + 18;
+    const int s0 = C3 == 64 ? 0 : 18 * (wave >> 1);
     const int p0 = min(32 * rt + col, 48);
     const int oh = p0 / 7, ow = p0 - oh * 7;
     const int pin = oh * 9 + ow;
@@ -387,30 +403,37 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     TowB<C3, H16> bw{prep + P::O3};
-    bw.fetch(s0, ct, lane, 0);
-    for (int s = s0; s < s1; s += 2) {
+    constexpr int NW = C3 == 64 ? NS : NS / 2;  // k-steps per wave: [s0, s0 + NW)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int ss = s + h;
-        if (ss + 1 < s1) bw.fetch(ss + 1, ct, lane, h ^ 1);
-        f16x8 b[2];
-        bw.get(h, b);
-        const int tap = ss >> 2, kh = tap / 3, kw = tap - kh * 3;
-        const int c8 = 2 * (ss & 3) + kh8;
-        const int p = pin + kh * 9 + kw, x = ow + kw;
-        f16x8 a[2];
-        a[0] = *reinterpret_cast<const f16x8*>(imgL + tow_pos<64, 1>(p, x, c8));
-        if constexpr (!H16) a[1] = *reinterpret_cast<const f16x8*>(imgL + tow_pos<64, 1>(p, x, 8 + c8));
-        if constexpr (H16) {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], acc, 0, 0, 0);
-          continue;
-        }
-        acc = mfma_x2(a, b, acc);
+    for (int i = 0; i < kTowDepth; ++i) bw.fetch(s0 + i, ct, lane, i);
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+      const int ss = s0 + i;
+      if (i + kTowDepth < NW) bw.fetch(ss + kTowDepth, ct, lane, (i + kTowDepth) % kTowSlots);
+      f16x8 b[2];
+      bw.get(i % kTowSlots, b);
+      const int tap = ss >> 2, kh = tap / 3, kw = tap - kh * 3;
+      const int c8 = 2 * (ss & 3) + kh8;
+      const int p = pin + kh * 9 + kw, x = ow + kw;
+      f16x8 a[2];
+      a[0] = *reinterpret_cast<const f16x8*>(imgL + tow_pos<64, 1>(p, x, c8));
+      if constexpr (!H16) a[1] = *reinterpret_cast<const f16x8*>(imgL + tow_pos<64, 1>(p, x, 8 + c8));
+      if constexpr (H16) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], acc, 0, 0, 0);
+        continue;
       }
+      acc = mfma_x2(a, b, acc);
     }
     const int c = 32 * ct + col;
     const float bias = b3[c], inv3 = 1.0f / (sa2 * sw3);
     float* g = a3g + img * st * (49 * C3);
+    uint32_t* mg = m3g ? m3g + img * st * (49 * C3 / 32) : nullptr;
+    auto emit3 = [&](int p, float v) {  // (active lanes: whole 32-lane halves)
+      v = fmaxf(__builtin_fmaf(v, inv3, bias), 0.f);
+      g[p * C3 + c] = v;
+      const unsigned long long bal = __ballot(v > 0.f);
+      if (mg && col == 0) mg[p * (C3 / 32) + ct] = (uint32_t)(bal >> (lane & 32));
+    };
     if constexpr (C3 == 32) {  // the second K half (waves 2, 3) through LDS to the first
       float* scr = reinterpret_cast<float*>(a1L);  // [rt][32 rows][32]
       if (wave >= 2) {
@@ -422,16 +445,14 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int p = 32 * rt + tow_row(r, lane);
-          if (p < 49)
-            g[p * C3 + c] = fmaxf(__builtin_fmaf(acc[r] + scr[(rt * 32 + tow_row(r, lane)) * 32 + col], inv3,
-                                                 bias), 0.f);
+          if (p < 49) emit3(p, acc[r] + scr[(rt * 32 + tow_row(r, lane)) * 32 + col]);
         }
       }
     } else {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int p = 32 * rt + tow_row(r, lane);
-        if (p < 49) g[p * C3 + c] = fmaxf(__builtin_fmaf(acc[r], inv3, bias), 0.f);
+        if (p < 49) emit3(p, acc[r]);
       }
     }
   }
@@ -441,14 +462,14 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
 template <int C3>
 inline void launch_tower(const uint8_t* obs, long long img_stride, int B, const float* P,
                          const long long* off, float* a1, float* a2, float* a3, long long st,
-                         const void* prep, hipStream_t s, bool h16 = false) {
+                         const void* prep, hipStream_t s, bool h16, uint32_t* m1, uint32_t* m2, uint32_t* m3) {
   const char* pp = static_cast<const char*>(prep);
   if (h16)
     hipLaunchKernelGGL((tower_kernel<C3, true>), dim3(B), dim3(256), 0, s, obs, img_stride, P + off[1],
-                       P + off[3], P + off[5], a1, a2, a3, st, pp);
+                       P + off[3], P + off[5], a1, a2, a3, st, pp, m1, m2, m3);
   else
     hipLaunchKernelGGL((tower_kernel<C3, false>), dim3(B), dim3(256), 0, s, obs, img_stride, P + off[1],
-                       P + off[3], P + off[5], a1, a2, a3, st, pp);
+                       P + off[3], P + off[5], a1, a2, a3, st, pp, m1, m2, m3);
 }
 
 // the header must be zero before the stats kernel's atomicMax (memset by the caller)

@@ -157,6 +157,15 @@ typedef struct acmi_acts {
   int ld_logits;
   float* ws;     /* optional split-K workspace (NULL: no split), floats:  */
   int64_t ws_floats; /* >= acmi_forward_ws_floats(B) enables it            */
+  /* optional ReLU' bit masks of a1..a3 (all three or none; NULL: none): bit e
+   * of word e / 32 = (a[e] > 0), i.e. one word per 32 channels of a pixel --
+   * m1 [B][400], m2 [B][81][2], m3 [B][49][C3/32] uint32.  acmi_forward writes
+   * them beside the activations (same image stride); acmi_backward and
+   * acmi_kfac_output_stats then mask the input gradients from them instead of
+   * re-reading the f32 activations (1/32 of the bytes; results bit-identical). */
+  uint32_t* m1;
+  uint32_t* m2;
+  uint32_t* m3;
 } acmi_acts_t;
 
 int64_t acmi_forward_ws_floats(int B);

@@ -134,6 +134,9 @@ def test_update_statistics_at_bench_shard_match_float64(lib, cuda):
     z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=cuda)
     t = dict(a1=z(B, 20, 20, 32), a2=z(B, 9, 9, 64), a3=z(B, 7, 7, C3), a4=z(B, 512), logits=z(B, A), value=z(B))
     acts = _lib.Acts(*[t[k].data_ptr() for k in ('a1', 'a2', 'a3', 'a4', 'logits', 'value')], A)
+    zi = lambda *s: torch.zeros(*s, dtype=torch.int32, device=cuda)  # the production path's ReLU' masks
+    t.update(m1=zi(B, 400), m2=zi(B, 162), m3=zi(B, 49 * C3 // 32))
+    acts.m1, acts.m2, acts.m3 = t['m1'].data_ptr(), t['m2'].data_ptr(), t['m3'].data_ptr()
     prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
     net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr())
     st = _lib.stream_handle()

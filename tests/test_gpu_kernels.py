@@ -65,12 +65,68 @@ def rand_params(A, C3, device, seed=0, scale=1.0):
     return p.to(device)
 
 
-def alloc_acts(B, A, C3, device):
+def alloc_acts(B, A, C3, device, masks=False):
     z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=device)
     t = dict(a1=z(B, 20, 20, 32), a2=z(B, 9, 9, 64), a3=z(B, 7, 7, C3), a4=z(B, 512), logits=z(B, A),
              value=z(B))
     acts = _lib.Acts(*[t[k].data_ptr() for k in ('a1', 'a2', 'a3', 'a4', 'logits', 'value')], A)
+    if masks:  # ReLU' bit masks (acmi_acts_t m1..m3)
+        zi = lambda *s: torch.zeros(*s, dtype=torch.int32, device=device)
+        t.update(m1=zi(B, 400), m2=zi(B, 162), m3=zi(B, 49 * C3 // 32))
+        acts.m1, acts.m2, acts.m3 = t['m1'].data_ptr(), t['m2'].data_ptr(), t['m3'].data_ptr()
     return t, acts
+
+
+def _relu_bits(a, words):
+    """uint32 words of (a > 0), bit e of word e // 32, as int32 [B, words]."""
+    b = (a.reshape(a.shape[0], words, 32) > 0).long()
+    v = (b << torch.arange(32, device=a.device)).sum(-1)
+    return torch.where(v >= 2 ** 31, v - 2 ** 32, v).int()
+
+
+@pytest.mark.parametrize('use_prep', [True, False], ids=['tower', 'per-layer'])
+def test_relu_masks_written_and_bit_identical(lib, cuda, use_prep):
+    """The ReLU' bit masks (acmi_acts_t m1..m3) written by the forward -- the fused
+    tower's ballots or the per-layer path's act_mask_kernel -- equal (a > 0) bit for
+    bit, and the backward and output statistics that mask their input gradients
+    from them instead of re-reading a1..a3 are bit-identical to the mask-free run."""
+    A, C3, B = 4, 32, 300
+    params = rand_params(A, C3, cuda, seed=41)
+    g = torch.Generator().manual_seed(42)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
+    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
+    net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr() if use_prep else None)
+    if use_prep:
+        _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), _lib.stream_handle())
+    ldh = 8
+    dhead = torch.zeros(B, ldh)
+    dhead[:, :A + 1] = torch.randn(B, A + 1, generator=g) / B
+    dhead = dhead.to(cuda)
+    z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=cuda)
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, None, None, so, ctypes.byref(tot))
+    ws = z(lib.acmi_backward_ws_floats(B, A, C3))
+    out = {}
+    for masks in (False, True):
+        t, acts = alloc_acts(B, A, C3, cuda, masks=masks)
+        _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+                  _lib.stream_handle())
+        d = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
+        bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
+        grads, astat, gstat = z(params.numel()), z(tot.value), z(tot.value)
+        _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
+                  ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), _lib.stream_handle())
+        d1 = d[0].clone()
+        _lib.call('acmi_kfac_output_stats', ctypes.byref(net), B, ctypes.byref(acts), ctypes.byref(bwd),
+                  7, 0, 3, _lib.ptr(gstat), _lib.ptr(ws), _lib.stream_handle())
+        torch.cuda.synchronize()
+        if masks:
+            for k, words in (('1', 400), ('2', 162), ('3', 49 * C3 // 32)):
+                assert torch.equal(t['m' + k], _relu_bits(t['a' + k], words)), k
+        out[masks] = (grads.cpu(), astat.cpu(), gstat.cpu(), d1.cpu())
+    for a, b in zip(out[False], out[True]):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize('M,N,K', [(128, 128, 32), (300, 260, 200), (1, 4, 4), (1000, 64, 1568)])
