@@ -99,12 +99,12 @@ def forward(B=512, reps=50):
 
 def band_scaling(sizes=(1024, 2048, 4096, 10240)):
     """conv2 band kernel time vs images: against its MFMA-bound time (sum over
-    groups of the busiest SIMD's sub-tiles x 4 x 6 MFMAs of 32 cycles per 16
+    groups of the busiest SIMD's sub-tiles x 4 x 3 f16x2 MFMAs of 32 cycles per 16
     image rows, over 256 CUs at 2.4 GHz) -- memory effects show as a growing ratio"""
     for M in sizes:
         info = (ctypes.c_int64 * 5)()
         _lib.call('acmi_band_info', 1, 32, M, info)
-        bound_ms = info[4] * 4 * 6 * 32 * (M / 16.0) / 256 / 2.4e9 * 1e3
+        bound_ms = info[4] * 4 * 3 * 32 * (M / 16.0) / 256 / 2.4e9 * 1e3
         _lib.call('acmi_prof_enable', 2, 64)
         backward(M, True, 2, reps=6)
         print('   M={} plan {} -> MFMA-bound {:.3f} ms'.format(M, list(info), bound_ms))
