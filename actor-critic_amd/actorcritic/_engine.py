@@ -287,28 +287,56 @@ class NetEngine(object):
             parallel.allreduce_sum_(st.red[:k])
             st.loss_reduced = True
 
+    def _packed(self, st):
+        """[grads | losses | A stats | G stats] with the (symmetric) factor statistics
+        as upper triangles (acmi_kfac_pack): what a K-FAC update all-reduces, 10.8 MB
+        instead of 18.1 at C3 = 32."""
+        if getattr(st, 'pk', None) is None:
+            L = self.layout
+            st.pk_na = int(self.lib.acmi_kfac_packed_floats(L.A, L.C3, 1))
+            st.pk_ng = int(self.lib.acmi_kfac_packed_floats(L.A, L.C3, 2))
+            st.pk = torch.zeros(st.n_grad_red + st.pk_na + st.pk_ng, dtype=torch.float32, device=self.device)
+        return st.pk
+
     def allreduce_begin(self, st, with_stats):
         """Starts summing what acmi_backward produced -- [grads | losses (| A factor
-        stats)], a prefix of ``red`` -- over ranks without waiting: RCCL runs it on its
-        own stream while the sampled-loss backward (acmi_kfac_output_stats, which writes
-        only the G part) computes on this one.  Returns the pending handle (None on one
-        rank); allreduce_end completes the buffer."""
+        stats, packed)] -- over ranks without waiting: RCCL runs it on its own stream
+        while the sampled-loss backward (acmi_kfac_output_stats, which writes only the
+        G part) computes on this one.  Returns the pending handle (None on one rank);
+        allreduce_end completes ``red``."""
+        st.pk_active = False
         if self.world_size <= 1:
             return None
         from actorcritic import parallel
-        k = st.n_grad_red + (self.layout.stat_off[5] if with_stats else 0)
         st.loss_reduced = True
-        return parallel.allreduce_sum_async(st.red[:k])
+        if not with_stats:
+            return parallel.allreduce_sum_async(st.red[:st.n_grad_red])
+        pk, ng, L = self._packed(st), st.n_grad_red, self.layout
+        pk[:ng].copy_(st.red[:ng])
+        _lib.call('acmi_kfac_pack', L.A, L.C3, 1, ctypes.c_void_p(st.stats.data_ptr()),
+                  ctypes.c_void_p(pk[ng:].data_ptr()), self.stream())
+        st.pk_active = True
+        return parallel.allreduce_sum_async(pk[:ng + st.pk_na])
 
     def allreduce_end(self, st, with_stats, pending):
-        """Sums the G factor stats (if any) and makes this stream wait for the pending
-        prefix sum, so ``red`` is fully reduced for the kernels enqueued next."""
+        """Sums the G factor stats (packed, if the prefix carried the A stats) and makes
+        this stream wait for the pending prefix sum, then unpacks: ``red`` is fully
+        reduced for the kernels enqueued next."""
         if self.world_size <= 1:
             return
         from actorcritic import parallel
-        if with_stats:
-            parallel.allreduce_sum_(st.red[st.n_grad_red + self.layout.stat_off[5]:])
+        if not st.pk_active:
+            pending.wait()
+            return
+        pk, ng, L = st.pk, st.n_grad_red, self.layout
+        _lib.call('acmi_kfac_pack', L.A, L.C3, 2, ctypes.c_void_p(st.stats.data_ptr()),
+                  ctypes.c_void_p(pk[ng + st.pk_na:].data_ptr()), self.stream())
+        parallel.allreduce_sum_(pk[ng + st.pk_na:])
         pending.wait()
+        st.red[:ng].copy_(pk[:ng])
+        _lib.call('acmi_kfac_unpack', L.A, L.C3, 3, ctypes.c_void_p(pk[ng:].data_ptr()),
+                  ctypes.c_void_p(st.stats.data_ptr()), self.stream())
+        st.pk_active = False
 
     # -- plumbing ------------------------------------------------------------
     def net(self):

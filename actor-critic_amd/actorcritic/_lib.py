@@ -64,6 +64,9 @@ _SIGS = {
     'acmi_band_info': (c_int, [c_int, c_int, c_i64, ctypes.POINTER(c_i64)]),
     'acmi_param_count': (c_i64, [c_int, c_int]),
     'acmi_conv_prep_bytes': (c_i64, [c_int]),
+    'acmi_kfac_packed_floats': (c_i64, [c_int, c_int, c_int]),
+    'acmi_kfac_pack': (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp]),
+    'acmi_kfac_unpack': (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     'acmi_conv_prepare': (c_int, [ctypes.POINTER(Net), c_vp, c_vp]),
     'acmi_param_offsets': (c_int, [c_int, c_int, ctypes.POINTER(c_i64)]),
     'acmi_kfac_layout': (c_int, [c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64),

@@ -166,6 +166,16 @@ __device__ void pivot_inverse(double (*P)[GJB + 1]) {
   }
 }
 
+// Symmetric sweep: the damped factors are symmetric, and the sweep operator
+//   M_kk <- -P^-1,  M_kj <- P^-1 M_kj,  M_ik <- M_ik P^-1,  M_ij <- M_ij - M_ik P^-1 M_kj
+// keeps every intermediate matrix symmetric (sweeping all pivots leaves -M^-1),
+// so gj_update_kernel computes the 64x64 tiles on and above the diagonal only
+// (half the work and traffic of the plain Gauss-Jordan update) and everything
+// reads element (r, c) from the upper triangle (gj_sym).
+__device__ __forceinline__ double gj_sym(const double* M, int np, int r, int c) {
+  return r <= c ? M[(long long)r * np + c] : M[(long long)c * np + r];
+}
+
 constexpr int PANEL_COLS = 64;
 // grid: (column chunks of PANEL_COLS, active matrices); thread (column j, pivot-row
 // quarter) forms 8 rows of Rrow' = Pinv M[kb.., j] (8 accumulators, 256 LDS reads)
@@ -192,7 +202,7 @@ __global__ __launch_bounds__(256) void gj_panel_kernel(MatSet s, double* ws, int
     } else {
       double col[GJB];
 #pragma unroll
-      for (int q = 0; q < GJB; ++q) col[q] = M[(long long)(kb + q) * np + j];
+      for (int q = 0; q < GJB; ++q) col[q] = gj_sym(M, np, kb + q, j);
       double acc[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] = 0.0;
@@ -209,16 +219,20 @@ __global__ __launch_bounds__(256) void gj_panel_kernel(MatSet s, double* ws, int
   const int rows = min(PANEL_COLS, np - c0);
   for (int e = threadIdx.x; e < rows * GJB; e += 256) {
     const int i = c0 + e / GJB, t = e % GJB;
-    C[(long long)i * GJB + t] = M[(long long)i * np + kb + t];
+    C[(long long)i * GJB + t] = gj_sym(M, np, i, kb + t);
   }
 }
 
-// grid: (np/64, np/64, active matrices); 64x64 tile, 4x4 per thread
+// grid: (upper-triangle 64x64 tiles of the largest matrix, active matrices);
+// 64x64 tile, 4x4 per thread
 __global__ __launch_bounds__(256) void gj_update_kernel(MatSet s, double* ws, int step) {
-  const int mi = blockIdx.z;
+  const int mi = blockIdx.y;
   const int np = s.np[mi];
-  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
-  if (i0 >= np || j0 >= np) return;
+  const int nt = (np + 63) / 64;
+  int ti = 0, rem = blockIdx.x;  // tile (ti, tj), ti <= tj, row-major over the upper triangle
+  while (ti < nt && rem >= nt - ti) rem -= nt - ti, ++ti;
+  if (ti >= nt) return;
+  const int i0 = ti * 64, j0 = (ti + rem) * 64;
   const int kb = step * GJB;
   double* M = ws + s.m_off[mi];
   const double* R = ws + s.row_off[mi];
@@ -263,10 +277,10 @@ __global__ __launch_bounds__(256) void gj_update_kernel(MatSet s, double* ws, in
       if (j >= np) continue;
       const bool jpiv = j >= kb && j < kb + GJB;
       double v;
-      if (ipiv) {
-        v = R[(long long)(i - kb) * np + j];  // pivot rows: Pinv M_kj (Pinv itself in-block)
-      } else {
-        v = (jpiv ? 0.0 : M[(long long)i * np + j]) - acc[a][b];
+      if (ipiv) {  // pivot rows: Pinv M_kj; the pivot block -Pinv
+        v = jpiv ? -R[(long long)(i - kb) * np + j] : R[(long long)(i - kb) * np + j];
+      } else {     // pivot columns: M_ik Pinv; the rest M_ij - M_ik Pinv M_kj
+        v = jpiv ? acc[a][b] : M[(long long)i * np + j] - acc[a][b];
       }
       M[(long long)i * np + j] = v;
     }
@@ -290,7 +304,7 @@ __global__ void gj_store_kernel(OutSet o, float* inv) {
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
        e += (long long)gridDim.x * blockDim.x) {
     const int r = (int)(e / ld), c = (int)(e - (long long)r * ld);
-    dst[e] = c < n ? (float)(0.5 * (M[(long long)r * np + c] + M[(long long)c * np + r])) : 0.f;
+    dst[e] = c < n ? (float)(-gj_sym(M, np, r, c)) : 0.f;  // the sweep leaves -M^-1
   }
 }
 
@@ -434,6 +448,52 @@ __global__ void kapply_kernel(float* p, float* v, const float* d, long long n, f
   }
 }
 
+// ---------------------------------------------------------------------------
+// factor statistics as upper triangles (the data-parallel all-reduce): factor f
+// (n x n row-major at stat_off[f], symmetric) <-> n(n+1)/2 floats, row r's
+// columns r .. n-1; the selected factors back to back.  Block (row r, factor).
+// ---------------------------------------------------------------------------
+struct PackSet {
+  int count;
+  long long src_off[11];  // full factor in the stats area
+  long long dst_off[11];  // packed triangle
+  int n[11];
+};
+
+static bool pack_set(const KLayout& K, int which, PackSet* p, long long* total) {
+  if (which < 1 || which > 3) return false;
+  p->count = 0;
+  long long o = 0;
+  for (int f = 0; f < 11; ++f) {
+    if (!((f < 5 ? 1 : 2) & which)) continue;
+    const int n = (int)(f < 5 ? K.din[f] : K.dout[f - 5]);
+    const int k = p->count++;
+    p->src_off[k] = K.stat_off[f];
+    p->dst_off[k] = o;
+    p->n[k] = n;
+    o += (long long)n * (n + 1) / 2;
+  }
+  *total = o;
+  return true;
+}
+
+template <bool PACK>
+__global__ __launch_bounds__(256) void kfac_pack_kernel(PackSet p, const float* src, float* dst) {
+  const int k = blockIdx.y, r = blockIdx.x, n = p.n[k];
+  if (r >= n) return;
+  const long long tri = p.dst_off[k] + (long long)r * n - (long long)r * (r - 1) / 2 - r;  // + c
+  const long long full = p.src_off[k];
+  for (int c = r + threadIdx.x; c < n; c += 256) {
+    if constexpr (PACK) {
+      dst[tri + c] = src[full + (long long)r * n + c];
+    } else {  // both halves: the factor comes back exactly symmetric
+      const float v = src[tri + c];
+      dst[full + (long long)r * n + c] = v;
+      dst[full + (long long)c * n + r] = v;
+    }
+  }
+}
+
 }  // namespace acmi
 
 using namespace acmi;
@@ -448,6 +508,38 @@ int acmi_kfac_ema(float* biased, float* factors, const float* stats, int64_t n, 
                      stats_scale);
   ACMI_LAUNCH_CHECK("acmi_kfac_ema");
   return ACMI_OK;
+}
+
+int64_t acmi_kfac_packed_floats(int A, int C3, int which) {
+  KLayout K;
+  PackSet p;
+  long long tot;
+  if (!klayout(A, C3, &K) || !pack_set(K, which, &p, &tot)) return -1;
+  return tot;
+}
+
+static int kfac_pack_launch(int A, int C3, int which, const float* src, float* dst, hipStream_t st, bool pack) {
+  KLayout K;
+  PackSet p;
+  long long tot;
+  ACMI_REQUIRE(src && dst && klayout(A, C3, &K) && pack_set(K, which, &p, &tot), ACMI_ERR_ARG,
+               "acmi_kfac_pack/unpack: bad arguments");
+  int maxn = 0;
+  for (int k = 0; k < p.count; ++k) maxn = std::max(maxn, p.n[k]);
+  if (pack)
+    hipLaunchKernelGGL(kfac_pack_kernel<true>, dim3(maxn, p.count), dim3(256), 0, st, p, src, dst);
+  else
+    hipLaunchKernelGGL(kfac_pack_kernel<false>, dim3(maxn, p.count), dim3(256), 0, st, p, src, dst);
+  ACMI_LAUNCH_CHECK("acmi_kfac_pack");
+  return ACMI_OK;
+}
+
+int acmi_kfac_pack(int A, int C3, int which, const float* stats, float* packed, acmi_stream_t stream) {
+  return kfac_pack_launch(A, C3, which, stats, packed, (hipStream_t)stream, true);
+}
+
+int acmi_kfac_unpack(int A, int C3, int which, const float* packed, float* stats, acmi_stream_t stream) {
+  return kfac_pack_launch(A, C3, which, packed, stats, (hipStream_t)stream, false);
 }
 
 int acmi_kfac_inverse_layout(int A, int C3, int64_t* offsets, int64_t* lds) {
@@ -552,8 +644,8 @@ int acmi_kfac_inverse(int A, int C3, const float* factors, float damping, int co
     }
     hipLaunchKernelGGL(gj_panel_kernel, dim3(cdiv(anp, PANEL_COLS), a.count), dim3(256), 0, st,
                        a, ws, step);
-    hipLaunchKernelGGL(gj_update_kernel, dim3(cdiv(anp, 64), cdiv(anp, 64), a.count), dim3(256),
-                       0, st, a, ws, step);
+    const int nt = cdiv(anp, 64);
+    hipLaunchKernelGGL(gj_update_kernel, dim3(nt * (nt + 1) / 2, a.count), dim3(256), 0, st, a, ws, step);
   }
   OutSet o;
   o.ws = ws;

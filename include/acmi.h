@@ -327,6 +327,18 @@ int acmi_kfac_ema(float* biased, float* factors, const float* stats,
                   int64_t n, float decay, float debias, float stats_scale,
                   acmi_stream_t stream);
 
+/* Factor statistics as upper triangles, for the data-parallel all-reduce of the
+ * A / G statistics (the symmetric half only, 40 % fewer
+ * bytes on the wire): which = 1 the A factors, 2 the G factors, 3 both; the
+ * selected factors of the acmi_kfac_layout stats area packed back to back,
+ * factor f (n x n) as n(n+1)/2 floats, row r's columns r .. n-1.  Unpack writes
+ * both halves (the factors come back exactly symmetric).  Stream-ordered. */
+int64_t acmi_kfac_packed_floats(int num_actions, int conv3_filters, int which);
+int acmi_kfac_pack(int num_actions, int conv3_filters, int which, const float* stats, float* packed,
+                   acmi_stream_t stream);
+int acmi_kfac_unpack(int num_actions, int conv3_filters, int which, const float* packed, float* stats,
+                     acmi_stream_t stream);
+
 /* ------------------------------------------------------------------------
  * Damped inverses (kfac inv_update_thunks, kfac_utils.py:46-50): per layer
  *   lambda_l = damping / (conv_normalize && l<3 ? locations_l : 1)

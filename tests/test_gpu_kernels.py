@@ -645,3 +645,42 @@ def test_conv1_afactor_and_weight_gradient_match_float64(lib, cuda, B):
         got = astat[so[0]:so[0] + 257 * 257].cpu().double().reshape(257, 257)
         rel = (got - ref).abs().max().item() / ref.abs().max().item()
         assert rel < 1e-6, rel
+
+
+def test_kfac_pack_unpack_round_trip(lib, cuda):
+    """acmi_kfac_pack / unpack (the data-parallel all-reduce of the factor statistics
+    as upper triangles): the packed A and G parts are the factors' upper triangles
+    row by row, back to back, and unpacking restores symmetric factors bit for bit
+    (and mirrors the upper triangle into the lower one)."""
+    A, C3 = 4, 32
+    din = (ctypes.c_int64 * 6)()
+    dout = (ctypes.c_int64 * 6)()
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, din, dout, so, ctypes.byref(tot))
+    g = torch.Generator().manual_seed(3)
+    stats = torch.zeros(tot.value)
+    tris = {1: [], 2: []}
+    for f in range(11):
+        n = din[f] if f < 5 else dout[f - 5]
+        m = torch.randn(n, n, generator=g)
+        m = m + m.t()
+        stats[so[f]:so[f] + n * n] = m.reshape(-1)
+        iu = torch.triu_indices(n, n)
+        tris[1 if f < 5 else 2].append(m[iu[0], iu[1]])
+    ref = {w: torch.cat(tris[w]) for w in (1, 2)}
+    ref[3] = torch.cat([ref[1], ref[2]])
+    sd = stats.to(cuda)
+    for which in (1, 2, 3):
+        n = int(lib.acmi_kfac_packed_floats(A, C3, which))
+        assert n == ref[which].numel()
+        pk = torch.zeros(n, device=cuda)
+        _lib.call('acmi_kfac_pack', A, C3, which, _lib.ptr(sd), _lib.ptr(pk), _lib.stream_handle())
+        torch.cuda.synchronize()
+        assert torch.equal(pk.cpu(), ref[which]), which
+    pk = torch.zeros(ref[3].numel(), device=cuda)
+    _lib.call('acmi_kfac_pack', A, C3, 3, _lib.ptr(sd), _lib.ptr(pk), _lib.stream_handle())
+    back = torch.zeros(tot.value, device=cuda)
+    _lib.call('acmi_kfac_unpack', A, C3, 3, _lib.ptr(pk), _lib.ptr(back), _lib.stream_handle())
+    torch.cuda.synchronize()
+    assert torch.equal(back.cpu(), stats)
