@@ -202,6 +202,10 @@ __global__ __launch_bounds__(256) void band_bounds_kernel(const float* w1, const
 // ---------------------------------------------------------------------------
 // the band kernel
 // ---------------------------------------------------------------------------
+#ifndef ACMI_BAND_DEPTH
+#define ACMI_BAND_DEPTH 2
+#endif
+constexpr int kBandDepth = ACMI_BAND_DEPTH;  // stages of loads in flight (register sets)
 constexpr int kBandRows = 16;                         // k-rows (images) per stage
 constexpr int kBandRowBytes = kBandSlabs * 64 * 2;    // 1024: one f16 row of the staged columns
 constexpr int kBandPart = kBandRows * kBandRowBytes;  // 16 KB
@@ -261,7 +265,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
       cld[u] = isx ? (uint32_t)p.kp : (uint32_t)p.ldy;
       cscale[u] = ((G.xmask >> (si & 7)) & 1) ? sx : sy;
     }
-    float4 ra[2][4];
+    float4 ra[kBandDepth][4];
     float csum[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
@@ -336,10 +340,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
           for (int r = 0; r < 16; ++r) acc[t][a][b][r] = 0.f;
 
     using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, 1>;
     if (nk > 0) {
       fetch(kbeg, S0{});
-      fetch(kbeg + kBandRows, S1{});
+      fetch(kbeg + kBandRows, std::integral_constant<int, 1>{});
+      if constexpr (kBandDepth > 2) fetch(kbeg + 2 * kBandRows, std::integral_constant<int, 2 % kBandDepth>{});
       commit(0, S0{});
     }
     __syncthreads();
@@ -366,22 +370,31 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
           acc[t][tm][tn] = c;
         }
     };
-    // step kt: loads of kt + 2 into the set that held kt, tile 0 from stage kt,
-    // the commit of kt + 1 (set SN) into the other stage, tile 1, barrier
-    auto step = [&](int kt, int cur, auto NT, auto SN) {
+    // step kt: loads of kt + kBandDepth into the register set that held kt,
+    // tile 0 from stage kt, the commit of kt + 1 (its set) into the other LDS
+    // stage, tile 1, barrier.  I = kt mod the unroll (compile-time sets, stages).
+    constexpr int U = kBandDepth == 3 ? 6 : 2;
+    auto step = [&](int kt, auto I, auto NT) {
       constexpr int nt = decltype(NT)::value;
-      constexpr int sn = decltype(SN)::value;
+      constexpr int i = decltype(I)::value;
+      const int cur = i & 1;
       const char* s = lds + cur * kBandBuf;
-      fetch(kbeg + (kt + 2) * kBandRows, std::integral_constant<int, sn ^ 1>{});
+      fetch(kbeg + (kt + kBandDepth) * kBandRows, std::integral_constant<int, i % kBandDepth>{});
       if constexpr (nt >= 1) tile(s, 0);
-      if (kt + 1 < nk) commit(cur ^ 1, SN);
+      if (kt + 1 < nk) commit(cur ^ 1, std::integral_constant<int, (i + 1) % kBandDepth>{});
       if constexpr (nt >= 2) tile(s, 1);
       __syncthreads();
     };
     auto run = [&](auto NT) {
-      for (int kt = 0; kt < nk; kt += 2) {
-        step(kt, 0, NT, S1{});
-        if (kt + 1 < nk) step(kt + 1, 1, NT, S0{});
+      for (int kt = 0; kt < nk; kt += U) {
+        step(kt, std::integral_constant<int, 0>{}, NT);
+        if (kt + 1 < nk) step(kt + 1, std::integral_constant<int, 1>{}, NT);
+        if constexpr (U > 2) {
+          if (kt + 2 < nk) step(kt + 2, std::integral_constant<int, 2>{}, NT);
+          if (kt + 3 < nk) step(kt + 3, std::integral_constant<int, 3>{}, NT);
+          if (kt + 4 < nk) step(kt + 4, std::integral_constant<int, 4>{}, NT);
+          if (kt + 5 < nk) step(kt + 5, std::integral_constant<int, 5>{}, NT);
+        }
       }
     };
     if (ntile == 0) run(std::integral_constant<int, 0>{});
