@@ -39,7 +39,10 @@ int acmi_abi_version(void);
 /* Arithmetic of the fused weight-gradient + K-FAC A-factor reductions (conv2,
  * conv3, heads; the dominant K-FAC covariance work, kfac cov_update_thunks,
  * actorcritic/kfac_utils.py:39,44).  Both modes are fp32-accurate:
- *   ACMI_GEMM_X3  bf16x3 split operands on the bf16 matrix cores (default)
+ *   ACMI_GEMM_X3  16-bit split operands on the 16-bit matrix cores (default):
+ *                 f16x2 (two f16 parts, 3 MFMAs, power-of-two scales from
+ *                 published maxima) for the conv tower, the dX chain, the band
+ *                 and fc4 reductions; bf16x3 (6 MFMAs) for the small rest
  *   ACMI_GEMM_F32 v_mfma_f32_32x32x2_f32
  * Initial mode from the environment variable ACMI_GEMM ("x3" / "f32").
  * Not stream-ordered: set it between launches. */
