@@ -41,7 +41,8 @@ class Bwd(ctypes.Structure):
 
 
 class EnvState(ctypes.Structure):
-    _fields_ = [('episode', c_vp), ('step', c_vp), ('length', c_vp), ('total', c_vp), ('done', c_vp)]
+    _fields_ = [('episode', c_vp), ('step', c_vp), ('length', c_vp), ('total', c_vp), ('done', c_vp),
+                ('game', c_vp)]
 
 
 class RolloutIO(ctypes.Structure):

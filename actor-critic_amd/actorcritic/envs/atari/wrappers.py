@@ -25,6 +25,35 @@ ATARI_NUM_ACTIONS = {'Breakout': 4, 'Pong': 6, 'SpaceInvaders': 6, 'Seaquest': 1
                      'Qbert': 6, 'Enduro': 9, 'MsPacman': 9, 'Asteroids': 14}
 
 
+# Atari-57 (the usual benchmark list, alphabetical) with each game's minimal action-set
+# size; the mixed-game synthetic stepper indexes games in this order (csrc/stepper.hpp
+# kGameActions, oracle.GAME_ACTIONS).  Under the full 18-action set a game's actions
+# past its minimal set step as NOOP.
+ATARI57 = ('Alien', 'Amidar', 'Assault', 'Asterix', 'Asteroids', 'Atlantis', 'BankHeist', 'BattleZone',
+           'BeamRider', 'Berzerk', 'Bowling', 'Boxing', 'Breakout', 'Centipede', 'ChopperCommand',
+           'CrazyClimber', 'Defender', 'DemonAttack', 'DoubleDunk', 'Enduro', 'FishingDerby', 'Freeway',
+           'Frostbite', 'Gopher', 'Gravitar', 'Hero', 'IceHockey', 'Jamesbond', 'Kangaroo', 'Krull',
+           'KungFuMaster', 'MontezumaRevenge', 'MsPacman', 'NameThisGame', 'Phoenix', 'Pitfall', 'Pong',
+           'PrivateEye', 'Qbert', 'Riverraid', 'RoadRunner', 'Robotank', 'Seaquest', 'Skiing', 'Solaris',
+           'SpaceInvaders', 'StarGunner', 'Surround', 'Tennis', 'TimePilot', 'Tutankham', 'UpNDown', 'Venture',
+           'VideoPinball', 'WizardOfWor', 'YarsRevenge', 'Zaxxon')
+ATARI57_ACTIONS = (18, 10, 7, 9, 14, 4, 18, 18, 9, 18, 6, 18, 4, 18, 18, 9, 18, 6, 18, 9, 18, 3, 18, 8, 18, 18,
+                   18, 18, 18, 18, 14, 18, 9, 6, 8, 18, 6, 18, 6, 18, 18, 18, 18, 3, 18, 6, 18, 5, 18, 10, 8,
+                   6, 18, 9, 10, 18, 18)
+
+
+def game_index(name):
+    """Index of an Atari-57 game ('Pong', 'PongNoFrameskip-v4', or an int)."""
+    if isinstance(name, (int, np.integer)):
+        if not 0 <= int(name) < len(ATARI57):
+            raise ValueError('game index {} out of range [0, {})'.format(name, len(ATARI57)))
+        return int(name)
+    hits = [i for i, g in enumerate(ATARI57) if name.startswith(g)]  # 'PongNoFrameskip-v4' -> Pong
+    if hits:
+        return max(hits, key=lambda i: len(ATARI57[i]))
+    raise ValueError('unknown Atari-57 game {!r}'.format(name))
+
+
 def num_actions_for(env_id):
     for k, v in ATARI_NUM_ACTIONS.items():
         if env_id.startswith(k):
@@ -131,9 +160,13 @@ class SyntheticAtariEnvs(object):
         num_actions: size of the Discrete action space (Breakout 4).
         seed: game seed (frames, rewards, episode lengths are pure functions of it).
         env_offset: global id of the first env (data-parallel shards use rank*num_envs).
+        games: None (every env the default game: Breakout's dynamics), 'atari57' (global
+            env e plays ATARI57[e % 57]: a mixed-game batch, BASELINE configs[4]), or one
+            game (name / index) per env.  Mixed batches need num_actions = 18 (the full
+            action set every game accepts).
     """
 
-    def __init__(self, num_envs, num_actions=4, seed=0, env_offset=0, device=None):
+    def __init__(self, num_envs, num_actions=4, seed=0, env_offset=0, device=None, games=None):
         _lib.require_gpu()
         self.num_envs = int(num_envs)
         self.seed = int(seed) & 0xFFFFFFFF
@@ -145,12 +178,28 @@ class SyntheticAtariEnvs(object):
         z = lambda dt: torch.zeros(N, dtype=dt, device=self.device)
         self._episode, self._step, self._length = z(torch.int32), z(torch.int32), z(torch.int32)
         self._total, self._done = z(torch.float32), z(torch.uint8)
+        self.games = None
+        if games is not None:
+            if isinstance(games, str) and games == 'atari57':
+                idx = [(self.env_offset + n) % len(ATARI57) for n in range(N)]
+            else:
+                idx = [game_index(g) for g in games]
+                if len(idx) != N:
+                    raise ValueError('games: {} entries for {} envs'.format(len(idx), N))
+            if len(set(idx)) > 1 and num_actions != 18:
+                raise ValueError('a mixed-game batch needs the full action set (num_actions=18)')
+            if max(ATARI57_ACTIONS[i] for i in idx) > num_actions:
+                raise ValueError('num_actions={} is smaller than a game\'s action set'.format(num_actions))
+            self.games = torch.tensor(idx, dtype=torch.uint8, device=self.device)
         self.state = _lib.EnvState(self._episode.data_ptr(), self._step.data_ptr(), self._length.data_ptr(),
-                                   self._total.data_ptr(), self._done.data_ptr())
+                                   self._total.data_ptr(), self._done.data_ptr(), self._game_ptr(0))
         self._obs = torch.zeros((N, 84, 84, 4), dtype=torch.uint8, device=self.device)
 
     def _stream(self):
         return _lib.stream_handle(self.device)
+
+    def _game_ptr(self, n0):
+        return None if self.games is None else self.games[n0:].data_ptr()
 
     def reset_into(self, obs_ptr, stride=OBS_BYTES):
         _lib.call('acmi_env_reset', ctypes.byref(self.state), self.num_envs, self.env_offset, self.seed,
@@ -172,7 +221,7 @@ class SyntheticAtariEnvs(object):
         if st is None:
             st = _lib.EnvState(self._episode[n0:].data_ptr(), self._step[n0:].data_ptr(),
                                self._length[n0:].data_ptr(), self._total[n0:].data_ptr(),
-                               self._done[n0:].data_ptr())
+                               self._done[n0:].data_ptr(), self._game_ptr(n0))
             self._range_states[n0] = st
         return st
 

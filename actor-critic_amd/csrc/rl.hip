@@ -313,7 +313,8 @@ __global__ __launch_bounds__(256) void env_reset_kernel(acmi_env_state_t st, int
                                                         long long stride) {
   const int n = blockIdx.x;
   const uint32_t e = (uint32_t)(env_offset + n);
-  const uint32_t base = key4(seed, e, 0u, RESET_TAG);
+  const GameParams gp = game_params(env_game(st, n));
+  const uint32_t base = key4(seed ^ gp.salt, e, 0u, RESET_TAG);
   uint4* out = reinterpret_cast<uint4*>(obs + (long long)n * stride);
   for (int g = threadIdx.x; g < FRAME_WORDS; g += blockDim.x) {
     const uint32_t w = word_hash(base, (uint32_t)g);
@@ -327,7 +328,7 @@ __global__ __launch_bounds__(256) void env_reset_kernel(acmi_env_state_t st, int
   if (threadIdx.x == 0) {
     st.episode[n] = 0;
     st.step[n] = 0;
-    st.length[n] = episode_length(seed, e, 0u);
+    st.length[n] = episode_length(seed, e, 0u, gp);
     st.total[n] = 0.f;
     st.done[n] = 0;
   }

@@ -18,8 +18,47 @@ constexpr uint32_t REW_HI = 15938355u;    // 2^24 - REW_LO
 __device__ __forceinline__ uint32_t word_hash(uint32_t base, uint32_t g) {
   return mix32(base ^ (g * 0x9E3779B9u));
 }
-__device__ __forceinline__ int32_t episode_length(uint32_t seed, uint32_t e, uint32_t k) {
-  return 50 + (int32_t)(key4(seed, e, k, LEN_TAG) % 451u);
+
+// Mixed-game synthetic Atari-57 (BASELINE configs[4]; the reference's MultiEnv
+// holds one game, multi_env.py:36-47).  Env n plays game st.game[n] (index into
+// the Atari-57 list, wrappers.ATARI57); a null game array = every env the
+// default game (Breakout's dynamics, no action masking).  A game fixes its
+// dynamics salt (XORed into the seed: its own frames, rewards and lengths), its
+// episode-length range, its +-1 reward rates and its legal-action count under
+// the full 18-action set (actions past it act as NOOP, as in ALE).  Breakout's
+// entry is the default game's dynamics.  Restated in oracle.game_params.
+constexpr int kNumGames = 57;
+constexpr int kGameBreakout = 12;
+__constant__ uint8_t kGameActions[kNumGames] = {
+    18, 10, 7, 9, 14, 4, 18, 18, 9, 18, 6, 18, 4, 18, 18, 9, 18, 6, 18, 9,
+    18, 3, 18, 8, 18, 18, 18, 18, 18, 18, 14, 18, 9, 6, 8, 18, 6, 18, 6, 18,
+    18, 18, 18, 3, 18, 6, 18, 5, 18, 10, 8, 6, 18, 9, 10, 18, 18};
+
+struct GameParams {
+  uint32_t salt, len_min, len_span, rew_lo, rew_hi, n_legal;
+};
+
+__device__ __forceinline__ GameParams game_params(int g) {  // g < 0: the default game
+  GameParams p{0u, 50u, 451u, REW_LO, REW_HI, 256u};
+  if (g < 0 || g == kGameBreakout) {
+    if (g == kGameBreakout) p.n_legal = 4u;
+    return p;
+  }
+  const uint32_t h = mix32(0x47414D45u ^ ((uint32_t)g * 0x9E3779B9u));
+  const uint32_t h2 = mix32(h), h3 = mix32(h2);
+  p.salt = h | 1u;
+  p.len_min = 30u + h2 % 171u;          // 30 .. 200
+  p.len_span = 100u + (h2 >> 8) % 1901u;  // episodes up to ~2100 steps
+  p.rew_lo = (uint32_t)(((uint64_t)(h3 & 0xFFFFu) * 838861u) >> 16);  // P(-1) in [0, 0.05)
+  p.rew_hi = 16777216u - 83886u - (uint32_t)(((uint64_t)(h3 >> 16) * (3355443u - 83886u)) >> 16);  // P(+1) in (0.005, 0.2]
+  p.n_legal = kGameActions[g];
+  return p;
+}
+__device__ __forceinline__ int env_game(acmi_env_state_t st, int n) { return st.game ? (int)st.game[n] : -1; }
+
+__device__ __forceinline__ int32_t episode_length(uint32_t seed, uint32_t e, uint32_t k,
+                                                  const GameParams& gp) {
+  return (int32_t)(gp.len_min + key4(seed ^ gp.salt, e, k, LEN_TAG) % gp.len_span);
 }
 
 // One env step for env n (global id e) by a whole 256-thread workgroup: reads
@@ -35,6 +74,7 @@ constexpr int kEnvWords = (FRAME_WORDS + kEnvThreads - 1) / kEnvThreads;  // 7
 struct EnvPre {  // an env's pre-step state and current stack words, loaded up front
   uint4 old[kEnvWords];
   int32_t k, t, L;
+  int game;
   float total;
   bool was_done;
 };
@@ -51,6 +91,7 @@ __device__ __forceinline__ void env_prefetch(acmi_env_state_t st, int n, const u
   p.t = st.step[n];
   p.L = st.length[n];
   p.total = st.total[n];
+  p.game = env_game(st, n);
 }
 
 // (the state of env n must have been read by every thread -- env_prefetch --
@@ -66,20 +107,22 @@ __device__ __forceinline__ void env_step_block_pre(acmi_env_state_t st, int n, u
   int32_t t = pre.t;
   int32_t L = pre.L;
   float total = pre.total;
+  const GameParams gp = game_params(pre.game);
   __syncthreads();
   if (was_done) {  // _AutoResetWrapper: reset lazily at the next step
     k += 1;
     t = 0;
-    L = episode_length(seed, e, (uint32_t)k);
+    L = episode_length(seed, e, (uint32_t)k, gp);
     total = 0.f;
   }
   t += 1;
-  const uint32_t a = action & 255u;
-  const uint32_t base = key4(seed, e, (uint32_t)k, (uint32_t)t * 256u + a);
+  const uint32_t a = (action & 255u) < gp.n_legal ? (action & 255u) : 0u;  // illegal: NOOP
+  const uint32_t gseed = seed ^ gp.salt;
+  const uint32_t base = key4(gseed, e, (uint32_t)k, (uint32_t)t * 256u + a);
   const uint32_t rh = mix32(base ^ REW_SALT) >> 8;
-  const float rew = rh < REW_LO ? -1.f : (rh >= REW_HI ? 1.f : 0.f);
+  const float rew = rh < gp.rew_lo ? -1.f : (rh >= gp.rew_hi ? 1.f : 0.f);
   const bool term = t >= L;
-  const uint32_t rbase = key4(seed, e, (uint32_t)k, RESET_TAG);
+  const uint32_t rbase = key4(gseed, e, (uint32_t)k, RESET_TAG);
   uint4* out = reinterpret_cast<uint4*>(obs_out);
 #pragma unroll
   for (int i = 0; i < kEnvWords; ++i) {

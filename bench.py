@@ -64,8 +64,11 @@ def measured_traffic(kernel, workload):
     return None
 
 
-def workload_name(algo, N, T, A, forward, world):
+def workload_name(algo, N, T, A, forward, world, games=None):
     """The BASELINE.json config a line measures (configs[1]-[4]; others: as given)."""
+    if games == 'atari57':
+        return ('Mixed Atari-57 {} {} envs/GPU x {} steps, {} actions, {} forward / fp32 K-FAC{}'.format(
+            algo.upper(), N, T, A, forward, ' (BASELINE configs[4] shard)' if forward == 'bf16' and A == 18 else ''))
     if forward == 'bf16':
         return ('Atari {} {} envs/GPU x {} steps, {} actions, bf16 forward / fp32 K-FAC (BASELINE configs[4] '
                 'shard)'.format(algo.upper(), N, T, A))
@@ -91,6 +94,9 @@ def parse():
     p.add_argument('--forward', choices=['f32', 'bf16'], default=None,
                    help='conv tower precision (default: ACMI_FORWARD or f32; bf16: BASELINE configs[4] '
                         '"bf16 forward / fp32 KFAC factors")')
+    p.add_argument('--games', choices=['atari57'], default=None,
+                   help='atari57: env e plays Atari-57 game e %% 57 (mixed-game batch, BASELINE configs[4]; '
+                        'needs --num-actions 18); default: every env synthetic Breakout')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-iters', type=int, default=3, help='timed CPU-baseline iterations (at most ~20 s)')
     p.add_argument('--quiet', action='store_true')
@@ -174,7 +180,8 @@ def run(args):
     A = args.num_actions
 
     sess.reset_default_graph()
-    env = MultiEnv(SyntheticAtariEnvs(N, num_actions=A, seed=1234, env_offset=rank * N, device=dev))
+    env = MultiEnv(SyntheticAtariEnvs(N, num_actions=A, seed=1234, env_offset=rank * N, device=dev,
+                                      games=args.games))
     model = AtariModel(env.observation_space, env.action_space, C3, random_seed=7, device=dev)
     agent = MultiEnvAgent(env, model, T)
     objective = A2CObjective(model, discount_factor=0.99, entropy_regularization_strength=0.01)
@@ -294,7 +301,8 @@ def run(args):
         sys.path.insert(0, os.path.join(ROOT, 'oracle'))
         import cpu_baseline
         # the same workload as the GPU line (envs, steps, algorithm, actions, C3)
-        r = cpu_baseline.run(n_envs=N, n_steps=T, iters=args.cpu_iters, A=A, C3=C3, algo=args.algo)
+        r = cpu_baseline.run(n_envs=N, n_steps=T, iters=args.cpu_iters, A=A, C3=C3, algo=args.algo,
+                             games=args.games)
         cpu = {'value': r['env_steps_per_s'], 'unit': 'env-steps/s', 'cores': r['threads'], 'kind': 'port',
                'sample': '{} timed iterations (after one warm-up) of the same {} workload ({} envs x {} steps): '
                          'torch-CPU fp32 restatement, {}{}'.format(
@@ -308,7 +316,8 @@ def run(args):
             'value': value, 'unit': 'env-steps/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': ms_per_step, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
             'dtype': 'fp32' if args.forward == 'f32' else 'bf16 forward / fp32 update', 'data': 'synthetic (hashed 84x84 u8 frames, random-init orthogonal weights)',
-            'config': {'workload': workload_name(args.algo, N, T, A, args.forward, world), 'algo': args.algo,
+            'config': {'workload': workload_name(args.algo, N, T, A, args.forward, world, args.games),
+                       'algo': args.algo, 'games': args.games or 'Breakout',
                        'envs_per_gpu': N, 'num_steps': T,
                 'global_envs': N * world, 'num_actions': A, 'conv3_filters': C3, 'forward': args.forward,
                 'parallelism': 'dp{}'.format(world)},

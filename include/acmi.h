@@ -408,6 +408,12 @@ int acmi_rmsprop_apply(float* params, float* ms, float* mom,
  * episode length 50 + (hash % 451).  State arrays are per env ([N]).
  * Stacks are NHWC [84][84][4] u8; env n reads obs_in + n*in_stride and
  * writes obs_out + n*out_stride (in-place allowed).
+ * Mixed games (Atari-57, BASELINE configs[4] -- an extension: the
+ * reference's MultiEnv holds one game, multi_env.py:36-47): with `game`
+ * set, env n plays game[n] (0..56, the order of wrappers.ATARI57), whose
+ * own salt, episode-length range, reward rates and legal-action count
+ * (actions past it step as NOOP) replace the defaults above; game 12
+ * (Breakout) keeps them.  game == NULL: every env the default game.
  * ---------------------------------------------------------------------- */
 typedef struct acmi_env_state {
   int32_t* episode;   /* episode index                                    */
@@ -415,6 +421,7 @@ typedef struct acmi_env_state {
   int32_t* length;    /* terminal step of the current episode             */
   float* total;       /* EpisodeInfoWrapper.total_reward                   */
   uint8_t* done;      /* _AutoResetWrapper._terminated                     */
+  const uint8_t* game; /* game index per env, or NULL (read only)          */
 } acmi_env_state_t;
 
 int acmi_env_reset(const acmi_env_state_t* st, int N, int env_offset,

@@ -70,8 +70,9 @@ class SyntheticRawAtari(object):
     """One synthetic game, raw 84x84x1 frames, with EpisodeInfoWrapper's episode total
     in info (wrappers.py:263-294).  Frames/rewards/lengths: oracle.SyntheticAtari's."""
 
-    def __init__(self, seed, env_id, num_actions):
-        self.seed, self.e = seed, env_id
+    def __init__(self, seed, env_id, num_actions, game=None):
+        self.seed, self.e, self.game = seed, env_id, game
+        self.salt, _, _, self.rew_lo, self.rew_hi, self.n_legal = oracle.game_params(game)
         self.k, self.t, self.total = -1, 0, 0.0
         self.L = 0
         self.action_space = _Discrete(num_actions)
@@ -80,15 +81,16 @@ class SyntheticRawAtari(object):
     def reset(self):
         self.k += 1
         self.t, self.total = 0, 0.0
-        self.L = oracle.episode_length(self.seed, self.e, self.k)
-        return oracle.reset_frame(self.seed, self.e, self.k)[..., None]
+        self.L = oracle.episode_length(self.seed, self.e, self.k, self.game)
+        return oracle.reset_frame(self.seed, self.e, self.k, self.game)[..., None]
 
     def step(self, action):
         self.t += 1
         a = int(action) & 255
-        base = int(oracle.key4(self.seed, self.e, self.k, self.t * 256 + a))
+        a = a if a < self.n_legal else 0
+        base = int(oracle.key4(self.seed ^ self.salt, self.e, self.k, self.t * 256 + a))
         rh = int(oracle.mix32(np.uint32(base) ^ oracle.REW_SALT)) >> 8
-        r = -1.0 if rh < oracle.REW_LO else (1.0 if rh >= oracle.REW_HI else 0.0)
+        r = -1.0 if rh < self.rew_lo else (1.0 if rh >= self.rew_hi else 0.0)
         term = self.t >= self.L
         self.total += r
         info = {}
@@ -101,14 +103,15 @@ class SyntheticRawAtari(object):
         pass
 
 
-def make_raw_env(seed, env_id, num_actions):
-    return SyntheticRawAtari(seed, env_id, num_actions)
+def make_raw_env(seed, env_id, num_actions, game=None):
+    return SyntheticRawAtari(seed, env_id, num_actions, game)
 
 
-def make_envs(n_envs, num_actions, seed, ipc):
+def make_envs(n_envs, num_actions, seed, ipc, games=None):
     from actorcritic.envs.atari.wrappers import FrameStackWrapper
     from actorcritic.multi_env import MultiEnv, create_subprocess_envs
-    fns = [functools.partial(make_raw_env, seed, e, num_actions) for e in range(n_envs)]
+    game = (lambda e: e % 57) if games == 'atari57' else (lambda e: None)
+    fns = [functools.partial(make_raw_env, seed, e, num_actions, game(e)) for e in range(n_envs)]
     raw = create_subprocess_envs(fns) if ipc else [fn() for fn in fns]
     return MultiEnv([FrameStackWrapper(env, 4) for env in raw])
 
@@ -172,7 +175,7 @@ def _sample(torch, logits, gen):
 
 
 def run(n_envs=32, n_steps=20, iters=3, A=4, C3=32, algo='acktr', seed=0, time_budget_s=20.0, ipc=None,
-        threads=None):
+        threads=None, games=None):
     """Times warm-up + up to `iters` iterations (at most ~time_budget_s); returns
     env-steps/s and the update / rollout split."""
     import torch
@@ -191,7 +194,7 @@ def run(n_envs=32, n_steps=20, iters=3, A=4, C3=32, algo='acktr', seed=0, time_b
     vel = [torch.zeros_like(w) for w in W]
     ms = [torch.ones_like(w) for w in W]
     gamma, beta, lr_acktr, lr_a2c = 0.99, 0.01, 0.25, 7e-4
-    env = make_envs(n_envs, A, seed, ipc)
+    env = make_envs(n_envs, A, seed, ipc, games)
     obs = np.stack(env.reset())
     stats = dict(rollout=0.0, update=0.0, n=0)
     inv_s = 0.0

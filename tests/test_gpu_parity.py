@@ -147,6 +147,60 @@ def test_stepper_matches_reference_wrapper_trace(lib, cuda):
         assert ep_seen[e] == [None if v is None else pytest.approx(v) for v in row]
 
 
+def test_mixed_game_stepper_matches_oracle(lib, cuda):
+    """Atari-57 mixed batch (BASELINE configs[4]): 64 envs, global ids 40.. so the game
+    index wraps, 18 actions (illegal ones step as NOOP), 300 steps -- several episodes of
+    the short games, auto-resets included -- bit-exact against the oracle envs."""
+    from actorcritic.envs.atari.wrappers import ATARI57, SyntheticAtariEnvs
+    N, off, seed = 64, 40, 77
+    env = SyntheticAtariEnvs(N, num_actions=18, seed=seed, env_offset=off, games='atari57')
+    games = [(off + n) % 57 for n in range(N)]
+    assert env.games.cpu().tolist() == games
+    ref = [oracle.SyntheticAtari(seed, off + n, game=g) for n, g in enumerate(games)]
+    o = env.reset().cpu().numpy()
+    for n in range(N):
+        np.testing.assert_array_equal(o[n], ref[n].reset())
+    rng = np.random.default_rng(1)
+    n_term = 0
+    for t in range(300):
+        a = rng.integers(0, 18, N).astype(np.int32)
+        ob, r, d, info = env.step(a)
+        ob, r, d = ob.cpu().numpy(), r.cpu().numpy(), d.cpu().numpy()
+        ep = info.episode_rewards.cpu().numpy()[:, 0]
+        for n in range(N):
+            rob, rr, rd, rep = ref[n].step(int(a[n]))
+            assert zlib.crc32(ob[n].tobytes()) == zlib.crc32(rob.tobytes()), (n, t)
+            assert r[n] == rr and bool(d[n]) == rd, (n, t, ATARI57[games[n]])
+            assert (np.isnan(ep[n]) and np.isnan(rep)) or ep[n] == rep
+            n_term += rd
+    assert n_term > 0
+
+
+def test_mixed_game_rollout_matches_oracle_env(lib, cuda):
+    """The fused rollout tail steps mixed games like the standalone stepper."""
+    from actorcritic import session as sess
+    from actorcritic.agents import MultiEnvAgent
+    from actorcritic.envs.atari.model import AtariModel
+    from actorcritic.envs.atari.wrappers import SyntheticAtariEnvs
+    from actorcritic.multi_env import MultiEnv
+    sess.reset_default_graph()
+    N, T, A = 6, 8, 18
+    env = MultiEnv(SyntheticAtariEnvs(N, num_actions=A, seed=9, env_offset=50, games='atari57'))
+    model = AtariModel(env.observation_space, env.action_space, 32, params=oracle.init_params(A, 32, seed=1),
+                       random_seed=3)
+    agent = MultiEnvAgent(env, model, T)
+    with sess.Session() as s:
+        obs, act, rew, term, nxt, _ = agent.interact(s)
+    o = obs.cpu().numpy()
+    for n in range(N):
+        ref = oracle.SyntheticAtari(9, 50 + n, game=(50 + n) % 57)
+        np.testing.assert_array_equal(o[n, 0], ref.reset())
+        for t in range(T):
+            ob, r, d, _ = ref.step(int(act[n, t]))
+            np.testing.assert_array_equal(o[n, t + 1] if t + 1 < T else nxt[n].cpu().numpy(), ob)
+            assert float(rew[n, t]) == r and bool(term[n, t]) == d
+
+
 def test_sampling_exact_with_given_uniforms_and_calibrated(lib, cuda):
     rng = np.random.default_rng(3)
     B, A = 4096, 6

@@ -173,3 +173,44 @@ def test_sharded_statistics_average_to_full_batch():
     g_sh = [oracle.backward(params, oracle.forward(params, obs[i:i + 2], A, C3), dl[i:i + 2] * 2, dv[i:i + 2] * 2,
                             A, C3)[0] for i in (0, 2)]
     np.testing.assert_allclose((g_sh[0] + g_sh[1]) / 2, g_full, rtol=1e-9, atol=1e-12)
+
+
+def test_atari57_game_table_and_names():
+    """Mixed-game synthetic Atari-57 (BASELINE configs[4]): the oracle's game table keeps
+    Breakout on the default dynamics, gives every other game its own salt, ranges inside
+    the documented bounds, and the host name table matches the device action table."""
+    sys.path.insert(0, os.path.join(ROOT, 'actor-critic_amd'))
+    from actorcritic.envs.atari import wrappers
+    assert len(wrappers.ATARI57) == 57 == len(wrappers.ATARI57_ACTIONS) == len(oracle.GAME_ACTIONS)
+    assert tuple(wrappers.ATARI57_ACTIONS) == tuple(oracle.GAME_ACTIONS)
+    assert wrappers.ATARI57[oracle.GAME_BREAKOUT] == 'Breakout'
+    assert oracle.game_params(None) == (0, 50, 451, oracle.REW_LO, oracle.REW_HI, 256)
+    assert oracle.game_params(oracle.GAME_BREAKOUT)[:5] == oracle.game_params(None)[:5]
+    salts = set()
+    for g in range(57):
+        salt, lmin, lspan, lo, hi, nl = oracle.game_params(g)
+        salts.add(salt)
+        if g == oracle.GAME_BREAKOUT:
+            continue
+        assert 30 <= lmin <= 200 and 100 <= lspan <= 2000
+        assert 0 <= lo < 0.05 * 2 ** 24 and 0.8 * 2 ** 24 <= hi < (1 - 0.005) * 2 ** 24 + 1
+        assert nl == wrappers.ATARI57_ACTIONS[g]
+    assert len(salts) == 57
+    assert wrappers.game_index('PongNoFrameskip-v4') == wrappers.ATARI57.index('Pong')
+    assert wrappers.game_index('BreakoutNoFrameskip-v4') == oracle.GAME_BREAKOUT
+    assert wrappers.game_index('Asterix') != wrappers.game_index('Asteroids')
+    with pytest.raises(ValueError):
+        wrappers.game_index('NotAGame')
+    # the default game is the same env as before the game table (golden traces)
+    e = oracle.SyntheticAtari(5, 2)
+    f = oracle.SyntheticAtari(5, 2, game=oracle.GAME_BREAKOUT)
+    np.testing.assert_array_equal(e.reset(), f.reset())
+    for t in range(80):
+        a, b = e.step(t % 4), f.step(t % 4)
+        np.testing.assert_array_equal(a[0], b[0])
+        assert a[1:3] == b[1:3]
+    # an illegal action of a 3-action game steps as NOOP
+    g = wrappers.ATARI57.index('Freeway')
+    x, y = oracle.SyntheticAtari(5, 0, game=g), oracle.SyntheticAtari(5, 0, game=g)
+    x.reset(), y.reset()
+    np.testing.assert_array_equal(x.step(17)[0], y.step(0)[0])
