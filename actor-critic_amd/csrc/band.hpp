@@ -206,6 +206,13 @@ __global__ __launch_bounds__(256) void band_bounds_kernel(const float* w1, const
 #define ACMI_BAND_DEPTH 2
 #endif
 constexpr int kBandDepth = ACMI_BAND_DEPTH;  // stages of loads in flight (register sets)
+#ifndef ACMI_BAND_ORDER
+#define ACMI_BAND_ORDER 0
+#endif
+#ifndef ACMI_BAND_PROBE  // timing probes (wrong results): 1 no split, 2 no column sums, 4 no loads,
+                         // 8 no LDS stores, 16 no MFMAs, 32 no LDS fragment reads
+#define ACMI_BAND_PROBE 0
+#endif
 constexpr int kBandRows = 16;                         // k-rows (images) per stage
 constexpr int kBandRowBytes = kBandSlabs * 64 * 2;    // 1024: one f16 row of the staged columns
 constexpr int kBandPart = kBandRows * kBandRowBytes;  // 16 KB
@@ -281,7 +288,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
       for (int r = 0; r < 2; ++r) {
         const bool rok = k0 + 2 * rp + r < kend;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) ra[set][2 * r + u] = stage_f4(cptr[u] + foff[u] + r * cld[u], rok && cok[u]);
+        for (int u = 0; u < 2; ++u) {
+          if constexpr (ACMI_BAND_PROBE & 4)
+            ra[set][2 * r + u] = make_float4((float)(k0 + r), (float)u, (float)lane, 1.f);
+          else
+            ra[set][2 * r + u] = stage_f4(cptr[u] + foff[u] + r * cld[u], rok && cok[u]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) foff[u] += (uint32_t)kBandRows * cld[u];
@@ -296,16 +308,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const float4 v = ra[set][2 * r + u];
-          csum[4 * u] += v.x;
-          csum[4 * u + 1] += v.y;
-          csum[4 * u + 2] += v.z;
-          csum[4 * u + 3] += v.w;
+          if constexpr (!(ACMI_BAND_PROBE & 2)) {
+            csum[4 * u] += v.x;
+            csum[4 * u + 1] += v.y;
+            csum[4 * u + 2] += v.z;
+            csum[4 * u + 3] += v.w;
+          }
           uint2 h, l;
-          split2(v.x, v.y, cscale[u], h.x, l.x);
-          split2(v.z, v.w, cscale[u], h.y, l.y);
+          if constexpr (ACMI_BAND_PROBE & 1) {
+            h.x = __float_as_uint(v.x) ^ __float_as_uint(v.y);
+            h.y = __float_as_uint(v.z) ^ __float_as_uint(v.w);
+            l = h;
+          } else {
+            split2(v.x, v.y, cscale[u], h.x, l.x);
+            split2(v.z, v.w, cscale[u], h.y, l.y);
+          }
           const int off = 8 * ((64 * u + lane) ^ q8);  // 8-byte slot (4 columns) of column 4*(64u + lane)
-          *reinterpret_cast<uint2*>(s + off) = h;
-          *reinterpret_cast<uint2*>(s + kBandPart + off) = l;
+          if constexpr (ACMI_BAND_PROBE & 8) {
+            csum[4 * u] += __uint_as_float(h.x ^ l.y);
+          } else {
+            *reinterpret_cast<uint2*>(s + off) = h;
+            *reinterpret_cast<uint2*>(s + kBandPart + off) = l;
+          }
         }
       }
     };
@@ -355,8 +379,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
         const char* sp = s + pt * kBandPart;
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
-          a[cb][pt] = cat8h(ds_tr16(sp + aoff[t][cb]), ds_tr16(sp + aoff[t][cb] + 4 * kBandRowBytes));
-          b[cb][pt] = cat8h(ds_tr16(sp + boff[t][cb]), ds_tr16(sp + boff[t][cb] + 4 * kBandRowBytes));
+          if constexpr (ACMI_BAND_PROBE & 32) {
+            a[cb][pt] = b[cb][pt] = f16x8{(_Float16)(float)(aoff[t][cb] + pt), (_Float16)(float)cb, 0, 0, 0, 0, 0, 0};
+          } else {
+            a[cb][pt] = cat8h(ds_tr16(sp + aoff[t][cb]), ds_tr16(sp + aoff[t][cb] + 4 * kBandRowBytes));
+            b[cb][pt] = cat8h(ds_tr16(sp + boff[t][cb]), ds_tr16(sp + boff[t][cb] + 4 * kBandRowBytes));
+          }
         }
       }
 #pragma unroll
@@ -364,9 +392,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
 #pragma unroll
         for (int tn = 0; tn < 2; ++tn) {
           f32x16 c = acc[t][tm][tn];
-          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][1], b[tn][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][0], b[tn][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][0], b[tn][0], c, 0, 0, 0);
+          if constexpr (ACMI_BAND_PROBE & 16) {
+            c[0] += (float)a[tm][1][0] + (float)b[tn][0][1] + (float)a[tm][0][2] + (float)b[tn][1][3];
+          } else {
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][1], b[tn][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][0], b[tn][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][0], b[tn][0], c, 0, 0, 0);
+          }
           acc[t][tm][tn] = c;
         }
     };
@@ -380,9 +412,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
       const int cur = i & 1;
       const char* s = lds + cur * kBandBuf;
       fetch(kbeg + (kt + kBandDepth) * kBandRows, std::integral_constant<int, i % kBandDepth>{});
+#if ACMI_BAND_ORDER == 1
+      // both tiles' fragment reads ahead of the commit's stores (the stores
+      // would order the second tile's reads behind them)
+      if constexpr (nt >= 1) tile(s, 0);
+      if constexpr (nt >= 2) tile(s, 1);
+      if (kt + 1 < nk) commit(cur ^ 1, std::integral_constant<int, (i + 1) % kBandDepth>{});
+#else
       if constexpr (nt >= 1) tile(s, 0);
       if (kt + 1 < nk) commit(cur ^ 1, std::integral_constant<int, (i + 1) % kBandDepth>{});
       if constexpr (nt >= 2) tile(s, 1);
+#endif
       __syncthreads();
     };
     auto run = [&](auto NT) {
