@@ -206,9 +206,6 @@ __global__ __launch_bounds__(256) void band_bounds_kernel(const float* w1, const
 #define ACMI_BAND_DEPTH 2
 #endif
 constexpr int kBandDepth = ACMI_BAND_DEPTH;  // stages of loads in flight (register sets)
-#ifndef ACMI_BAND_ORDER
-#define ACMI_BAND_ORDER 0
-#endif
 #ifndef ACMI_BAND_PROBE  // timing probes (wrong results): 1 no split, 2 no column sums, 4 no loads,
                          // 8 no LDS stores, 16 no MFMAs, 32 no LDS fragment reads
 #define ACMI_BAND_PROBE 0
@@ -412,17 +409,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
       const int cur = i & 1;
       const char* s = lds + cur * kBandBuf;
       fetch(kbeg + (kt + kBandDepth) * kBandRows, std::integral_constant<int, i % kBandDepth>{});
-#if ACMI_BAND_ORDER == 1
-      // both tiles' fragment reads ahead of the commit's stores (the stores
-      // would order the second tile's reads behind them)
-      if constexpr (nt >= 1) tile(s, 0);
-      if constexpr (nt >= 2) tile(s, 1);
-      if (kt + 1 < nk) commit(cur ^ 1, std::integral_constant<int, (i + 1) % kBandDepth>{});
-#else
       if constexpr (nt >= 1) tile(s, 0);
       if (kt + 1 < nk) commit(cur ^ 1, std::integral_constant<int, (i + 1) % kBandDepth>{});
       if constexpr (nt >= 2) tile(s, 1);
-#endif
       __syncthreads();
     };
     auto run = [&](auto NT) {
