@@ -415,6 +415,17 @@ inline void launch_gemm3_f16(const OpA& a, const OpB& b, const Epi& e, int I, in
                      amax_b);
 }
 
+// the f16x2 form with split-K and the symmetric skip (Gram matrices of tensors
+// whose max a dX epilogue published)
+template <int BM, int BN, int BK, int WTM, int WTN, class OpA, class OpB, class Epi>
+inline void launch_gemm3_f16_splitk(const OpA& a, const OpB& b, const Epi& e, int I, int J, int K, int zdim,
+                                    int k_chunk, const unsigned* amax_a, const unsigned* amax_b,
+                                    hipStream_t s, int sym_cols = 0) {
+  hipLaunchKernelGGL((gemm3_kernel<BM, BN, BK, WTM, WTN, true, false, OpA, OpB, Epi, true>),
+                     dim3(live_tiles<BM, BN>(I, J, sym_cols) * zdim), dim3(256), 0, s, a, b, e, I, J, K, k_chunk,
+                     sym_cols, amax_a, amax_b);
+}
+
 // launch_gemm's interface, run on gemm3_kernel (bf16x3, K-tile BK3) in
 // ACMI_GEMM_X3 mode and on gemm_kernel (f32 MFMA, K-tile BK) otherwise
 template <int BM, int BN, int BK, int WTM, int WTN, bool SPLITK, bool COLSUM, int BK3 = 16,

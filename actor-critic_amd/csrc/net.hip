@@ -928,10 +928,13 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
   return ACMI_OK;
 }
 
-// G = g^T g / rows for g [rows][ld] (first n columns), via split-K
+// G = g^T g / rows for g [rows][ld] (first n columns), via split-K; gmax: the
+// published max |g| (bit pattern) -- the wide Grams then run on f16x2 split
+// operands (three MFMAs per product instead of bf16x3's six)
 static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
                       float* part, long long part_cap, float* out,
-                      hipStream_t s, float* out_v = nullptr, int v_index = -1) {
+                      hipStream_t s, float* out_v = nullptr, int v_index = -1,
+                      const unsigned* gmax = nullptr) {
   int np, nc;
   if (n <= 32) {  // narrow: streaming Gram kernel (f32 MFMA; 64 wide runs faster on the split-K
                   // bf16x3 GEMM below: conv2's G factor 82 + 25 -> 59 + 16 us)
@@ -951,7 +954,10 @@ static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
     RowsAsI<DenseRows> op{src};
     ACMI_REQUIRE(pl.floats <= part_cap, ACMI_ERR_WS, "gcov workspace too small");
     EpiPartial epi{part, np, np};
-    launch_mm<64, 64, 32, 1, 1, true, false, 16>(op, op, epi, np, np, (int)rows, nc, pl.ch, s, np);
+    if (gmax && g_gemm_mode == ACMI_GEMM_X3)
+      launch_gemm3_f16_splitk<64, 64, 16, 1, 1>(op, op, epi, np, np, (int)rows, nc, (int)pl.ch, gmax, gmax, s, np);
+    else
+      launch_mm<64, 64, 32, 1, 1, true, false, 16>(op, op, epi, np, np, (int)rows, nc, pl.ch, s, np);
   }
   if (nc <= 64)
     hipLaunchKernelGGL(finalize_cov_thread_kernel, dim3(cdiv((long long)sub * sub, 256)), dim3(256), 0,
@@ -1267,11 +1273,14 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
   rc = gcov_layer(ghead, ldg, L.A + 1, B, L.A, part, cap, gstat + L.stat_off[5 + 4], s,
                   gstat + L.stat_off[5 + 5], L.A);
   if (rc) return rc;
-  rc = gcov_layer(bw->d4, 512, 512, B, 512, part, cap, gstat + L.stat_off[5 + 3], s);
+  // (the dX chain above published max |d4| and max |d2| into dxs)
+  rc = gcov_layer(bw->d4, 512, 512, B, 512, part, cap, gstat + L.stat_off[5 + 3], s, nullptr, -1,
+                  dxs + kBsMaxD4);
   if (rc) return rc;
   rc = gcov_layer(bw->d3, C3, C3, 49LL * B, C3, part, cap, gstat + L.stat_off[5 + 2], s);
   if (rc) return rc;
-  rc = gcov_layer(bw->d2, 64, 64, 81LL * B, 64, part, cap, gstat + L.stat_off[5 + 1], s);
+  rc = gcov_layer(bw->d2, 64, 64, 81LL * B, 64, part, cap, gstat + L.stat_off[5 + 1], s, nullptr, -1,
+                  dxs + kBsMaxD2);
   if (rc) return rc;
   if (!g1_done) rc = gcov_layer(bw->d1, 32, 32, 400LL * B, 32, part, cap, gstat + L.stat_off[5 + 0], s);
   return rc;
