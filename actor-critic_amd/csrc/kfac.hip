@@ -191,18 +191,29 @@ __global__ __launch_bounds__(256) void gj_panel_kernel(MatSet s, double* ws, int
   __shared__ double P[GJB][GJB + 1];
   for (int e = threadIdx.x; e < GJB * GJB; e += 256)
     P[e / GJB][e % GJB] = M[(long long)(kb + e / GJB) * np + kb + e % GJB];
-  __syncthreads();
-  pivot_inverse(P);
   const int j = c0 + (threadIdx.x & (PANEL_COLS - 1));
   const int t0 = (threadIdx.x >> 6) * 8;  // this thread's 8 pivot rows
+  const bool jcol = j < np && !(j >= kb && j < kb + GJB);
+  // every load of the panel issued before the pivot sweep (none depends on it):
+  // the column of M this thread transforms, and the old pivot columns of the
+  // chunk's rows (Ccol) -- their latency hides behind the 32 sweeps
+  double col[GJB];
+#pragma unroll
+  for (int q = 0; q < GJB; ++q) col[q] = jcol ? gj_sym(M, np, kb + q, j) : 0.0;
+  const int rows = min(PANEL_COLS, np - c0);
+  double cold[PANEL_COLS * GJB / 256];
+#pragma unroll
+  for (int u = 0; u < PANEL_COLS * GJB / 256; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    cold[u] = e < rows * GJB ? gj_sym(M, np, c0 + e / GJB, kb + e % GJB) : 0.0;
+  }
+  __syncthreads();
+  pivot_inverse(P);
   if (j < np) {
-    if (j >= kb && j < kb + GJB) {
+    if (!jcol) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) R[(long long)(t0 + t) * np + j] = P[t0 + t][j - kb];
     } else {
-      double col[GJB];
-#pragma unroll
-      for (int q = 0; q < GJB; ++q) col[q] = gj_sym(M, np, kb + q, j);
       double acc[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] = 0.0;
@@ -216,10 +227,10 @@ __global__ __launch_bounds__(256) void gj_panel_kernel(MatSet s, double* ws, int
   }
   // Ccol[i][t] = M[i][kb + t] for the rows i of this chunk (old values): t
   // fastest over consecutive threads, so reads and writes are coalesced
-  const int rows = min(PANEL_COLS, np - c0);
-  for (int e = threadIdx.x; e < rows * GJB; e += 256) {
-    const int i = c0 + e / GJB, t = e % GJB;
-    C[(long long)i * GJB + t] = gj_sym(M, np, i, kb + t);
+#pragma unroll
+  for (int u = 0; u < PANEL_COLS * GJB / 256; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    if (e < rows * GJB) C[(long long)(c0 + e / GJB) * GJB + e % GJB] = cold[u];
   }
 }
 
@@ -237,6 +248,25 @@ __global__ __launch_bounds__(256) void gj_update_kernel(MatSet s, double* ws, in
   double* M = ws + s.m_off[mi];
   const double* R = ws + s.row_off[mi];
   const double* C = ws + s.col_off[mi];
+  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
+  // the old value each of this thread's outputs starts from, loaded before the
+  // panel staging (pivot rows: Pinv M_kj from the row panel; other rows M_ij;
+  // pivot columns of other rows need none)
+  double old[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int i = i0 + ty + 16 * a;
+    const bool ipiv = i >= kb && i < kb + GJB;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int j = j0 + tx + 16 * b;
+      const bool jpiv = j >= kb && j < kb + GJB;
+      old[a][b] = (i >= np || j >= np) ? 0.0
+                  : ipiv               ? R[(long long)(i - kb) * np + j]
+                  : jpiv               ? 0.0
+                                       : M[(long long)i * np + j];
+    }
+  }
   __shared__ double Cs[64][GJB + 1];
   __shared__ double Rs[GJB][64 + 1];
   for (int e = threadIdx.x; e < 64 * GJB; e += 256) {
@@ -248,7 +278,6 @@ __global__ __launch_bounds__(256) void gj_update_kernel(MatSet s, double* ws, in
   __syncthreads();
   // 4x4 outputs per thread, register-blocked: per pivot column t, 4 values of
   // Ccol and 4 of Rrow' feed 16 FMAs
-  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
   double acc[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -278,9 +307,9 @@ __global__ __launch_bounds__(256) void gj_update_kernel(MatSet s, double* ws, in
       const bool jpiv = j >= kb && j < kb + GJB;
       double v;
       if (ipiv) {  // pivot rows: Pinv M_kj; the pivot block -Pinv
-        v = jpiv ? -R[(long long)(i - kb) * np + j] : R[(long long)(i - kb) * np + j];
+        v = jpiv ? -old[a][b] : old[a][b];
       } else {     // pivot columns: M_ik Pinv; the rest M_ij - M_ik Pinv M_kj
-        v = jpiv ? acc[a][b] : M[(long long)i * np + j] - acc[a][b];
+        v = jpiv ? acc[a][b] : old[a][b] - acc[a][b];
       }
       M[(long long)i * np + j] = v;
     }
