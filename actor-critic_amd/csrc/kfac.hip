@@ -141,28 +141,42 @@ __global__ void damp_kernel(DampSet d, const double* tr, double* ws) {
 
 // Gauss-Jordan (sweep) inverse of the GJB x GJB pivot block in LDS, all 256
 // threads: per sweep t every thread reads the pivot row / column entries of its
-// four elements, the block synchronises, and the four updated elements are
-// written back (two barriers per sweep; 4x fewer sequential steps than one wave
-// broadcasting the pivot column with readlane: 13 -> ~4 us per panel).
-__device__ void pivot_inverse(double (*P)[GJB + 1]) {
+// four elements from one LDS image and writes the four updated elements to the
+// other (ping-pong: one barrier per sweep; 32 sweeps end in P).  1/pivot from
+// v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient, a third
+// of the division sequence's latency).  The sweep was 12 of a panel launch's
+// 22 us with the division and two barriers per sweep.
+__device__ __forceinline__ double recip_f64(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+__device__ void pivot_inverse(double (*P)[GJB + 1], double (*Q)[GJB + 1]) {
   const int tid = threadIdx.x;
   const int c = tid & (GJB - 1), r0 = tid >> 5;  // rows r0, r0+8, r0+16, r0+24
-  for (int t = 0; t < GJB; ++t) {
-    const double ipiv = 1.0 / P[t][t];
-    const double ptc = P[t][c];
-    double v[4];
+  static_assert(GJB % 2 == 0, "an even number of sweeps ends in P");
+  for (int t = 0; t < GJB; t += 2) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = r0 + 8 * q;
-      const double prt = P[r][t];
-      const double prc = P[r][c];
-      if (r == t) v[q] = c == t ? ipiv : ptc * ipiv;
-      else v[q] = c == t ? -prt * ipiv : prc - prt * ptc * ipiv;
+    for (int h = 0; h < 2; ++h) {
+      double (*src)[GJB + 1] = h ? Q : P;
+      double (*dst)[GJB + 1] = h ? P : Q;
+      const int tt = t + h;
+      const double ipiv = recip_f64(src[tt][tt]);
+      const double ptc = src[tt][c];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = r0 + 8 * q;
+        const double prt = src[r][tt];
+        const double prc = src[r][c];
+        double v;
+        if (r == tt) v = c == tt ? ipiv : ptc * ipiv;
+        else v = c == tt ? -prt * ipiv : prc - prt * ptc * ipiv;
+        dst[r][c] = v;
+      }
+      __syncthreads();
     }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; ++q) P[r0 + 8 * q][c] = v[q];
-    __syncthreads();
   }
 }
 
@@ -189,6 +203,7 @@ __global__ __launch_bounds__(256) void gj_panel_kernel(MatSet s, double* ws, int
   double* R = ws + s.row_off[mi];
   double* C = ws + s.col_off[mi];
   __shared__ double P[GJB][GJB + 1];
+  __shared__ double Q[GJB][GJB + 1];
   for (int e = threadIdx.x; e < GJB * GJB; e += 256)
     P[e / GJB][e % GJB] = M[(long long)(kb + e / GJB) * np + kb + e % GJB];
   const int j = c0 + (threadIdx.x & (PANEL_COLS - 1));
@@ -208,7 +223,7 @@ __global__ __launch_bounds__(256) void gj_panel_kernel(MatSet s, double* ws, int
     cold[u] = e < rows * GJB ? gj_sym(M, np, c0 + e / GJB, kb + e % GJB) : 0.0;
   }
   __syncthreads();
-  pivot_inverse(P);
+  pivot_inverse(P, Q);
   if (j < np) {
     if (!jcol) {
 #pragma unroll
