@@ -14,4 +14,6 @@ run configs3_shard_acktr_512x20 || exit $?
 run configs2_acktr_32x20 --envs-per-gpu 32 --steps 50 --warmup 10 || exit $?
 run configs1_a2c_32x5 --algo a2c --envs-per-gpu 32 --steps 100 --warmup 10 || exit $?
 run configs4_shard_bf16_1024x20_a18 --forward bf16 --num-actions 18 --envs-per-gpu 1024 || exit $?
+run configs4_mixed_atari57_1024x20_a18_bf16 --forward bf16 --num-actions 18 --envs-per-gpu 1024 --games atari57 \
+  --cpu-iters 2 || exit $?
 exit 0
