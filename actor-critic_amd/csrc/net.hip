@@ -234,11 +234,14 @@ struct TailArgs {
   long long img_stride;
 };
 constexpr int kMaxHeads = 32;
+// sx [512], sl [kMaxHeads], s_action: the block's scratch in LDS; mirror
+// (nullable): the new stack also goes there (the fused next-step tower's image)
 template <int NZ>
-__global__ __launch_bounds__(256) void rollout_tail_kernel(
+__device__ __forceinline__ void rollout_tail_body(
     const float* part, int nz, const float* b4, float* a4, long long a4_stride, int B,
     const float* wpi, const float* bpi, const float* wv, const float* bv, int A, float* logits,
-    long long l_stride, float* value, long long v_stride, TailArgs ta) {
+    long long l_stride, float* value, long long v_stride, const TailArgs& ta, float* sx, float* sl,
+    int& s_action, uint4* mirror) {
   const int row = blockIdx.x;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   EnvPre pre;  // the env's state and current stack: in flight during the heads
@@ -254,9 +257,6 @@ __global__ __launch_bounds__(256) void rollout_tail_kernel(
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int e = 0; e < 8; ++e) hw[h][e] = head_w(min(wave + 4 * h, A), e);  // (unused past A)
-  __shared__ float sx[512];
-  __shared__ float sl[kMaxHeads];
-  __shared__ int s_action;
   float* x = a4 + (long long)row * a4_stride;
   if (NZ > 0) {
     // both columns' NZ slab loads issued before the (fixed-order) sums
@@ -314,7 +314,47 @@ __global__ __launch_bounds__(256) void rollout_tail_kernel(
   __syncthreads();
   env_step_block_pre(io.state, row, (uint32_t)(io.env_offset + row), io.env_seed, (uint32_t)s_action, pre,
                      io.obs_out + (long long)row * io.out_stride, io.rewards, io.terminals,
-                     io.episode_rewards, io.ld);
+                     io.episode_rewards, io.ld, mirror);
+}
+
+template <int NZ>
+__global__ __launch_bounds__(256) void rollout_tail_kernel(
+    const float* part, int nz, const float* b4, float* a4, long long a4_stride, int B,
+    const float* wpi, const float* bpi, const float* wv, const float* bv, int A, float* logits,
+    long long l_stride, float* value, long long v_stride, TailArgs ta) {
+  __shared__ float sx[512];
+  __shared__ float sl[kMaxHeads];
+  __shared__ int s_action;
+  rollout_tail_body<NZ>(part, nz, b4, a4, a4_stride, B, wpi, bpi, wv, bv, A, logits, l_stride, value, v_stride,
+                        ta, sx, sl, s_action, nullptr);
+}
+
+// The rollout tail of step t fused with the conv tower of step t + 1 (the
+// acmi_rollout_io_t next_acts contract): the env step leaves the new stack in
+// the tower's LDS image as well as in obs_out, the tower then runs on it --
+// one launch and one image round trip fewer per step, the same arithmetic.
+// The tail's scratch sits in the tower's a1 region (unused until conv1's
+// epilogue).  Two blocks per CU, like the tower.
+struct NextTower {
+  const float *b1, *b2, *b3;
+  float *a1, *a2, *a3;
+  long long st;
+  const char* prep;
+  uint32_t *m1, *m2, *m3;
+};
+template <int NZ, int C3, bool H16>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void rollout_tail_tower_kernel(
+    const float* part, int nz, const float* b4, float* a4, long long a4_stride, int B,
+    const float* wpi, const float* bpi, const float* wv, const float* bv, int A, float* logits,
+    long long l_stride, float* value, long long v_stride, TailArgs ta, NextTower nt) {
+  __shared__ __attribute__((aligned(16))) char lds[kTowLds + kTowScr];
+  float* sx = reinterpret_cast<float*>(lds + kTowObs);
+  int* s_action = reinterpret_cast<int*>(sx + 512 + kMaxHeads);
+  rollout_tail_body<NZ>(part, nz, b4, a4, a4_stride, B, wpi, bpi, wv, bv, A, logits, l_stride, value, v_stride,
+                        ta, sx, sx + 512, *s_action, reinterpret_cast<uint4*>(lds));
+  __syncthreads();  // the image in LDS; the tail's scratch free again
+  tower_body<C3, H16, true>(nullptr, 0, nt.b1, nt.b2, nt.b3, nt.a1, nt.a2, nt.a3, nt.st, nt.prep, nt.m1, nt.m2,
+                            nt.m3, lds, blockIdx.x);
 }
 
 inline int roundup4(int x) { return (x + 3) & ~3; }
@@ -415,12 +455,23 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   ACMI_REQUIRE(tower || g_forward_mode == ACMI_FWD_F32, ACMI_ERR_ARG,
                "16-bit forward needs the fused tower: net->conv_prep and 16-byte aligned observations / image "
                "stride");
+  // step fusion (acmi_rollout_io_t): this step's tower ran in the previous
+  // step's tail; the next step's tower runs in this step's tail
+  const bool tower_done = tail && tail->io.tower_done;
+  const acmi_acts_t* nxt = tail ? tail->io.next_acts : nullptr;
+  ACMI_REQUIRE(tower || (!tower_done && !nxt), ACMI_ERR_ARG,
+               "rollout step fusion needs the fused tower (x3 gemm mode, conv_prep, 16-byte aligned images)");
+  ACMI_REQUIRE(!nxt || (nxt->a1 && nxt->a2 && nxt->a3 && masks_ok(nxt) && tail->io.next_act_stride >= 1 &&
+                        (uintptr_t)tail->io.obs_out % 16 == 0 && tail->io.out_stride % 16 == 0),
+               ACMI_ERR_ARG, "acmi_rollout_step: bad next_acts / next_act_stride / obs_out alignment");
   if (tower) {
     // the three convs fused per image (16-byte image loads)
-    prof_begin(ACMI_PROF_CONV1_FWD, s);
-    launch_tower<C3>(obs, img_stride, B, P, L.off, a->a1, a->a2, a->a3, st, prep, s,
-                     g_forward_mode == ACMI_FWD_BF16, a->m1, a->m2, a->m3);
-    prof_end(ACMI_PROF_CONV1_FWD, s);
+    if (!tower_done) {
+      prof_begin(ACMI_PROF_CONV1_FWD, s);
+      launch_tower<C3>(obs, img_stride, B, P, L.off, a->a1, a->a2, a->a3, st, prep, s,
+                       g_forward_mode == ACMI_FWD_BF16, a->m1, a->m2, a->m3);
+      prof_end(ACMI_PROF_CONV1_FWD, s);
+    }
   } else {
   {  // conv1: [B,84,84,4]u8 -> [B,20,20,32]; the u8 patches stay bytes in LDS
     using Src = ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>;
@@ -488,8 +539,26 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   const dim3 hg(cdiv(B, 4)), hb(256);
   const float* hp = split ? a->ws : nullptr;
   float* hv = want_value ? a->value : nullptr;
+  NextTower ntw{};
+  if (nxt) ntw = NextTower{P + L.off[1], P + L.off[3], P + L.off[5], nxt->a1, nxt->a2, nxt->a3,
+                          tail->io.next_act_stride, static_cast<const char*>(prep), nxt->m1, nxt->m2, nxt->m3};
+  const bool h16 = g_forward_mode == ACMI_FWD_BF16;
+  // the fused tail + next tower at the rollout's split-K count; any other (or
+  // no) split runs the tail and then the next step's tower as two launches
+  const bool fuse_next = nxt && split && nz == 8;
 #define ACMI_HEADS(NZ)                                                                          \
-  if (tail)                                                                                     \
+  if (tail && fuse_next && NZ == 8) {                                                           \
+    if (h16)                                                                                    \
+      hipLaunchKernelGGL((rollout_tail_tower_kernel<8, C3, true>), dim3(B), hb, 0, s, hp, nz,    \
+                         P + L.off[7], a->a4, st * 512, B, P + L.off[8], P + L.off[9],          \
+                         P + L.off[10], P + L.off[11], L.A, a->logits, st * a->ld_logits, hv, st, \
+                         *tail, ntw);                                                           \
+    else                                                                                        \
+      hipLaunchKernelGGL((rollout_tail_tower_kernel<8, C3, false>), dim3(B), hb, 0, s, hp, nz,   \
+                         P + L.off[7], a->a4, st * 512, B, P + L.off[8], P + L.off[9],          \
+                         P + L.off[10], P + L.off[11], L.A, a->logits, st * a->ld_logits, hv, st, \
+                         *tail, ntw);                                                           \
+  } else if (tail)                                                                              \
     hipLaunchKernelGGL(rollout_tail_kernel<NZ>, dim3(B), hb, 0, s, hp, nz, P + L.off[7], a->a4,  \
                        st * 512, B, P + L.off[8], P + L.off[9], P + L.off[10], P + L.off[11],    \
                        L.A, a->logits, st * a->ld_logits, hv, st, *tail);                        \
@@ -517,6 +586,9 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
     default: ACMI_REQUIRE(false, ACMI_ERR_ARG, "fc4 split factor %d out of range", nz);
   }
 #undef ACMI_HEADS
+  if (nxt && !fuse_next)  // the next step's tower on the stacks the tail just wrote
+    launch_tower<C3>(tail->io.obs_out, tail->io.out_stride, B, P, L.off, nxt->a1, nxt->a2, nxt->a3,
+                     tail->io.next_act_stride, prep, s, h16, nxt->m1, nxt->m2, nxt->m3);
   ACMI_LAUNCH_CHECK("acmi_forward");
   return ACMI_OK;
 }

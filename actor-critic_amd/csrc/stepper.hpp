@@ -97,11 +97,13 @@ __device__ __forceinline__ void env_prefetch(acmi_env_state_t st, int n, const u
 // (the state of env n must have been read by every thread -- env_prefetch --
 // before this is called: it begins with the barrier that orders those reads
 // before thread 0's state writes)
+// mirror (nullable): the new stack is also stored there, 16-byte word g at
+// mirror[g] (the fused rollout tail hands it to the next step's conv tower in LDS)
 __device__ __forceinline__ void env_step_block_pre(acmi_env_state_t st, int n, uint32_t e, uint32_t seed,
                                                    uint32_t action, const EnvPre& pre,
                                                    uint8_t* obs_out, float* rewards,
                                                    uint8_t* terminals, float* ep_rewards,
-                                                   long long ld) {
+                                                   long long ld, uint4* mirror = nullptr) {
   const bool was_done = pre.was_done;
   int32_t k = pre.k;
   int32_t t = pre.t;
@@ -144,6 +146,7 @@ __device__ __forceinline__ void env_step_block_pre(acmi_env_state_t st, int n, u
     o.z = (term ? 0u : (old.z >> 8)) | (((f >> 16) & 255u) << 24);
     o.w = (term ? 0u : (old.w >> 8)) | ((f >> 24) << 24);
     out[g] = o;
+    if (mirror) mirror[g] = o;
   }
   if (threadIdx.x == 0) {
     total += rew;

@@ -215,24 +215,26 @@ struct TowB {
 // H16 (acmi_set_forward_mode ACMI_FWD_BF16): one f16 MFMA per product on the h
 // parts alone -- every operand rounded once to f16 after its power-of-two scale
 // (11-bit significands, u8 pixels exact; a bf16 forward's precision or better).
-template <int C3, bool H16 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, const float* b2,
-                  const float* b3, float* a1g, float* a2g, float* a3g, long long st, const char* prep,
-                  uint32_t* m1g, uint32_t* m2g, uint32_t* m3g) {
+// The tower of image `img` by one 256-thread block over the caller's LDS
+// (kTowLds + kTowScr bytes).  IMG_IN_LDS: the u8 image is already in the
+// image region (written there by the fused rollout tail's env step, which
+// also stored it to obs) and is not loaded again.
+template <int C3, bool H16, bool IMG_IN_LDS>
+__device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_stride, const float* b1,
+                                           const float* b2, const float* b3, float* a1g, float* a2g, float* a3g,
+                                           long long st, const char* prep, uint32_t* m1g, uint32_t* m2g,
+                                           uint32_t* m3g, char* lds, long long img) {
   using P = TowerPrep<C3>;
   const unsigned* hdr = reinterpret_cast<const unsigned*>(prep + P::HDR);
   const float sw1 = f16x2_scale_of_bits(hdr + kTowMaxW1), sw2 = f16x2_scale_of_bits(hdr + kTowMaxW2);
   const float sw3 = f16x2_scale_of_bits(hdr + kTowMaxW3), sa1 = f16x2_scale_of_bits(hdr + kTowMaxA1);
   const float sa2 = f16x2_scale_of_bits(hdr + kTowMaxA2);
-  __shared__ __attribute__((aligned(16))) char lds[kTowLds + kTowScr];
   char* const imgL = lds;           // u8 image; later a2
   char* const a1L = lds + kTowObs;  // a1; later conv3 scratch
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kh8 = lane >> 5;
-  const long long img = blockIdx.x;
 
-  {  // the u8 image: all of a thread's 16-byte loads before its LDS stores
+  if constexpr (!IMG_IN_LDS) {  // the u8 image: all of a thread's 16-byte loads before its LDS stores
     constexpr int N16 = kTowObs / 16, NPT = (N16 + 255) / 256;
     const uint4* src = reinterpret_cast<const uint4*>(obs + img * img_stride);
     uint4 v[NPT];
@@ -249,7 +251,7 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
     // 384-399) by K halves on waves 2 (k-steps 0-7) and 3 (8-15), added through
     // LDS.  Odd blocks rotate the roles by two, so the two blocks of a CU give
     // every SIMD the same conv1 load: 3 + 3.5 tiles.
-    const int w = (wave + 2 * (blockIdx.x & 1)) & 3;
+    const int w = (wave + 2 * (int)(img & 1)) & 3;
     auto tile_of = [&](int u) { return u < 3 ? w + 4 * u : 12; };
     int abase[4];
 #pragma unroll
@@ -456,6 +458,16 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
       }
     }
   }
+}
+
+template <int C3, bool H16 = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, const float* b2,
+                  const float* b3, float* a1g, float* a2g, float* a3g, long long st, const char* prep,
+                  uint32_t* m1g, uint32_t* m2g, uint32_t* m3g) {
+  __shared__ __attribute__((aligned(16))) char lds[kTowLds + kTowScr];
+  tower_body<C3, H16, false>(obs, img_stride, b1, b2, b3, a1g, a2g, a3g, st, prep, m1g, m2g, m3g, lds,
+                             blockIdx.x);
 }
 
 // prep: acmi_conv_prepare's fragments + bounds (required)

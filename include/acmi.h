@@ -494,6 +494,16 @@ typedef struct acmi_rollout_io {
   uint8_t* terminals;
   float* episode_rewards;
   int64_t ld;
+  /* Step fusion (zero / NULL: off).  next_acts: after its env step, each
+   * env's workgroup runs the NEXT step's conv tower on the stack it just
+   * wrote (obs_out, image stride out_stride), from LDS, into next_acts'
+   * a1..a3 / m1..m3 rows (image stride next_act_stride) -- the tower launch
+   * of the next step is then skipped by passing tower_done = 1 with it.
+   * Needs the fused tower (x3 gemm mode, prepared weights, 16-byte aligned
+   * obs_out / out_stride).  Bit-identical to the unfused steps. */
+  int tower_done;
+  const struct acmi_acts* next_acts;
+  int64_t next_act_stride;
 } acmi_rollout_io_t;
 int acmi_rollout_step(const acmi_net_t* net, const uint8_t* obs,
                       int64_t img_stride, int B, const acmi_acts_t* acts,

@@ -193,22 +193,26 @@ def test_two_stream_rollout_is_bit_identical(lib, cuda, monkeypatch):
     in a row (the later ones start mid-episode from auto-reset states)."""
     from actorcritic import session as sess
     outs = []
-    for split, graph, fused in (('0', '0', '0'), ('0', '0', '1'), ('1', '0', '0'), ('1', '0', '1'),
-                                ('1', '1', '1'), ('0', '1', '1')):
+    # (split, graph, fused tail, step fusion: step t's tail runs step t+1's tower)
+    for split, graph, fused, fsteps in (('0', '0', '0', '0'), ('0', '0', '1', '0'), ('0', '0', '1', '1'),
+                                        ('1', '0', '0', '0'), ('1', '0', '1', '1'), ('1', '1', '1', '1'),
+                                        ('0', '1', '1', '1')):
         monkeypatch.setenv('ACMI_ROLLOUT_SPLIT', split)
         monkeypatch.setenv('ACMI_ROLLOUT_GRAPH', graph)
         monkeypatch.setenv('ACMI_ROLLOUT_FUSED', fused)
+        monkeypatch.setenv('ACMI_ROLLOUT_FUSE_STEPS', fsteps)
         env, model, agent, obj, gs, opt, op = _bench_like()
         got = []
         with sess.Session() as s:
             for _ in range(3):
                 obs, act, rew, term, nxt, info = agent.interact(s)
                 acts = agent._bufs.acts
-                got += [x.clone() for x in (obs, act, rew, term, nxt, info.episode_rewards, acts.a1, acts.a4,
-                                            acts.logits, acts.value)]
+                got += [x.clone() for x in (obs, act, rew, term, nxt, info.episode_rewards, acts.a1, acts.a2,
+                                            acts.a3, acts.a4, acts.m1, acts.m2, acts.m3, acts.logits, acts.value)]
         torch.cuda.synchronize()
         assert agent._bufs.halves == (split == '1')
         assert (agent._bufs.graph is not None) == (graph == '1')
+        assert agent._bufs.fuse_steps == (fused == '1' and fsteps == '1')
         outs.append(got)
     for other in outs[1:]:
         for i, (a, b) in enumerate(zip(outs[0], other)):
