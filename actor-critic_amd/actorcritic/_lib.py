@@ -157,7 +157,7 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.acmi_abi_version() != 2:
+        if lib.acmi_abi_version() != 3:
             raise ImportError('libacmi ABI mismatch')
         _lib = lib
     return _lib

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define ACMI_ABI_VERSION 2
+#define ACMI_ABI_VERSION 3  /* 3: acmi_env_state_t.game, acmi_rollout_io_t step fusion fields */
 
 enum {
   ACMI_OK = 0,
