@@ -86,10 +86,8 @@ class _RolloutBuffers(object):
         self.use_graph = os.environ.get('ACMI_ROLLOUT_GRAPH', '0') == '1'
         self.fused = os.environ.get('ACMI_ROLLOUT_FUSED', '1') != '0'
         # step fusion: step t's tail also runs step t+1's conv tower (needs the
-        # fused tower: x3 gemm mode and prepared weights)
-        lib = _lib.load()
-        self.fuse_steps = (self.fused and os.environ.get('ACMI_ROLLOUT_FUSE_STEPS', '1') != '0' and
-                           lib.acmi_get_gemm_mode() == _lib.GEMM_X3)
+        # fused tower: x3 gemm mode, checked per step, and prepared weights)
+        self.fuse_steps = self.fused and os.environ.get('ACMI_ROLLOUT_FUSE_STEPS', '1') != '0'
         self.graph, self.graph_key, self.warm = None, None, False
         self.ctr_dev = torch.zeros(1, dtype=torch.int32, device=dev)
 
@@ -266,7 +264,7 @@ def _half_step(eng, env, rb, h, N2, T, A, t, seed, dev_ctr=False):
     if rb.fused:  # tower + fused heads/sample/env-step tail (acmi_rollout_step)
         # step fusion: step t's tower ran in step t-1's tail; step t's tail runs
         # step t+1's tower (not the last step's: the bootstrap forward is the update's)
-        fuse = rb.fuse_steps
+        fuse = rb.fuse_steps and eng.lib.acmi_get_gemm_mode() == _lib.GEMM_X3  # fixed within a rollout
         nxt = rb.acts.view(row + 1, T, ws_rows=N2) if fuse and t + 1 < T else None
         io = _lib.RolloutIO(seed, 0, ctr, ctr_dev, row0, act_t, eng._bad_rows.data_ptr(), env.range_state(n0),
                             env.env_offset + n0, env.seed, dst, dstride, rew, term, ep, T,

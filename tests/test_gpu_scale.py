@@ -212,7 +212,7 @@ def test_two_stream_rollout_is_bit_identical(lib, cuda, monkeypatch):
         torch.cuda.synchronize()
         assert agent._bufs.halves == (split == '1')
         assert (agent._bufs.graph is not None) == (graph == '1')
-        assert agent._bufs.fuse_steps == (fused == '1' and fsteps == '1')
+        assert agent._bufs.fuse_steps == (fused == '1' and fsteps == '1')  # (x3 gemm mode: the default)
         outs.append(got)
     for other in outs[1:]:
         for i, (a, b) in enumerate(zip(outs[0], other)):
