@@ -50,7 +50,7 @@ class RolloutIO(ctypes.Structure):
                 ('row_offset', c_int), ('actions', c_vp), ('bad_rows', c_vp), ('state', EnvState),
                 ('env_offset', c_int), ('env_seed', c_u32), ('obs_out', c_vp), ('out_stride', c_i64),
                 ('rewards', c_vp), ('terminals', c_vp), ('episode_rewards', c_vp), ('ld', c_i64),
-                ('tower_done', c_int), ('next_acts', c_vp), ('next_act_stride', c_i64)]
+                ('tower_done', c_int), ('next_acts', c_vp), ('next_act_stride', c_i64), ('obs_copy', c_vp)]
 
 
 # name -> (restype, argtypes)

@@ -143,7 +143,8 @@ class MultiEnvAgent(Agent):
         """The T-step rollout as one chain (rb.halves False) or as the two env halves'
         chains on the current stream and rb.side."""
         main = torch.cuda.current_stream(eng.device)
-        rb.obs[:, 0].copy_(rb.next_obs)
+        if not rb.fused:  # (the fused step 0 reads next_obs in place and files it into obs[:, 0])
+            rb.obs[:, 0].copy_(rb.next_obs)
         if rb.halves:
             rb.side.wait_stream(main)
         N2 = N // 2 if rb.halves else N
@@ -266,10 +267,14 @@ def _half_step(eng, env, rb, h, N2, T, A, t, seed, dev_ctr=False):
         # step t+1's tower (not the last step's: the bootstrap forward is the update's)
         fuse = rb.fuse_steps and eng.lib.acmi_get_gemm_mode() == _lib.GEMM_X3  # fixed within a rollout
         nxt = rb.acts.view(row + 1, T, ws_rows=N2) if fuse and t + 1 < T else None
+        # step 0 reads the previous rollout's final stacks (next_obs) in place and
+        # copies them into obs[:, 0] (the batch's step-0 rows) as it goes
+        src_t, sstride = (rb.next_obs.data_ptr() + n0 * OBS_BYTES, OBS_BYTES) if t == 0 else (src, T * OBS_BYTES)
         io = _lib.RolloutIO(seed, 0, ctr, ctr_dev, row0, act_t, eng._bad_rows.data_ptr(), env.range_state(n0),
                             env.env_offset + n0, env.seed, dst, dstride, rew, term, ep, T,
-                            1 if fuse and t > 0 else 0, ctypes.addressof(nxt) if nxt is not None else None, T)
-        _lib.call('acmi_rollout_step', ctypes.byref(eng.net()), ctypes.c_void_p(src), T * OBS_BYTES, N2,
+                            1 if fuse and t > 0 else 0, ctypes.addressof(nxt) if nxt is not None else None, T,
+                            src if t == 0 else None)
+        _lib.call('acmi_rollout_step', ctypes.byref(eng.net()), ctypes.c_void_p(src_t), sstride, N2,
                   ctypes.byref(acts), T, ctypes.byref(io), eng.stream())
         return
     eng.forward(src, N2, acts, want_value=True, img_stride=T * OBS_BYTES, act_stride=T)

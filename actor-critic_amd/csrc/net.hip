@@ -246,6 +246,14 @@ __device__ __forceinline__ void rollout_tail_body(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   EnvPre pre;  // the env's state and current stack: in flight during the heads
   env_prefetch(ta.io.state, row, ta.obs + (long long)row * ta.img_stride, pre);
+  if (ta.io.obs_copy) {  // the stacks this step read, filed where the batch keeps them
+    uint4* cp = reinterpret_cast<uint4*>(ta.io.obs_copy + (long long)row * ta.io.out_stride);
+#pragma unroll
+    for (int i = 0; i < kEnvWords; ++i) {
+      const int g = threadIdx.x + kEnvThreads * i;
+      if (g < FRAME_WORDS) cp[g] = pre.old[i];
+    }
+  }
   // head a's weight for a4 element lane + 64 e (a == A: the value head); the
   // wave's first two heads are loaded now, beside the slab and stack loads
   auto head_w = [&](int a, int e) {
@@ -461,6 +469,8 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   const acmi_acts_t* nxt = tail ? tail->io.next_acts : nullptr;
   ACMI_REQUIRE(tower || (!tower_done && !nxt), ACMI_ERR_ARG,
                "rollout step fusion needs the fused tower (x3 gemm mode, conv_prep, 16-byte aligned images)");
+  ACMI_REQUIRE(!tail || !tail->io.obs_copy || ((uintptr_t)tail->io.obs_copy % 16 == 0 && tail->io.out_stride % 16 == 0),
+               ACMI_ERR_ARG, "acmi_rollout_step: obs_copy must be 16-byte aligned");
   ACMI_REQUIRE(!nxt || (nxt->a1 && nxt->a2 && nxt->a3 && masks_ok(nxt) && tail->io.next_act_stride >= 1 &&
                         (uintptr_t)tail->io.obs_out % 16 == 0 && tail->io.out_stride % 16 == 0),
                ACMI_ERR_ARG, "acmi_rollout_step: bad next_acts / next_act_stride / obs_out alignment");

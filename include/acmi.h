@@ -504,6 +504,10 @@ typedef struct acmi_rollout_io {
   int tower_done;
   const struct acmi_acts* next_acts;
   int64_t next_act_stride;
+  /* nullable: the stacks this step reads (obs) are also copied to
+   * obs_copy + b*out_stride (step 0 reads the previous rollout's final
+   * stacks in place and files them into the batch's step-0 rows) */
+  uint8_t* obs_copy;
 } acmi_rollout_io_t;
 int acmi_rollout_step(const acmi_net_t* net, const uint8_t* obs,
                       int64_t img_stride, int B, const acmi_acts_t* acts,
