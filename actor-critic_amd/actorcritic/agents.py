@@ -157,7 +157,8 @@ class MultiEnvAgent(Agent):
                 eng.sample_counter += 1
         if rb.halves:
             main.wait_stream(rb.side)
-        rb.actions.copy_(rb.actions_tn.t())
+        if not rb.fused:  # (the fused tail writes actions [N, T] itself)
+            rb.actions.copy_(rb.actions_tn.t())
 
     def _rollout_graph(self, eng, env, rb, N, T, A, seed):
         """The two-chain rollout as one hipGraph (torch.cuda.CUDAGraph over the
@@ -270,7 +271,9 @@ def _half_step(eng, env, rb, h, N2, T, A, t, seed, dev_ctr=False):
         # step 0 reads the previous rollout's final stacks (next_obs) in place and
         # copies them into obs[:, 0] (the batch's step-0 rows) as it goes
         src_t, sstride = (rb.next_obs.data_ptr() + n0 * OBS_BYTES, OBS_BYTES) if t == 0 else (src, T * OBS_BYTES)
-        io = _lib.RolloutIO(seed, 0, ctr, ctr_dev, row0, act_t, eng._bad_rows.data_ptr(), env.range_state(n0),
+        # actions straight into the [N, T] batch (element b at [b*T], like the rewards)
+        act_nt = rb.actions.data_ptr() + 4 * row
+        io = _lib.RolloutIO(seed, 0, ctr, ctr_dev, row0, act_nt, eng._bad_rows.data_ptr(), env.range_state(n0),
                             env.env_offset + n0, env.seed, dst, dstride, rew, term, ep, T,
                             1 if fuse and t > 0 else 0, ctypes.addressof(nxt) if nxt is not None else None, T,
                             src if t == 0 else None)

@@ -316,7 +316,7 @@ __device__ __forceinline__ void rollout_tail_body(
     const int y = sample_row(sl, A, io.seed, io.stream_id, ctr, (uint32_t)(row + io.row_offset),
                              nullptr, 0, &bad);
     if (bad) atomicAdd(io.bad_rows, 1);
-    io.actions[row] = y;
+    io.actions[(long long)row * io.ld] = y;
     s_action = y;
   }
   __syncthreads();

@@ -483,7 +483,7 @@ typedef struct acmi_rollout_io {
   uint32_t seed, stream_id, counter; /* sampler RNG key                      */
   const uint32_t* counter_dev;       /* nullable: counter += *counter_dev     */
   int row_offset;                    /* global row of batch row 0            */
-  int32_t* actions;                  /* [B] out                              */
+  int32_t* actions;                  /* out, element b at [b*ld] (ld below)  */
   int32_t* bad_rows;                 /* device counter of non-finite rows    */
   acmi_env_state_t state;            /* env state of batch row 0's env       */
   int env_offset;                    /* global env id of batch row 0         */
