@@ -57,6 +57,7 @@ class RolloutIO(ctypes.Structure):
 _SIGS = {
     'acmi_last_error': (ctypes.c_char_p, []),
     'acmi_abi_version': (c_int, []),
+    'acmi_abi_struct_sizes': (c_int, [c_vp, c_int]),
     'acmi_set_forward_mode': (c_int, [c_int]),
     'acmi_get_forward_mode': (c_int, []),
     'acmi_set_gemm_mode': (c_int, [c_int]),

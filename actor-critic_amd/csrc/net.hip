@@ -1376,6 +1376,14 @@ extern "C" {
 
 const char* acmi_last_error(void) { return g_err; }
 int acmi_abi_version(void) { return ACMI_ABI_VERSION; }
+int acmi_abi_struct_sizes(int64_t* sizes, int n) {
+  const int64_t all[5] = {(int64_t)sizeof(acmi_net_t), (int64_t)sizeof(acmi_acts_t), (int64_t)sizeof(acmi_bwd_t),
+                          (int64_t)sizeof(acmi_env_state_t), (int64_t)sizeof(acmi_rollout_io_t)};
+  if (!sizes || n < 0) return 0;
+  const int k = n < 5 ? n : 5;
+  for (int i = 0; i < k; ++i) sizes[i] = all[i];
+  return k;
+}
 
 int acmi_set_gemm_mode(int mode) {
   ACMI_REQUIRE(mode == ACMI_GEMM_F32 || mode == ACMI_GEMM_X3, ACMI_ERR_ARG,

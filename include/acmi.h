@@ -35,6 +35,10 @@ typedef void* acmi_stream_t; /* hipStream_t */
 
 const char* acmi_last_error(void);
 int acmi_abi_version(void);
+/* Host-only: sizeof of the ABI structs, in the order acmi_net_t, acmi_acts_t,
+ * acmi_bwd_t, acmi_env_state_t, acmi_rollout_io_t (n <= 5 written), so a
+ * binding can check its struct mirrors (returns the number written). */
+int acmi_abi_struct_sizes(int64_t* sizes, int n);
 
 /* Arithmetic of the fused weight-gradient + K-FAC A-factor reductions (conv2,
  * conv3, heads; the dominant K-FAC covariance work, kfac cov_update_thunks,

@@ -31,6 +31,17 @@ def test_library_exports_every_declared_symbol(lib):
     assert lib.acmi_abi_version() == 3
 
 
+def test_ctypes_struct_mirrors_match_the_c_abi(lib):
+    """The Python binding's ctypes mirrors have the C structs' sizes (a field added
+    on one side only -- e.g. acmi_rollout_io_t's step-fusion fields -- would shift
+    every later field the kernels read)."""
+    from actorcritic import _lib
+    sizes = (ctypes.c_int64 * 5)()
+    assert lib.acmi_abi_struct_sizes(ctypes.cast(sizes, ctypes.c_void_p), 5) == 5
+    mirrors = (_lib.Net, _lib.Acts, _lib.Bwd, _lib.EnvState, _lib.RolloutIO)
+    assert [ctypes.sizeof(m) for m in mirrors] == list(sizes)
+
+
 def test_gemm_launch_plans_cover_every_tile(lib):
     # host-only planner check inside libacmi: slab groups of the fused
     # wgrad/A-factor reduction (symred.hpp) and split-K chunking
