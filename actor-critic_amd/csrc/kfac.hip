@@ -481,6 +481,19 @@ __global__ void kcoeff_kernel(const float* part, int nb, float lr, float c, floa
   }
 }
 
+// y[i][j] = sum_k A[i][k] g[k][j] for the narrow (dout % 4 != 0) first
+// products of the K-FAC step: block (i, j), one wave over k (fixed order:
+// lane-strided partial sums, then the butterfly)
+__global__ __launch_bounds__(64) void kfac_narrow_kernel(const float* a, int lda, const float* g, int dout, int n,
+                                                       float* y, int ldy) {
+  const int i = blockIdx.x, j = blockIdx.y;
+  const float* ar = a + (long long)i * lda;
+  float s = 0.f;
+  for (int k = threadIdx.x; k < n; k += 64) s += ar[k] * g[(long long)k * dout + j];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) y[(long long)i * ldy + j] = s;
+}
+
 __global__ void kapply_kernel(float* p, float* v, const float* d, long long n, float lr,
                               float mom, const float* coeff) {
   const float cf = coeff[0];
@@ -838,9 +851,9 @@ int acmi_kfac_step(int A, int C3, float* params, float* velocity, const float* g
       g1.e[q] = EpiStore{t1, ldg};
       g1.I[q] = din, g1.J[q] = dout, g1.K[q] = din;
     } else {
-      launch_gemm<128, 32, 32, 1, 1, false, false>(MatI<true>{ainv, lda, din, din},
-                                                   MatI<false>{g, dout, din, dout}, EpiStore{t1, ldg},
-                                                   din, dout, din, 1, 0, s);
+      // (a GEMM launch of 128 x 32 tiles for these few columns was 19.6 us at
+      // dout = 1: one wave per output instead)
+      hipLaunchKernelGGL(kfac_narrow_kernel, dim3(din, dout), dim3(64), 0, s, ainv, lda, g, dout, din, t1, ldg);
     }
     const int q = g2.n++;
     g2.a[q] = MatTK<true>{t1, ldg, dout, din};
