@@ -197,6 +197,7 @@ class NetEngine(object):
         self._bad_rows = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._prep, self._prep_version = None, None
         self.sample_counter = 0
+        self._comm = None  # comm_timing: [(start event, end event, bytes)] per update
 
     # -- update plumbing -------------------------------------------------------
     def update_state(self, M):
@@ -310,12 +311,14 @@ class NetEngine(object):
         from actorcritic import parallel
         st.loss_reduced = True
         if not with_stats:
+            st.comm_bytes = 4 * st.n_grad_red
             return parallel.allreduce_sum_async(st.red[:st.n_grad_red])
         pk, ng, L = self._packed(st), st.n_grad_red, self.layout
         pk[:ng].copy_(st.red[:ng])
         _lib.call('acmi_kfac_pack', L.A, L.C3, 1, ctypes.c_void_p(st.stats.data_ptr()),
                   ctypes.c_void_p(pk[ng:].data_ptr()), self.stream())
         st.pk_active = True
+        st.comm_bytes = 4 * (ng + st.pk_na + st.pk_ng)
         return parallel.allreduce_sum_async(pk[:ng + st.pk_na])
 
     def allreduce_end(self, st, with_stats, pending):
@@ -325,18 +328,43 @@ class NetEngine(object):
         if self.world_size <= 1:
             return
         from actorcritic import parallel
+        marks = self._comm_mark() if self._comm is not None else None
         if not st.pk_active:
             pending.wait()
-            return
-        pk, ng, L = st.pk, st.n_grad_red, self.layout
-        _lib.call('acmi_kfac_pack', L.A, L.C3, 2, ctypes.c_void_p(st.stats.data_ptr()),
-                  ctypes.c_void_p(pk[ng + st.pk_na:].data_ptr()), self.stream())
-        parallel.allreduce_sum_(pk[ng + st.pk_na:])
-        pending.wait()
-        st.red[:ng].copy_(pk[:ng])
-        _lib.call('acmi_kfac_unpack', L.A, L.C3, 3, ctypes.c_void_p(pk[ng:].data_ptr()),
-                  ctypes.c_void_p(st.stats.data_ptr()), self.stream())
-        st.pk_active = False
+        else:
+            pk, ng, L = st.pk, st.n_grad_red, self.layout
+            _lib.call('acmi_kfac_pack', L.A, L.C3, 2, ctypes.c_void_p(st.stats.data_ptr()),
+                      ctypes.c_void_p(pk[ng + st.pk_na:].data_ptr()), self.stream())
+            parallel.allreduce_sum_(pk[ng + st.pk_na:])
+            pending.wait()
+            st.red[:ng].copy_(pk[:ng])
+            _lib.call('acmi_kfac_unpack', L.A, L.C3, 3, ctypes.c_void_p(pk[ng:].data_ptr()),
+                      ctypes.c_void_p(st.stats.data_ptr()), self.stream())
+            st.pk_active = False
+        if marks is not None:
+            marks[1].record()
+            self._comm.append((marks[0], marks[1], st.comm_bytes))
+
+    # -- communication timing (bench.py allreduce_ms) ----------------------------
+    def comm_timing(self, on):
+        """Records HIP events on the compute stream around allreduce_end -- from the end
+        of the sampled-loss backward to the reduced buffer being ready (G-tail pack and
+        sum, the wait for the asynchronous prefix sum, unpack): the time the update's
+        compute stream stands still on the exchange step, skew between ranks included."""
+        self._comm = [] if on else None
+
+    def _comm_mark(self):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return e0, e1
+
+    def comm_collect(self):
+        """(mean ms per update, bytes all-reduced per update, updates seen) of the
+        exchanges recorded since comm_timing(True); call after a synchronize."""
+        if not self._comm:
+            return 0.0, 0, 0
+        ms = [a.elapsed_time(b) for a, b, _ in self._comm]
+        return sum(ms) / len(ms), self._comm[-1][2], len(ms)
 
     # -- plumbing ------------------------------------------------------------
     def net(self):

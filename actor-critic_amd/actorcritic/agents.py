@@ -86,7 +86,7 @@ class _RolloutBuffers(object):
         self.use_graph = os.environ.get('ACMI_ROLLOUT_GRAPH', '0') == '1'
         self.fused = os.environ.get('ACMI_ROLLOUT_FUSED', '1') != '0'
         # step fusion: step t's tail also runs step t+1's conv tower (needs the
-        # fused tower: x3 gemm mode, checked per step, and prepared weights)
+        # fused tower: x3 gemm mode, checked once per rollout, and prepared weights)
         self.fuse_steps = self.fused and os.environ.get('ACMI_ROLLOUT_FUSE_STEPS', '1') != '0'
         self.graph, self.graph_key, self.warm = None, None, False
         self.ctr_dev = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -148,11 +148,14 @@ class MultiEnvAgent(Agent):
         if rb.halves:
             rb.side.wait_stream(main)
         N2 = N // 2 if rb.halves else N
+        # step fusion is decided once per rollout: a gemm mode switched mid-rollout must
+        # not let step t skip a tower that step t-1's tail never ran
+        fuse = bool(rb.fused and rb.fuse_steps and eng.lib.acmi_get_gemm_mode() == _lib.GEMM_X3)
         for t in range(T):
-            _half_step(eng, env, rb, 0, N2, T, A, t, seed, dev_ctr)
+            _half_step(eng, env, rb, 0, N2, T, A, t, seed, dev_ctr, fuse)
             if rb.halves:
                 with torch.cuda.stream(rb.side):
-                    _half_step(eng, env, rb, 1, N2, T, A, t, seed, dev_ctr)
+                    _half_step(eng, env, rb, 1, N2, T, A, t, seed, dev_ctr, fuse)
             if not dev_ctr:
                 eng.sample_counter += 1
         if rb.halves:
@@ -167,7 +170,11 @@ class MultiEnvAgent(Agent):
         that differs between rollouts lives in device memory (observations, env
         states, parameters updated in place); the RNG counter is refreshed in
         rb.ctr_dev before each replay."""
-        key = (eng.params.data_ptr(), id(env), seed, eng.rank)
+        # everything the captured launches bake in: buffers, env, seed, rank, and the
+        # arithmetic modes / step fusion that chose the captured kernels
+        lib = eng.lib
+        key = (eng.params.data_ptr(), id(env), seed, eng.rank, int(lib.acmi_get_gemm_mode()),
+               int(lib.acmi_get_forward_mode()), bool(rb.fuse_steps))
         if rb.graph is None or rb.graph_key != key:
             if not rb.warm:  # first rollout eager: loads the code objects, sizes workspaces
                 rb.warm = True
@@ -238,10 +245,11 @@ class MultiEnvAgent(Agent):
         return out[:5] + (EpisodeInfoBatch(out[5]),)
 
 
-def _half_step(eng, env, rb, h, N2, T, A, t, seed, dev_ctr=False):
+def _half_step(eng, env, rb, h, N2, T, A, t, seed, dev_ctr=False, fuse=False):
     """Rollout step t of env half h (envs h*N2 .. h*N2+N2-1) on the current stream.
     dev_ctr: the sampler's RNG counter is rb.ctr_dev + t (graph capture) instead of
-    the host eng.sample_counter."""
+    the host eng.sample_counter.  fuse: step fusion for the whole rollout (decided
+    once by the caller, so tower_done at step t means step t-1 passed next_acts)."""
     n0 = h * N2
     row = n0 * T + t
     obs0 = rb.obs.data_ptr()
@@ -266,7 +274,6 @@ def _half_step(eng, env, rb, h, N2, T, A, t, seed, dev_ctr=False):
     if rb.fused:  # tower + fused heads/sample/env-step tail (acmi_rollout_step)
         # step fusion: step t's tower ran in step t-1's tail; step t's tail runs
         # step t+1's tower (not the last step's: the bootstrap forward is the update's)
-        fuse = rb.fuse_steps and eng.lib.acmi_get_gemm_mode() == _lib.GEMM_X3  # fixed within a rollout
         nxt = rb.acts.view(row + 1, T, ws_rows=N2) if fuse and t + 1 < T else None
         # step 0 reads the previous rollout's final stacks (next_obs) in place and
         # copies them into obs[:, 0] (the batch's step-0 rows) as it goes

@@ -27,6 +27,11 @@ def rank():
     return dist.get_rank() if is_initialized() else 0
 
 
+def backend_name():
+    """'nccl' (= RCCL on ROCm), 'gloo', or None on one process."""
+    return dist.get_backend() if is_initialized() else None
+
+
 def local_rank():
     return int(os.environ.get('LOCAL_RANK', '0'))
 

@@ -206,6 +206,9 @@ __global__ __launch_bounds__(256) void band_bounds_kernel(const float* w1, const
 #define ACMI_BAND_DEPTH 2
 #endif
 constexpr int kBandDepth = ACMI_BAND_DEPTH;  // stages of loads in flight (register sets)
+#ifndef ACMI_BAND_PIPE  // 1: fragment reads one sub-tile ahead of the MFMAs (see the loop); 0: plain order
+#define ACMI_BAND_PIPE 1
+#endif
 #ifndef ACMI_BAND_PROBE  // timing probes (wrong results): 1 no split, 2 no column sums, 4 no loads,
                          // 8 no LDS stores, 16 no MFMAs, 32 no LDS fragment reads
 #define ACMI_BAND_PROBE 0
@@ -295,15 +298,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
 #pragma unroll
       for (int u = 0; u < 2; ++u) foff[u] += (uint32_t)kBandRows * cld[u];
     };
-    auto commit = [&](int buf, auto S) {
+    // one staged float4 (row 2 rp + r, run u) of register set `set` into LDS buffer buf
+    auto commit1 = [&](int buf, auto S, int r, int u) {
       constexpr int set = decltype(S)::value;
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
+      {
         const int krow = 2 * rp + r;
         char* s = lds + buf * kBandBuf + krow * kBandRowBytes;
         const int q8 = 8 * (krow & 3);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        {
           const float4 v = ra[set][2 * r + u];
           if constexpr (!(ACMI_BAND_PROBE & 2)) {
             csum[4 * u] += v.x;
@@ -329,6 +331,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
           }
         }
       }
+    };
+    auto commit = [&](int buf, auto S) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) commit1(buf, S, r, u);
     };
 
     auto slot_off = [&](int colblock) {
@@ -361,6 +369,121 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
           for (int r = 0; r < 16; ++r) acc[t][a][b][r] = 0.f;
 
     using S0 = std::integral_constant<int, 0>;
+#if ACMI_BAND_PIPE
+    // Software-pipelined fragment reads.  Each wave's sub-tiles of stage kt are
+    // read from LDS one sub-tile AHEAD of their MFMAs, and the last sub-tile of a
+    // stage is multiplied after the barrier, while the next stage's first
+    // fragments are in flight:
+    //   barrier(kt-1) | read (kt,0) | mma (kt-1,last) + commit of stage kt+1
+    //   (VALU split and LDS stores interleaved with those MFMAs) | fetch kt+2 |
+    //   read (kt,1) | mma (kt,0) | barrier(kt) | read (kt+1,0) | ...
+    // so no MFMA block waits for a burst of LDS reads issued right before it (in
+    // the plain order every wave of the CU reads at the same time after each
+    // barrier and the matrix pipes idle until the fragments return).  Fragment
+    // sets: F[t] for tile t when a wave has two sub-tiles; by stage parity when
+    // it has one.  Stages past the chunk end stage zeros (masked loads), so the
+    // commit is unconditional and the trailing read is harmless.
+    struct Frag {
+      f16x8 a[2][2], b[2][2];  // [32-column block][part h, l]
+    };
+    Frag F[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) F[f].a[x][y] = F[f].b[x][y] = f16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    auto fread = [&](const char* s, int t, Frag& f) {
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) {
+        const char* sp = s + pt * kBandPart;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          f.a[cb][pt] = cat8h(ds_tr16(sp + aoff[t][cb]), ds_tr16(sp + aoff[t][cb] + 4 * kBandRowBytes));
+          f.b[cb][pt] = cat8h(ds_tr16(sp + boff[t][cb]), ds_tr16(sp + boff[t][cb] + 4 * kBandRowBytes));
+        }
+      }
+    };
+    // one 32x32 block (tm, tn) of sub-tile t: the three f16x2 MFMAs
+    auto fmma1 = [&](auto T, const Frag& f, int tm, int tn) {
+      constexpr int t = decltype(T)::value;
+      f32x16 c = acc[t][tm][tn];
+      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[tm][1], f.b[tn][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[tm][0], f.b[tn][1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[tm][0], f.b[tn][0], c, 0, 0, 0);
+      acc[t][tm][tn] = c;
+    };
+    auto fmma = [&](auto T, const Frag& f) {
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) fmma1(T, f, tm, tn);
+    };
+    // sub-tile t's MFMAs with the commit of LDS buffer buf interleaved: block
+    // (tm, tn) = p's three MFMAs, then staged float4 p's split + stores (they
+    // issue while the third MFMA runs)
+    auto fmma_commit = [&](auto T, const Frag& f, int buf) {
+#pragma unroll
+      for (int p4 = 0; p4 < 4; ++p4) {
+        fmma1(T, f, p4 >> 1, p4 & 1);
+        commit1(buf, S0{}, p4 >> 1, p4 & 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    using T0 = std::integral_constant<int, 0>;
+    using T1 = std::integral_constant<int, 1>;
+    // one register set of staged loads: stage kt+1 is committed at the start of
+    // step kt and stage kt+2 fetched into the same registers right after (one
+    // stage of latency, as with two sets committed mid-step)
+    if (nk > 0) {
+      fetch(kbeg, S0{});
+      commit(0, S0{});
+      fetch(kbeg + kBandRows, S0{});
+    }
+    __syncthreads();
+    if (ntile > 0) fread(lds, 0, F[0]);
+    auto pstep = [&](int kt, auto I, auto NT) {
+      constexpr int nt = decltype(NT)::value;
+      constexpr int i = decltype(I)::value;
+      const int cur = i & 1;
+      const char* s = lds + cur * kBandBuf;
+      // the previous stage's last sub-tile (zero fragments before the first
+      // stage) with the commit of stage kt+1 interleaved
+      if constexpr (nt == 2) fmma_commit(T1{}, F[1], cur ^ 1);
+      if constexpr (nt == 1) fmma_commit(T0{}, F[(i + 1) & 1], cur ^ 1);
+      if constexpr (nt == 0) commit(cur ^ 1, S0{});
+      fetch(kbeg + (kt + 2) * kBandRows, S0{});
+      if constexpr (nt == 2) {
+        fread(s, 1, F[1]);
+        fmma(T0{}, F[0]);
+      }
+      // (the MFMAs stay before the barrier: sunk past it, they would leave the
+      // tile-1 reads just issued exposed at the barrier's wait)
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+      const char* sn = lds + (cur ^ 1) * kBandBuf;
+      if constexpr (nt == 2) fread(sn, 0, F[0]);
+      if constexpr (nt == 1) fread(sn, 0, F[(i + 1) & 1]);
+    };
+    auto prun = [&](auto NT) {
+      for (int kt = 0; kt < nk; kt += 2) {
+        pstep(kt, std::integral_constant<int, 0>{}, NT);
+        if (kt + 1 < nk) pstep(kt + 1, std::integral_constant<int, 1>{}, NT);
+      }
+      // the last stage's deferred sub-tile
+      constexpr int nt = decltype(NT)::value;
+      if constexpr (nt == 2) fmma(T1{}, F[1]);
+      if constexpr (nt == 1) {
+        if (nk > 0) {
+          if ((nk - 1) & 1) fmma(T0{}, F[1]);
+          else fmma(T0{}, F[0]);
+        }
+      }
+    };
+    if (ntile == 0) prun(std::integral_constant<int, 0>{});
+    else if (ntile == 1) prun(std::integral_constant<int, 1>{});
+    else prun(std::integral_constant<int, 2>{});
+#else
     if (nk > 0) {
       fetch(kbeg, S0{});
       fetch(kbeg + kBandRows, std::integral_constant<int, 1>{});
@@ -429,6 +552,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
     if (ntile == 0) run(std::integral_constant<int, 0>{});
     else if (ntile == 1) run(std::integral_constant<int, 1>{});
     else run(std::integral_constant<int, 2>{});
+
+#endif
 
     // tiles, unscaled, into their compact slots of this chunk
     const int khalf = lane >> 5;

@@ -24,12 +24,18 @@ namespace acmi {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 
-// power of two putting a bound mx at < 2^14; 1 for a zero / non-finite bound
+constexpr int F16X2_MAX_SCALE_EXP = 60;
+
+// power of two putting a bound mx at < 2^14; 1 for a zero / non-finite bound.
+// The exponent is capped at 2^60 so that the product of two scales (<= 2^120) and
+// its reciprocal (>= 2^-120) stay finite normal floats: a bound below 2^-46 then
+// loses precision gracefully (its scaled values sit below 2^14) instead of the
+// scale overflowing to inf and the unscale 1/(s_a s_b) zeroing the product.
 __device__ __forceinline__ float f16x2_scale(float mx) {
   if (!(mx > 0.f) || !(mx < 3.0e38f)) return 1.f;
   int e;
   (void)frexpf(mx, &e);  // mx < 2^e
-  return ldexpf(1.f, 14 - e);
+  return ldexpf(1.f, min(14 - e, F16X2_MAX_SCALE_EXP));
 }
 // the scale of a published bound (common.hpp amax_read: all 64 lanes active)
 __device__ __forceinline__ float f16x2_scale_of_bits(const unsigned* mx) {

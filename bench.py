@@ -213,6 +213,7 @@ def run(args):
         torch.cuda.synchronize()
         site = _lib.PROF_CONV2_WGRAD
         _lib.call('acmi_prof_enable', site, max(1, args.steps))
+        model.engine.comm_timing(True)
         marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
         inv_flags = []
         t0 = time.perf_counter()
@@ -226,7 +227,10 @@ def run(args):
         tot_ms, cnt = ctypes.c_double(), ctypes.c_int()
         _lib.call('acmi_prof_collect', ctypes.byref(tot_ms), ctypes.byref(cnt))
         _lib.call('acmi_prof_enable', 0, 0)
+        comm_ms, comm_bytes, comm_n = model.engine.comm_collect()
+        model.engine.comm_timing(False)
     elapsed = parallel.max_over_ranks(elapsed, dev)
+    comm_ms_max = parallel.max_over_ranks(comm_ms, dev)
     roll_ms = [m[0].elapsed_time(m[1]) for m in marks]
     upd_ms = [m[1].elapsed_time(m[2]) for m in marks]
     env_steps = N * T * args.steps * world
@@ -304,10 +308,12 @@ def run(args):
         r = cpu_baseline.run(n_envs=N, n_steps=T, iters=args.cpu_iters, A=A, C3=C3, algo=args.algo,
                              games=args.games)
         cpu = {'value': r['env_steps_per_s'], 'unit': 'env-steps/s', 'cores': r['threads'], 'kind': 'port',
-               'sample': '{} timed iterations (after one warm-up) of the same {} workload ({} envs x {} steps): '
-                         'torch-CPU fp32 restatement, {}{}'.format(
-                             r['iters'], args.algo.upper(), r['n_envs'], r['n_steps'], r['structure'],
+               'sample': '{} timed iterations (after one warm-up; per iteration min {:.2f} s, max {:.2f} s) of '
+                         'the same {} workload ({} envs x {} steps): torch-CPU fp32 restatement, {}{}'.format(
+                             r['iters'], min(r['iter_s']), max(r['iter_s']), args.algo.upper(), r['n_envs'],
+                             r['n_steps'], r['structure'],
                              ', K-FAC inverse timed once and amortised 1/10' if acktr else ''),
+               'iter_s': r['iter_s'],
                'update_ms': r['update_ms'], 'rollout_ms': r['rollout_ms']}
 
     if rank == 0:
@@ -323,6 +329,10 @@ def run(args):
                 'parallelism': 'dp{}'.format(world)},
             'update_ms': mean(upd_ms), 'update_ms_inverse_iters': mean(upd_inv),
             'update_ms_plain_iters': mean(upd_plain), 'rollout_ms': mean(roll_ms),
+            # communication: compute-stream stall on the per-update all-reduce
+            # (NetEngine.comm_timing; max over ranks), bytes summed per update
+            'allreduce_ms': comm_ms_max if world > 1 else 0.0, 'allreduce_bytes': comm_bytes,
+            'allreduce_updates_timed': comm_n, 'dist_backend': parallel.backend_name(),
             'roofline': roofline, 'cpu_baseline': cpu,
         }
         if cpu:

@@ -61,9 +61,15 @@ int acmi_get_gemm_mode(void);
  *   ACMI_FWD_F32   f16x2 split operands (scaled f16 h + l, three MFMAs per
  *                  product), f32-accurate (default)
  *   ACMI_FWD_BF16  one 16-bit MFMA per product: weights and conv2/conv3 inputs
- *                  scaled by powers of two and rounded once to f16 (11-bit
- *                  significands -- at least bf16's precision; u8 pixels exact),
- *                  f32 accumulation
+ *                  scaled by powers of two and rounded once to f16 (u8 pixels
+ *                  exact), f32 accumulation.  The error bound is RELATIVE TO
+ *                  EACH TENSOR'S RANGE: elements within 2^-14 of their tensor's
+ *                  bound keep 11-bit significands (finer than bf16's 8), but
+ *                  f16's exponent range is narrower than bf16's -- elements
+ *                  below ~2^-28 of the bound become f16 subnormals and below
+ *                  ~2^-38 flush to zero, where bf16 would keep them.  The
+ *                  bounds are weight-derived (loose), which widens that margin;
+ *                  the tests check error against each tensor's range
  * The backward, the K-FAC statistics and the optimizers stay f32-accurate; they
  * read the activations the forward produced.  Initial mode from ACMI_FORWARD
  * ("bf16" / "f32").  Not stream-ordered: set it between launches.

@@ -175,9 +175,10 @@ def _sample(torch, logits, gen):
 
 
 def run(n_envs=32, n_steps=20, iters=3, A=4, C3=32, algo='acktr', seed=0, time_budget_s=20.0, ipc=None,
-        threads=None, games=None):
-    """Times warm-up + up to `iters` iterations (at most ~time_budget_s); returns
-    env-steps/s and the update / rollout split."""
+        threads=None, games=None, min_iters=3):
+    """Times warm-up + up to `iters` iterations; after `min_iters` timed iterations it
+    stops once ~time_budget_s have passed.  Returns env-steps/s, the update / rollout
+    split and every timed iteration's seconds (the spread of the sample)."""
     import torch
     threads = threads or cpu_threads()
     torch.set_num_threads(threads)
@@ -196,7 +197,7 @@ def run(n_envs=32, n_steps=20, iters=3, A=4, C3=32, algo='acktr', seed=0, time_b
     gamma, beta, lr_acktr, lr_a2c = 0.99, 0.01, 0.25, 7e-4
     env = make_envs(n_envs, A, seed, ipc, games)
     obs = np.stack(env.reset())
-    stats = dict(rollout=0.0, update=0.0, n=0)
+    stats = dict(rollout=0.0, update=0.0, n=0, iter_s=[], env=0.0)
     inv_s = 0.0
     t_start = time.perf_counter()
     try:
@@ -209,8 +210,11 @@ def run(n_envs=32, n_steps=20, iters=3, A=4, C3=32, algo='acktr', seed=0, time_b
             for t in range(n_steps):
                 ob_steps[:, t] = obs
                 a = _sample(torch, net.forward(obs, False)['logits'], gen).numpy()
+                te = time.perf_counter()
                 nxt, r, d, _ = env.step(a.tolist())
                 obs = np.stack(nxt)
+                if it > 0:
+                    stats['env'] += time.perf_counter() - te
                 actions[:, t], rewards[:, t], terms[:, t] = a, r, d
             t1 = time.perf_counter()
             M = n_envs * n_steps
@@ -265,7 +269,8 @@ def run(n_envs=32, n_steps=20, iters=3, A=4, C3=32, algo='acktr', seed=0, time_b
                 stats['rollout'] += t1 - t0
                 stats['update'] += t2 - t1
                 stats['n'] += 1
-                if time.perf_counter() - t_start > time_budget_s:
+                stats['iter_s'].append(t2 - t0)
+                if stats['n'] >= min_iters and time.perf_counter() - t_start > time_budget_s:
                     break
         if acktr:  # the damped inverses (every 10 updates), timed once, amortised
             t3 = time.perf_counter()
@@ -283,9 +288,14 @@ def run(n_envs=32, n_steps=20, iters=3, A=4, C3=32, algo='acktr', seed=0, time_b
     per_iter = (stats['rollout'] + stats['update']) / n + inv_s / 10.0
     return dict(env_steps_per_s=n_envs * n_steps / per_iter, update_ms=1e3 * (stats['update'] / n + inv_s / 10.0),
                 rollout_ms=1e3 * stats['rollout'] / n, inverse_ms=1e3 * inv_s, iters=stats['n'], threads=threads,
-                n_envs=n_envs, n_steps=n_steps, ipc=ipc, algo=algo,
+                n_envs=n_envs, n_steps=n_steps, ipc=ipc, algo=algo, iter_s=stats['iter_s'],
                 structure=('{} SubprocessEnv children (Pipe protocol) + ThreadPoolExecutor({})'.format(n_envs, n_envs)
-                           if ipc else '{} in-process envs on a ThreadPoolExecutor({})'.format(n_envs, n_envs)))
+                           if ipc else '{} in-process envs on a ThreadPoolExecutor({}) (one SubprocessEnv child per env '
+                           'is used up to 64 envs; {} children plus the {}-thread pool would approach the GPU box\'s '
+                           'limit on processes per call; in-process env stepping was {:.1f}% of the timed '
+                           'iterations, so the Pipe round trips the reference pays are NOT in this number)'.format(
+                               n_envs, n_envs, n_envs, n_envs, 100.0 * stats['env'] / max(1e-9, sum(stats['iter_s'])))),
+                env_step_frac=stats['env'] / max(1e-9, sum(stats['iter_s'])))
 
 
 if __name__ == '__main__':

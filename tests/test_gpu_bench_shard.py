@@ -117,20 +117,16 @@ def _rel(got, ref):
     return ((got.double() - ref).abs().max() / ref.abs().max()).item()
 
 
-def test_update_statistics_at_bench_shard_match_float64(lib, cuda):
-    """One acmi_backward (loss gradients + A factors) and one acmi_kfac_output_stats
-    (G factors of the sampled losses) over M = 512 x 20 = 10240 images -- the
-    BASELINE configs[3] per-GPU shard, default arithmetic (bf16x3, band reductions,
-    pre-split weights) -- against float64 on the GPU."""
+def _stats_vs_float64(lib, cuda, B, params, seed=2024):
+    """One acmi_forward + acmi_backward (loss gradients + A factors) + one
+    acmi_kfac_output_stats (G factors of the sampled losses) over B images, each
+    block against float64 (and against plain float32 arithmetic of the same
+    formulas): {(kind, block): (kernel rel err, plain-f32 rel err)}."""
     from actorcritic._engine import Layout
-    A, C3, B = 4, 32, 512 * 20
+    A, C3 = 4, 32
     L = Layout(A, C3)
-    params = torch.from_numpy(L.init_params(seed=7)).to(cuda)
-    gen = torch.Generator(device=cuda).manual_seed(2024)
+    gen = torch.Generator(device=cuda).manual_seed(seed)
     obs = torch.randint(0, 256, (B, 84, 84, 4), generator=gen, device=cuda, dtype=torch.uint8)
-    info = (ctypes.c_int64 * 5)()
-    _lib.call('acmi_band_info', 1, C3, B, info)
-    assert info[2] >= 2, list(info)  # the production plan of the bench shard: several image chunks
     z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=cuda)
     t = dict(a1=z(B, 20, 20, 32), a2=z(B, 9, 9, 64), a3=z(B, 7, 7, C3), a4=z(B, 512), logits=z(B, A), value=z(B))
     acts = _lib.Acts(*[t[k].data_ptr() for k in ('a1', 'a2', 'a3', 'a4', 'logits', 'value')], A)
@@ -159,14 +155,14 @@ def test_update_statistics_at_bench_shard_match_float64(lib, cuda):
     ds = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
     dhead_s = z(B, ldh)  # the sampled chain writes its own head gradients here
     bwd_s = _lib.Bwd(*[x.data_ptr() for x in ds], dhead_s.data_ptr(), ldh)
-    seed, counter = 0x4b464143, 41
-    _lib.call('acmi_kfac_output_stats', ctypes.byref(net), B, ctypes.byref(acts), ctypes.byref(bwd_s), seed, 0,
+    seed_s, counter = 0x4b464143, 41
+    _lib.call('acmi_kfac_output_stats', ctypes.byref(net), B, ctypes.byref(acts), ctypes.byref(bwd_s), seed_s, 0,
               counter, _lib.ptr(gstat), _lib.ptr(ws), st)
     torch.cuda.synchronize()
     assert torch.isfinite(grads).all() and torch.isfinite(astat).all() and torch.isfinite(gstat).all()
 
     # the sampled head gradients from the kernel's own f32 logits and counters
-    g_pi, g_v, _ = oracle.sampled_head_grads(t['logits'].cpu().numpy(), seed, 0, counter)
+    g_pi, g_v, _ = oracle.sampled_head_grads(t['logits'].cpu().numpy(), seed_s, 0, counter)
     g_pi = torch.from_numpy(np.asarray(g_pi, np.float64)).to(cuda)
     g_v = torch.from_numpy(np.asarray(g_v, np.float64)).to(cuda)
     ref = _Ref(L.split(params), A, C3, cuda)
@@ -193,10 +189,46 @@ def test_update_statistics_at_bench_shard_match_float64(lib, cuda):
         errs[('G', l)] = (_rel(gstat[so[5 + l]:so[5 + l] + n * n].reshape(n, n), gf_ref[l]), _rel(gf_32[l], gf_ref[l]))
     for k, (v, v32) in errs.items():
         print(k, 'kernel %.2e  plain f32 %.2e' % (v, v32))
+    return errs
+
+
+def test_update_statistics_at_bench_shard_match_float64(lib, cuda):
+    """One acmi_backward (loss gradients + A factors) and one acmi_kfac_output_stats
+    (G factors of the sampled losses) over M = 512 x 20 = 10240 images -- the
+    BASELINE configs[3] per-GPU shard, default arithmetic (f16x2 / bf16x3, band
+    reductions, pre-split weights) -- against float64 on the GPU."""
+    from actorcritic._engine import Layout
+    B = 512 * 20
+    info = (ctypes.c_int64 * 5)()
+    _lib.call('acmi_band_info', 1, 32, B, info)
+    assert info[2] >= 2, list(info)  # the production plan of the bench shard: several image chunks
+    params = torch.from_numpy(Layout(4, 32).init_params(seed=7)).to(cuda)
+    errs = _stats_vs_float64(lib, cuda, B, params)
     # f32-class: within the section 5 bound (gradients / A factors 2e-5, G 5e-5)
     # or within 4x of what plain float32 arithmetic of the same formulas gets --
     # at 10240 images the weight-gradient sums cancel (random-sign head
     # gradients), which magnifies every implementation's rounding alike
+    for k, (v, v32) in errs.items():
+        tol = 5e-5 if k[0] == 'G' else 2e-5
+        assert v < max(tol, 4 * v32), (k, v, v32)
+
+
+def test_update_statistics_with_tiny_output_gradients(lib, cuda):
+    """Head weights scaled to ~1e-17: every output gradient d1..d4 (and so the G
+    factors' Grams of one tensor with itself) sits near 1e-17 ~ 2^-56.  f16x2 scales
+    each operand by a power of two putting its bound below 2^14 (f16x2.hpp
+    f16x2_scale); uncapped, that scale would be 2^70 and the Gram's unscale
+    1/(s s) = 1/2^140 = 1/inf would zero the factor.  The cap (2^60) keeps it
+    finite: the G factors (~1e-34), the gradients and the A factors stay within the
+    bench-shard test's f32-class bounds of float64."""
+    from actorcritic._engine import Layout
+    L = Layout(4, 32)
+    p = L.init_params(seed=7)
+    for blk in (8, 9, 10, 11):  # fc_policy W, b; fc_baseline W, b
+        o, e = L.offsets[blk], (L.offsets[blk + 1] if blk < 11 else L.nparams)
+        p[o:e] *= np.float32(1e-15)
+    params = torch.from_numpy(p).to(cuda)
+    errs = _stats_vs_float64(lib, cuda, 256, params, seed=5)
     for k, (v, v32) in errs.items():
         tol = 5e-5 if k[0] == 'G' else 2e-5
         assert v < max(tol, 4 * v32), (k, v, v32)

@@ -152,3 +152,10 @@ def test_bench_self_launches_ranks():
     assert out['n_gpus'] == 2 and out['config']['parallelism'] == 'dp2'
     assert out['config']['global_envs'] == 32 and out['config']['envs_per_gpu'] == 16
     assert out['value'] > 0 and out['cpu_baseline'] is None
+    # the communication leg is separated from compute: the compute stream's stall on
+    # the per-update all-reduce (ms, max over ranks) and the bytes summed per update
+    # (grads + 4 loss scalars + packed A and G statistics, ACKTR C3 = 32: 10.8 MB)
+    assert out['dist_backend'] == 'gloo'
+    assert out['allreduce_updates_timed'] == 2
+    assert out['allreduce_ms'] > 0 and out['allreduce_ms'] < out['ms_per_step']
+    assert 10.0e6 < out['allreduce_bytes'] < 11.5e6, out['allreduce_bytes']

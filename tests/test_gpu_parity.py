@@ -294,7 +294,7 @@ def test_first_order_optimizers_match_oracle(lib, cuda):
     np.testing.assert_allclose(ms.cpu().numpy(), rms, rtol=1e-5)
 
 
-def _build(N=3, T=4, A=4, C3=32, seed=5):
+def _build(N=3, T=4, A=4, C3=32, seed=5, games=None):
     from actorcritic import session as sess
     from actorcritic.agents import MultiEnvAgent
     from actorcritic.envs.atari.model import AtariModel
@@ -304,7 +304,8 @@ def _build(N=3, T=4, A=4, C3=32, seed=5):
     from actorcritic.nn import linear_decay
     from actorcritic.objectives import A2CObjective
     sess.reset_default_graph()
-    env = MultiEnv(SyntheticAtariEnvs(N, num_actions=A, seed=seed))
+    kw = {} if games is None else dict(games=games)
+    env = MultiEnv(SyntheticAtariEnvs(N, num_actions=A, seed=seed, **kw))
     params = oracle.init_params(A, C3, seed=1)
     model = AtariModel(env.observation_space, env.action_space, C3, params=params, random_seed=3)
     agent = MultiEnvAgent(env, model, T)
@@ -355,34 +356,90 @@ def test_rollout_matches_oracle_env_and_tower(lib, cuda):
         np.testing.assert_array_equal(act[:, t].cpu().numpy(), oracle.sample_f32(lg[:, t], u))
 
 
-@pytest.mark.parametrize('N,T', [(3, 5), (32, 20)], ids=['toy', 'configs2-32x20'])
-def test_acktr_update_matches_oracle(lib, cuda, N, T):
+_UPDATE_CASES = [
+    # (N, T, A, games, forward)
+    (3, 5, 4, None, 'f32'),
+    (32, 20, 4, None, 'f32'),
+    (32, 20, 18, 'atari57', 'f32'),
+    (32, 20, 18, 'atari57', 'bf16'),
+]
+
+
+@pytest.fixture
+def forward_mode(lib):
+    """Sets acmi_set_forward_mode for one test and restores the previous mode."""
+    prev = lib.acmi_get_forward_mode()
+    yield lambda m: _lib.call('acmi_set_forward_mode', _lib.FWD_BF16 if m == 'bf16' else _lib.FWD_F32)
+    _lib.call('acmi_set_forward_mode', prev)
+
+
+def _blocks(A, C3):
+    """[(name, lo, hi)] of the six K-FAC blocks ([W; b] contiguous) in the flat layout."""
+    off, n = oracle.param_offsets(A, C3)
+    names = ['conv1', 'conv2', 'conv3', 'fc4', 'fc_policy', 'fc_baseline']
+    return [(names[l], off[2 * l], off[2 * l + 2] if l < 5 else n) for l in range(6)]
+
+
+@pytest.mark.parametrize('N,T,A,games,fwd', _UPDATE_CASES,
+                         ids=['toy', 'configs2-32x20', 'configs4-a18-atari57', 'configs4-a18-atari57-bf16fwd'])
+def test_acktr_update_matches_oracle(lib, cuda, forward_mode, N, T, A, games, fwd):
     """One steady-state ACKTR update at gs=40 (covariance update + inverse + apply)
-    against the float64 oracle on the same rollout -- at a toy size and at the
+    against the float64 oracle on the same rollout -- at a toy size, at the
     reference's own ACKTR config, BASELINE configs[2] (32 envs x 20 steps, C3 = 32,
-    a2c_acktr.py:306-310, :51-53): A/G factors, the damped inverses, the
-    preconditioned gradients (north_star rel-L2 1e-3), the trust-region coefficient
-    and the parameter step."""
+    a2c_acktr.py:306-310, :51-53), and at the configs[4] action space (A = 18, mixed
+    Atari-57 games): A/G factors, the damped inverses, the preconditioned gradients
+    (north_star rel-L2 1e-3) and the parameter step, all PER K-FAC BLOCK (the value
+    head's 513 and the policy head's 19 x 18 entries are < 0.3 % of the vector; a
+    global norm could hide them), and the trust-region coefficient.
+
+    A = 18 runs the policy head's categorical G factor at 18 x 18
+    (policies.py:146-158), the heads' weight gradient + A factor with 19 dY columns,
+    and the K-FAC step's narrow first product for A % 4 != 0 (kfac.hip
+    kfac_narrow_kernel).  The bf16 case runs the rollout tower on bf16 MFMAs
+    (BASELINE configs[4] "bf16 forward / fp32 KFAC"); the update behind it is f32,
+    so the oracle's backward, factors and step are fed the GPU's own bf16-forward
+    activations, logits, values and targets (a2c_acktr.py:243-247) -- what is
+    checked is the f32 update on those inputs, at the f32 tolerances."""
     from actorcritic import session as sess
-    A, C3 = 4, 32
-    env, model, agent, obj, gs, opt, op, params = _build(N, T, A, C3)
+    forward_mode(fwd)
+    C3 = 32
+    env, model, agent, obj, gs, opt, op, params = _build(N, T, A, C3, games=games)
     gs.assign(40)
     with sess.Session() as s:
         data = agent.interact(s)
         feed = _feed(model, data)
-        fwd = model.engine.lookup_rollout(data[0])
-        logits32 = fwd.flat_logits.cpu().numpy().copy()
+        fwd_out = model.engine.lookup_rollout(data[0])
+        logits32 = fwd_out.flat_logits.cpu().numpy().copy()
         p_before = model.params.cpu().numpy().astype(np.float64)
+        if fwd == 'bf16':
+            acts = fwd_out.acts
+            M = N * T
+            gpu = dict(a1=acts.a1[:M], a2=acts.a2[:M], a3=acts.a3[:M], a4=acts.a4[:M],
+                       logits=fwd_out.flat_logits, value=fwd_out.flat_value)
+            gpu = {k: v.cpu().double().numpy() for k, v in gpu.items()}
+            tg_gpu = s.run(obj.target_values, feed_dict=feed)
         s.run(op, feed_dict=feed)
         torch.cuda.synchronize()
     obs, act, rew, term, nxt, _ = [x for x in data]
     M = N * T
-    full = oracle.forward(p_before, obs.cpu().numpy().reshape(M, 84, 84, 4), A, C3)
-    vb = oracle.forward(p_before, nxt.cpu().numpy(), A, C3)['value']
-    tg = oracle.targets_f64(rew.cpu().numpy(), term.cpu().numpy(), vb, 0.99).reshape(-1)
+    if fwd == 'bf16':
+        full = dict(gpu, x=obs.cpu().numpy().reshape(M, 84, 84, 4).astype(np.float64) / 255.0)
+        full['a3f'] = full['a3'].reshape(M, -1)
+        tg = np.asarray(tg_gpu, np.float64).reshape(-1)
+        # the bf16 tower is within 1e-2 of float64 (test_bf16_forward_mode); the
+        # update is only meaningful if its inputs are close to the f32 forward
+        ref_fwd = oracle.forward(p_before, obs.cpu().numpy().reshape(M, 84, 84, 4), A, C3)
+        rel = np.abs(full['logits'] - ref_fwd['logits']).max() / np.abs(ref_fwd['logits']).max()
+        assert rel < 1e-2, rel
+    else:
+        full = oracle.forward(p_before, obs.cpu().numpy().reshape(M, 84, 84, 4), A, C3)
+        vb = oracle.forward(p_before, nxt.cpu().numpy(), A, C3)['value']
+        tg = oracle.targets_f64(rew.cpu().numpy(), term.cpu().numpy(), vb, 0.99).reshape(-1)
     lg = oracle.a2c_loss_and_head_grads(full['logits'], full['value'], act.cpu().numpy().reshape(-1), tg)
     grads, _, afac = oracle.backward(p_before, full, lg['dlogits'], lg['dvalue'], A, C3, with_a_factors=True)
     g_pi, g_v, y = oracle.sampled_head_grads(logits32, 0x4b464143, 0, 40)
+    if games is not None:
+        assert len(np.unique(y)) > 4  # the draws reach actions beyond Breakout's four
     gfac = oracle.g_factors(p_before, full, g_pi, g_v, A, C3)
     st = opt.state
     L = model.engine.layout
@@ -397,6 +454,7 @@ def test_acktr_update_matches_oracle(lib, cuda, N, T):
         got = fac[L.stat_off[5 + l]:L.stat_off[5 + l] + d * d].reshape(d, d)
         rel = np.abs(got - gfac[l]).max() / np.abs(gfac[l]).max()
         assert rel < 5e-5, ('G', l, rel)
+    assert L.dout[4] == A
     inv = oracle.damped_inverses(afac, gfac, 0.01)
     # the damped inverses, each against the float64 inverse of the oracle's factors
     # (their difference is the f32 factors' rounding seen through the damped
@@ -411,10 +469,17 @@ def test_acktr_update_matches_oracle(lib, cuda, N, T):
     new_p, vel, precon, coeff = oracle.kfac_step(p_before, np.zeros_like(p_before), grads, inv,
                                                  oracle.linear_decay(0.25, 0.025, 40, 1000), 0.9, 1e-4, A, C3)
     got_pre = st['precon'].cpu().numpy().astype(np.float64)
+    got_p = model.params.cpu().numpy().astype(np.float64)
     rel_l2 = np.linalg.norm(got_pre - precon) / np.linalg.norm(precon)
     assert rel_l2 < 1e-3, rel_l2  # north_star: preconditioned gradients within 1e-3 rel-L2
+    # ... and per K-FAC block, so a wrong head block cannot hide in the global norm
+    for name, lo, hi in _blocks(A, C3):
+        e_pre = np.linalg.norm(got_pre[lo:hi] - precon[lo:hi]) / np.linalg.norm(precon[lo:hi])
+        e_step = np.linalg.norm(got_p[lo:hi] - new_p[lo:hi]) / np.linalg.norm(new_p[lo:hi] - p_before[lo:hi])
+        print('block %-11s precon rel-L2 %.2e  step rel-L2 %.2e' % (name, e_pre, e_step))
+        assert e_pre < 1e-3, (name, 'precon', e_pre)
+        assert e_step < 1e-3, (name, 'step', e_step)
     assert float(st['coeff'][0]) == pytest.approx(coeff, rel=1e-3)
-    got_p = model.params.cpu().numpy().astype(np.float64)
     assert np.linalg.norm(got_p - new_p) / np.linalg.norm(new_p - p_before) < 1e-3
     assert gs.value == 41
 
