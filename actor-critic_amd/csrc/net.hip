@@ -435,7 +435,10 @@ int g_forward_mode = [] {
 // split factor for fc4 at small batch (64 x 128 tiles over 512 columns; 4 / 6 /
 // 12 / 16 chunks measured no better than 8)
 static void fc4_plan(int B, int K, int* nz, int* chunk) {
-  constexpr int maxsp = 8;
+  // ACMI_FC4_SPLIT_SMALL: the split cap at batches <= 128 (default 16: the chain
+  // of k-steps per chunk, not the slab traffic, sets fc4's time there)
+  static const int small_sp = getenv("ACMI_FC4_SPLIT_SMALL") ? atoi(getenv("ACMI_FC4_SPLIT_SMALL")) : 16;
+  const int maxsp = B <= 128 ? std::max(1, std::min(16, small_sp)) : 8;
   const int blocks = cdiv(B, 64) * 4;
   int sp = blocks >= 256 ? 1 : std::min(maxsp, cdiv(256 * maxsp / 8, blocks));
   const int q = g_gemm_mode == ACMI_GEMM_X3 ? 16 : 32;  // the split GEMM's K-tile
@@ -555,16 +558,17 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   const bool h16 = g_forward_mode == ACMI_FWD_BF16;
   // the fused tail + next tower at the rollout's split-K count; any other (or
   // no) split runs the tail and then the next step's tower as two launches
-  const bool fuse_next = nxt && split && nz == 8;
+  // (small batches run the 16-wave tower, which the fused tail does not host)
+  const bool fuse_next = nxt && split && (nz == 8 || nz == 16) && B > wide_tower_max();
 #define ACMI_HEADS(NZ)                                                                          \
-  if (tail && fuse_next && NZ == 8) {                                                           \
+  if (tail && fuse_next && (NZ == 8 || NZ == 16)) {                                             \
     if (h16)                                                                                    \
-      hipLaunchKernelGGL((rollout_tail_tower_kernel<8, C3, true>), dim3(B), hb, 0, s, hp, nz,    \
+      hipLaunchKernelGGL((rollout_tail_tower_kernel<NZ == 16 ? 16 : 8, C3, true>), dim3(B), hb, 0, s, hp, nz, \
                          P + L.off[7], a->a4, st * 512, B, P + L.off[8], P + L.off[9],          \
                          P + L.off[10], P + L.off[11], L.A, a->logits, st * a->ld_logits, hv, st, \
                          *tail, ntw);                                                           \
     else                                                                                        \
-      hipLaunchKernelGGL((rollout_tail_tower_kernel<8, C3, false>), dim3(B), hb, 0, s, hp, nz,   \
+      hipLaunchKernelGGL((rollout_tail_tower_kernel<NZ == 16 ? 16 : 8, C3, false>), dim3(B), hb, 0, s, hp, nz, \
                          P + L.off[7], a->a4, st * 512, B, P + L.off[8], P + L.off[9],          \
                          P + L.off[10], P + L.off[11], L.A, a->logits, st * a->ld_logits, hv, st, \
                          *tail, ntw);                                                           \
