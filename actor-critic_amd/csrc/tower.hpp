@@ -241,6 +241,9 @@ struct TowB {
 #define ACMI_WIDE_DEPTH 6
 #endif
 constexpr int kWideDepth = ACMI_WIDE_DEPTH;
+#ifndef ACMI_TOW_PROBE  // 4-wave body timing probes (wrong results): 1 stop after conv1, 2 after conv2,
+#define ACMI_TOW_PROBE 0  // 4 no global stores, 8 stop after the image load
+#endif
 #ifndef ACMI_WIDE_PROBE  // timing probes (wrong results): 1 stop after conv1, 2 after conv2, 4 no global stores
 #define ACMI_WIDE_PROBE 0
 #endif
@@ -545,6 +548,10 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
 #pragma unroll
     for (int i = 0; i < kTowDepth; ++i) bw.fetch(i, 0, lane, i);
     __syncthreads();
+    if constexpr (ACMI_TOW_PROBE & 8) {
+      if (tid == 0 && (unsigned char)imgL[7] == 255 && imgL[5000] == 3) a1g[img] = 1.f;
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       if (s + kTowDepth < 16) bw.fetch(s + kTowDepth, 0, lane, (s + kTowDepth) % kTowSlots);
@@ -567,9 +574,9 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     auto emit1 = [&](int p, float v) {
       v = fmaxf(__builtin_fmaf(v * inv1, 1.0f / 255.0f, bias), 0.f);
       tow_put<32, 2>(a1L, p, p % 20, col, v, sa1);
-      g[p * 32 + col] = v;
+      if constexpr (!(ACMI_TOW_PROBE & 4)) g[p * 32 + col] = v;
       const unsigned long long bal = __ballot(v > 0.f);
-      if (mg && col == 0) mg[p] = (uint32_t)(bal >> (lane & 32));
+      if (!(ACMI_TOW_PROBE & 4) && mg && col == 0) mg[p] = (uint32_t)(bal >> (lane & 32));
     };
 #pragma unroll
     for (int u = 0; u < 3; ++u)
@@ -591,6 +598,10 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     }
   }
   __syncthreads();
+  if constexpr (ACMI_TOW_PROBE & 1) {
+    if (tid == 0 && a1L[5] == 3 && a1L[333] == 4) a1g[img] = 1.f;
+    return;
+  }
 
   // ---- conv2: a1 -> a2 [9][9][64] ------------------------------------------------
   {
@@ -649,9 +660,9 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     auto emit = [&](int p, float v) {
       v = fmaxf(__builtin_fmaf(v, inv2, bias), 0.f);
       tow_put<64, 1>(imgL, p, p % 9, c, v, sa2);
-      g[p * 64 + c] = v;
+      if constexpr (!(ACMI_TOW_PROBE & 4)) g[p * 64 + c] = v;
       const unsigned long long bal = __ballot(v > 0.f);
-      if (mg && col == 0) mg[2 * p + ct] = (uint32_t)(bal >> (lane & 32));
+      if (!(ACMI_TOW_PROBE & 4) && mg && col == 0) mg[2 * p + ct] = (uint32_t)(bal >> (lane & 32));
     };
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -667,6 +678,10 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     }
   }
   __syncthreads();
+  if constexpr (ACMI_TOW_PROBE & 2) {
+    if (tid == 0 && imgL[5] == 3 && imgL[333] == 4) a1g[img] = 1.f;
+    return;
+  }
 
   // ---- conv3: a2 -> a3 [7][7][C3] -------------------------------------------------
   {
@@ -708,9 +723,9 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     uint32_t* mg = m3g ? m3g + img * st * (49 * C3 / 32) : nullptr;
     auto emit3 = [&](int p, float v) {  // (active lanes: whole 32-lane halves)
       v = fmaxf(__builtin_fmaf(v, inv3, bias), 0.f);
-      g[p * C3 + c] = v;
+      if constexpr (!(ACMI_TOW_PROBE & 4)) g[p * C3 + c] = v;
       const unsigned long long bal = __ballot(v > 0.f);
-      if (mg && col == 0) mg[p * (C3 / 32) + ct] = (uint32_t)(bal >> (lane & 32));
+      if (!(ACMI_TOW_PROBE & 4) && mg && col == 0) mg[p * (C3 / 32) + ct] = (uint32_t)(bal >> (lane & 32));
     };
     if constexpr (C3 == 32) {  // the second K half (waves 2, 3) through LDS to the first
       float* scr = reinterpret_cast<float*>(a1L);  // [rt][32 rows][32]
