@@ -23,7 +23,10 @@
 
 namespace acmi {
 
-constexpr int kFc4Depth = 3;  // k-steps in flight ahead of the one computed
+#ifndef ACMI_FC4_DEPTH
+#define ACMI_FC4_DEPTH 3
+#endif
+constexpr int kFc4Depth = ACMI_FC4_DEPTH;  // k-steps in flight ahead of the one computed
 
 // W4 [K][512] -> [K/16 steps][16 col tiles][part h, l][64 lanes] x 16 B, scaled
 // by the power of two of hdr[kTowMaxW4] (the tower's header)

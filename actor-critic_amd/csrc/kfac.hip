@@ -145,47 +145,16 @@ __global__ void damp_kernel(DampSet d, const double* tr, double* ws) {
 // other (ping-pong: one barrier per sweep; 32 sweeps end in P).  1/pivot from
 // v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient, a third
 // of the division sequence's latency).  The sweep was 12 of a panel launch's
-// 22 us with the division and two barriers per sweep.
+// 22 us with the division and two barriers per sweep.  (One wave doing all
+// 32 x 32 elements without barriers -- 16 per lane -- measured slower: 2.52 vs
+// 1.69 ms per inverse; the longer per-lane LDS chains cost more than the
+// barriers.)
 __device__ __forceinline__ double recip_f64(double d) {
   double r = __builtin_amdgcn_rcp(d);
   double e = fma(-d, r, 1.0);
   r = fma(r, e, r);
   e = fma(-d, r, 1.0);
   return fma(r, e, r);
-}
-// The same sweeps by ONE wave (64 lanes, 16 elements each) without barriers:
-// the LDS operations of a wave execute in issue order, so sweep t + 1 reads
-// what sweep t wrote; the other waves of the block wait at one barrier after it.
-// (256 threads: 32 sweeps x one barrier each was ~12 of the panel's 17.7 us.)
-__device__ void pivot_inverse_wave(double (*P)[GJB + 1], double (*Q)[GJB + 1]) {
-  const int lane = threadIdx.x & 63;
-  const int c = lane & (GJB - 1), r0 = lane >> 5;  // rows r0, r0+2, ..., r0+30
-  static_assert(GJB == 32 && GJB % 2 == 0, "two row halves of 16, an even number of sweeps");
-  for (int t = 0; t < GJB; t += 2) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      double (*src)[GJB + 1] = h ? Q : P;
-      double (*dst)[GJB + 1] = h ? P : Q;
-      const int tt = t + h;
-      const double ipiv = recip_f64(src[tt][tt]);
-      const double ptc = src[tt][c];
-      double prt[16], prc[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        prt[q] = src[r0 + 2 * q][tt];
-        prc[q] = src[r0 + 2 * q][c];
-      }
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int r = r0 + 2 * q;
-        double v;
-        if (r == tt) v = c == tt ? ipiv : ptc * ipiv;
-        else v = c == tt ? -prt[q] * ipiv : prc[q] - prt[q] * ptc * ipiv;
-        dst[r][c] = v;
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
 }
 __device__ void pivot_inverse(double (*P)[GJB + 1], double (*Q)[GJB + 1]) {
   const int tid = threadIdx.x;
@@ -225,9 +194,6 @@ __device__ __forceinline__ double gj_sym(const double* M, int np, int r, int c) 
 }
 
 constexpr int PANEL_COLS = 64;
-#ifndef ACMI_PIVOT_WAVE  // 1: the pivot block's sweeps by one wave without barriers
-#define ACMI_PIVOT_WAVE 1
-#endif
 // grid: (column chunks of PANEL_COLS, active matrices); thread (column j, pivot-row
 // quarter) forms 8 rows of Rrow' = Pinv M[kb.., j] (8 accumulators, 256 LDS reads)
 __global__ __launch_bounds__(256) void gj_panel_kernel(MatSet s, double* ws, int step) {
@@ -260,12 +226,7 @@ __global__ __launch_bounds__(256) void gj_panel_kernel(MatSet s, double* ws, int
     cold[u] = e < rows * GJB ? gj_sym(M, np, c0 + e / GJB, kb + e % GJB) : 0.0;
   }
   __syncthreads();
-#if ACMI_PIVOT_WAVE
-  if (threadIdx.x < 64) pivot_inverse_wave(P, Q);
-  __syncthreads();
-#else
   pivot_inverse(P, Q);
-#endif
   if (j < np) {
     if (!jcol) {
 #pragma unroll

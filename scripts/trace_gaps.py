@@ -43,6 +43,8 @@ def main(path, marker='returns_kernel', skip=0):
         else:
             cur_e = max(cur_e, e)
     busy += min(cur_e, w1) - cur_b
+    if w1 > cur_e:  # the idle time before the next iteration's first kernel
+        gaps.append(w1 - cur_e)
     span = w1 - w0
     per = lambda x: x / iters / 1e3
     print('# Kernel-trace timeline: {} iterations (window {} .. {} by `{}`)\n'.format(iters, w0, w1, marker))

@@ -396,10 +396,15 @@ def test_acktr_update_matches_oracle(lib, cuda, forward_mode, N, T, A, games, fw
     (policies.py:146-158), the heads' weight gradient + A factor with 19 dY columns,
     and the K-FAC step's narrow first product for A % 4 != 0 (kfac.hip
     kfac_narrow_kernel).  The bf16 case runs the rollout tower on bf16 MFMAs
-    (BASELINE configs[4] "bf16 forward / fp32 KFAC"); the update behind it is f32,
-    so the oracle's backward, factors and step are fed the GPU's own bf16-forward
-    activations, logits, values and targets (a2c_acktr.py:243-247) -- what is
-    checked is the f32 update on those inputs, at the f32 tolerances."""
+    (BASELINE configs[4] "bf16 forward / fp32 KFAC"); the update behind it is f32.
+
+    The oracle's backward, factors and step are fed the GPU's own forward --
+    activations, logits, values, targets (a2c_acktr.py:243-247) -- after that forward
+    is checked against the float64 oracle forward (rel 1e-5, bf16: 1e-2): what is
+    compared is the update's arithmetic on identical inputs.  (With the float64
+    forward's own ReLU masks, a pre-activation within f32 rounding of zero takes the
+    other branch; at 640 rows x 12800 conv1 outputs such flips move conv1's G factor
+    by ~1e-4, more than the update's rounding.)"""
     from actorcritic import session as sess
     forward_mode(fwd)
     C3 = 32
@@ -411,30 +416,31 @@ def test_acktr_update_matches_oracle(lib, cuda, forward_mode, N, T, A, games, fw
         fwd_out = model.engine.lookup_rollout(data[0])
         logits32 = fwd_out.flat_logits.cpu().numpy().copy()
         p_before = model.params.cpu().numpy().astype(np.float64)
-        if fwd == 'bf16':
-            acts = fwd_out.acts
-            M = N * T
-            gpu = dict(a1=acts.a1[:M], a2=acts.a2[:M], a3=acts.a3[:M], a4=acts.a4[:M],
-                       logits=fwd_out.flat_logits, value=fwd_out.flat_value)
-            gpu = {k: v.cpu().double().numpy() for k, v in gpu.items()}
-            tg_gpu = s.run(obj.target_values, feed_dict=feed)
+        acts = fwd_out.acts
+        M = N * T
+        gpu = dict(a1=acts.a1[:M], a2=acts.a2[:M], a3=acts.a3[:M], a4=acts.a4[:M],
+                   logits=fwd_out.flat_logits, value=fwd_out.flat_value)
+        gpu = {k: v.cpu().double().numpy() for k, v in gpu.items()}
+        tg_gpu = s.run(obj.target_values, feed_dict=feed)
         s.run(op, feed_dict=feed)
         torch.cuda.synchronize()
     obs, act, rew, term, nxt, _ = [x for x in data]
     M = N * T
-    if fwd == 'bf16':
-        full = dict(gpu, x=obs.cpu().numpy().reshape(M, 84, 84, 4).astype(np.float64) / 255.0)
-        full['a3f'] = full['a3'].reshape(M, -1)
-        tg = np.asarray(tg_gpu, np.float64).reshape(-1)
-        # the bf16 tower is within 1e-2 of float64 (test_bf16_forward_mode); the
-        # update is only meaningful if its inputs are close to the f32 forward
-        ref_fwd = oracle.forward(p_before, obs.cpu().numpy().reshape(M, 84, 84, 4), A, C3)
-        rel = np.abs(full['logits'] - ref_fwd['logits']).max() / np.abs(ref_fwd['logits']).max()
-        assert rel < 1e-2, rel
-    else:
-        full = oracle.forward(p_before, obs.cpu().numpy().reshape(M, 84, 84, 4), A, C3)
-        vb = oracle.forward(p_before, nxt.cpu().numpy(), A, C3)['value']
-        tg = oracle.targets_f64(rew.cpu().numpy(), term.cpu().numpy(), vb, 0.99).reshape(-1)
+    # the GPU forward and targets against float64 (f32: rel 1e-5; the bf16 tower
+    # within 1e-2, test_bf16_forward_mode)
+    ref_fwd = oracle.forward(p_before, obs.cpu().numpy().reshape(M, 84, 84, 4), A, C3)
+    vb = oracle.forward(p_before, nxt.cpu().numpy(), A, C3)['value']
+    tg_ref = oracle.targets_f64(rew.cpu().numpy(), term.cpu().numpy(), vb, 0.99).reshape(-1)
+    ftol = 1e-2 if fwd == 'bf16' else 1e-5
+    for k in ('a1', 'a2', 'a3', 'a4', 'logits', 'value'):
+        r = ref_fwd[k].reshape(gpu[k].shape)
+        rel = np.abs(gpu[k] - r).max() / np.abs(r).max()
+        assert rel < ftol, ('forward', k, rel)
+    tg = np.asarray(tg_gpu, np.float64).reshape(-1)
+    assert np.abs(tg - tg_ref).max() <= (1e-2 if fwd == 'bf16' else 1e-5) * max(1.0, np.abs(tg_ref).max())
+    # the update's inputs: the GPU's own forward
+    full = dict(gpu, x=obs.cpu().numpy().reshape(M, 84, 84, 4).astype(np.float64) / 255.0)
+    full['a3f'] = full['a3'].reshape(M, -1)
     lg = oracle.a2c_loss_and_head_grads(full['logits'], full['value'], act.cpu().numpy().reshape(-1), tg)
     grads, _, afac = oracle.backward(p_before, full, lg['dlogits'], lg['dvalue'], A, C3, with_a_factors=True)
     g_pi, g_v, y = oracle.sampled_head_grads(logits32, 0x4b464143, 0, 40)
