@@ -559,16 +559,18 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // the fused tail + next tower at the rollout's split-K count; any other (or
   // no) split runs the tail and then the next step's tower as two launches
   // (small batches run the 16-wave tower, which the fused tail does not host)
-  const bool fuse_next = nxt && split && (nz == 8 || nz == 16) && B > wide_tower_max();
+  // (fused at the split counts the plan produces: 8 at the rollout batch; 14 / 16
+  // below 128 images -- K = 1568 / 3136 in chunks of 7 / 13 k16-steps)
+  const bool fuse_next = nxt && split && (nz == 8 || nz == 14 || nz == 16) && B > wide_tower_max();
 #define ACMI_HEADS(NZ)                                                                          \
-  if (tail && fuse_next && (NZ == 8 || NZ == 16)) {                                             \
+  if (tail && fuse_next && (NZ == 8 || NZ == 14 || NZ == 16)) {                                 \
     if (h16)                                                                                    \
-      hipLaunchKernelGGL((rollout_tail_tower_kernel<NZ == 16 ? 16 : 8, C3, true>), dim3(B), hb, 0, s, hp, nz, \
+      hipLaunchKernelGGL((rollout_tail_tower_kernel<NZ == 16 ? 16 : NZ == 14 ? 14 : 8, C3, true>), dim3(B), hb, 0, s, hp, nz, \
                          P + L.off[7], a->a4, st * 512, B, P + L.off[8], P + L.off[9],          \
                          P + L.off[10], P + L.off[11], L.A, a->logits, st * a->ld_logits, hv, st, \
                          *tail, ntw);                                                           \
     else                                                                                        \
-      hipLaunchKernelGGL((rollout_tail_tower_kernel<NZ == 16 ? 16 : 8, C3, false>), dim3(B), hb, 0, s, hp, nz, \
+      hipLaunchKernelGGL((rollout_tail_tower_kernel<NZ == 16 ? 16 : NZ == 14 ? 14 : 8, C3, false>), dim3(B), hb, 0, s, hp, nz, \
                          P + L.off[7], a->a4, st * 512, B, P + L.off[8], P + L.off[9],          \
                          P + L.off[10], P + L.off[11], L.A, a->logits, st * a->ld_logits, hv, st, \
                          *tail, ntw);                                                           \

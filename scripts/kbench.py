@@ -122,6 +122,8 @@ if __name__ == '__main__':
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 4096)
     elif what == 'c2':  # conv2 dX site (ACMI_PROF_CONV2_DX = 5)
         backward(int(sys.argv[2]) if len(sys.argv) > 2 else 10240, False, 5, reps=10)
+    elif what == 'backward1x':  # the conv2 band launch alone (site 2), ten timed reps
+        backward(int(sys.argv[2]) if len(sys.argv) > 2 else 10240, True, 2, reps=10)
     elif what == 'backward1':  # a short run for PMC passes
         backward(int(sys.argv[2]) if len(sys.argv) > 2 else 10240, True, 2, reps=2)
     elif what == 'backward':
