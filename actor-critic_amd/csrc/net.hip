@@ -561,7 +561,7 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // (small batches run the 16-wave tower, which the fused tail does not host)
   // (fused at the split counts the plan produces: 8 at the rollout batch; 14 / 16
   // below 128 images -- K = 1568 / 3136 in chunks of 7 / 13 k16-steps)
-  const bool fuse_next = nxt && split && (nz == 8 || nz == 14 || nz == 16) && B > wide_tower_max();
+  const bool fuse_next = nxt && split && (nz == 8 || nz == 14 || nz == 16);
 #define ACMI_HEADS(NZ)                                                                          \
   if (tail && fuse_next && (NZ == 8 || NZ == 14 || NZ == 16)) {                                 \
     if (h16)                                                                                    \

@@ -69,7 +69,6 @@ __device__ __forceinline__ void tow_put(char* img, int p, int x, int ch, float v
   *reinterpret_cast<_Float16*>(img + tow_elem<C, S>(p, x, ch, 1)) = l;
 }
 
-
 // Prepared weights (acmi_conv_prepare): conv1/conv2/conv3 weights split once
 // per parameter version into the f16 h/l parts of every lane's B fragment,
 // fragment-major -- [k16 step][32-col tile][part h,l][lane] x 16 B -- so the
@@ -234,257 +233,15 @@ struct TowB {
 };
 
 
-// B-fragment prefetch depth of the 16-wave body: a wave there multiplies one
-// tile per k-step (2-3 MFMAs), so the L2 round trip of the weights needs more
-// steps in flight than in the 4-wave body (3.5 tiles per k-step)
-#ifndef ACMI_WIDE_DEPTH
-#define ACMI_WIDE_DEPTH 6
-#endif
-constexpr int kWideDepth = ACMI_WIDE_DEPTH;
-#ifndef ACMI_TOW_PROBE  // 4-wave body timing probes (wrong results): 1 stop after conv1, 2 after conv2,
-#define ACMI_TOW_PROBE 0  // 4 no global stores, 8 stop after the image load
-#endif
-#ifndef ACMI_WIDE_PROBE  // timing probes (wrong results): 1 stop after conv1, 2 after conv2, 4 no global stores
-#define ACMI_WIDE_PROBE 0
-#endif
-// The tower of one image on 16 waves (tower_body's NW = 16; the image already
-// in LDS).  The units of the 4-wave body, one per wave:
-//   conv1  waves 0-11 row tile w (full K); waves 12 / 13 tile 12's k-steps 0-7 /
-//          8-15, added half 0 + half 1;
-//   conv2  waves 0-3 tile (w / 2, column tile w % 2) (full K); waves 4-7 row
-//          tile 2, column tile w % 2, K half (w - 4) / 2, added half 0 + half 1;
-//   conv3  waves 0-3 exactly as in the 4-wave body.
-// Same k orders, same additions: bit-identical to it.
-template <int C3, bool H16>
-__device__ __forceinline__ void tower_wide(const float* b1, const float* b2, const float* b3, float* a1g,
-                                           float* a2g, float* a3g, long long st, const char* prep, uint32_t* m1g,
-                                           uint32_t* m2g, uint32_t* m3g, char* lds, long long img) {
-  using P = TowerPrep<C3>;
-  const unsigned* hdr = reinterpret_cast<const unsigned*>(prep + P::HDR);
-  const float sw1 = f16x2_scale_of_bits(hdr + kTowMaxW1), sw2 = f16x2_scale_of_bits(hdr + kTowMaxW2);
-  const float sw3 = f16x2_scale_of_bits(hdr + kTowMaxW3), sa1 = f16x2_scale_of_bits(hdr + kTowMaxA1);
-  const float sa2 = f16x2_scale_of_bits(hdr + kTowMaxA2);
-  char* const imgL = lds;
-  char* const a1L = lds + kTowObs;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int col = lane & 31, kh8 = lane >> 5;
+#ifndef ACMI_TOW_PROBE  // timing probes (wrong results): 1 stop after conv1, 2 after conv2, 4 no global
+#define ACMI_TOW_PROBE 0  // stores, 8 stop after the image load, 16 no conv1 epilogue, 32 no conv1 MFMAs,
+#endif                    // 64 conv1 without the weight loads' dependency
 
-  // ---- conv1 ----
-  {
-    const int tile = min(wave, 12);
-    const bool active = wave < 14;
-    const int p0 = min(32 * tile + col, 399);
-    const int oh = p0 / 20, ow = p0 - oh * 20;
-    const int abase = (4 * oh * 84 + 4 * ow) * 4 + 8 * kh8;
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    TowB<32, H16, kWideDepth> bw{prep + P::O1};
-    if (active) {
-#pragma unroll
-      for (int i = 0; i < kWideDepth; ++i) bw.fetch(i, 0, lane, i);
-    }
-    __syncthreads();
-    if (active) {
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        if (s + kWideDepth < 16) bw.fetch(s + kWideDepth, 0, lane, (s + kWideDepth) % (kWideDepth + 1));
-        f16x8 b[2];
-        bw.get(s % (kWideDepth + 1), b);
-        if (wave >= 12 && (s >> 3) != wave - 12) continue;
-        const int koff = (s >> 1) * 336 + 16 * (s & 1);
-        const f16x8 a = u8x8_to_f16(*reinterpret_cast<const uint2*>(imgL + abase + koff));
-        if constexpr (!H16) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[0], acc, 0, 0, 0);
-      }
-    }
-    const float bias = b1[col], inv1 = 16777216.0f / sw1;
-    float* g = a1g + img * st * 12800;
-    uint32_t* mg = m1g ? m1g + img * st * 400 : nullptr;
-    auto emit1 = [&](int p, float v) {
-      v = fmaxf(__builtin_fmaf(v * inv1, 1.0f / 255.0f, bias), 0.f);
-      tow_put<32, 2>(a1L, p, p % 20, col, v, sa1);
-      if constexpr (!(ACMI_WIDE_PROBE & 4)) g[p * 32 + col] = v;
-      const unsigned long long bal = __ballot(v > 0.f);
-      if (mg && col == 0) mg[p] = (uint32_t)(bal >> (lane & 32));
-    };
-    if (wave < 12) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) emit1(32 * wave + tow_row(r, lane), acc[r]);
-    }
-    float* scr12 = reinterpret_cast<float*>(lds + kTowLds);  // [16 rows][32]
-    if (wave == 13) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (tow_row(r, lane) < 16) scr12[tow_row(r, lane) * 32 + col] = acc[r];
-    }
-    __syncthreads();
-    if (wave == 12) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = tow_row(r, lane);
-        if (m < 16) emit1(384 + m, acc[r] + scr12[m * 32 + col]);
-      }
-    }
-  }
-  __syncthreads();
-  if constexpr (ACMI_WIDE_PROBE & 1) return;
-
-  // ---- conv2 ----
-  {
-    const bool full = wave < 4, half = wave >= 4 && wave < 8;
-    const int ct = wave & 1;
-    const int rt = full ? (wave >> 1) : 2;
-    const int hk0 = half ? 16 * ((wave - 4) >> 1) : 0;
-    const int p0 = min(32 * rt + col, 80);
-    const int oh = p0 / 9, ow = p0 - oh * 9;
-    const int pin = 2 * oh * 20 + 2 * ow, pxx = 2 * ow;
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    // k-steps hk0 .. hk0 + NS2 - 1 in order (the loop fully unrolled: the B slots
-    // are compile-time register indices)
-    auto run2 = [&](auto NSc) {
-      constexpr int NS2 = decltype(NSc)::value;
-      TowB<64, H16, kWideDepth> bw{prep + P::O2};
-#pragma unroll
-      for (int i = 0; i < kWideDepth; ++i) bw.fetch(hk0 + i, ct, lane, i);
-#pragma unroll
-      for (int i = 0; i < NS2; ++i) {
-        const int s = hk0 + i;
-        if (i + kWideDepth < NS2) bw.fetch(s + kWideDepth, ct, lane, (i + kWideDepth) % (kWideDepth + 1));
-        f16x8 b[2];
-        bw.get(i % (kWideDepth + 1), b);
-        const int tap = s >> 1, kh = tap >> 2, kw = tap & 3;
-        const int c8 = 2 * (s & 1) + kh8;
-        const int p = pin + kh * 20 + kw, x = pxx + kw;
-        f16x8 a[2];
-        a[0] = *reinterpret_cast<const f16x8*>(a1L + tow_pos<32, 2>(p, x, c8));
-        if constexpr (!H16) a[1] = *reinterpret_cast<const f16x8*>(a1L + tow_pos<32, 2>(p, x, 4 + c8));
-        if constexpr (H16) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], acc, 0, 0, 0);
-        else acc = mfma_x2(a, b, acc);
-      }
-    };
-    if (full) run2(std::integral_constant<int, 32>{});
-    else if (half) run2(std::integral_constant<int, 16>{});
-    float* scr = reinterpret_cast<float*>(imgL + 81 * 64 * 4);  // [ct][17 rows][32]
-    if (wave >= 6 && wave < 8) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = tow_row(r, lane);
-        if (m < 17) scr[(ct * 17 + m) * 32 + col] = acc[r];
-      }
-    }
-    __syncthreads();
-    const int c = 32 * ct + col;
-    const float bias = b2[c], inv2 = 1.0f / (sa1 * sw2);
-    float* g = a2g + img * st * 5184;
-    uint32_t* mg = m2g ? m2g + img * st * 162 : nullptr;
-    auto emit = [&](int p, float v) {
-      v = fmaxf(__builtin_fmaf(v, inv2, bias), 0.f);
-      tow_put<64, 1>(imgL, p, p % 9, c, v, sa2);
-      if constexpr (!(ACMI_WIDE_PROBE & 4)) g[p * 64 + c] = v;
-      const unsigned long long bal = __ballot(v > 0.f);
-      if (mg && col == 0) mg[2 * p + ct] = (uint32_t)(bal >> (lane & 32));
-    };
-    if (full) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) emit(32 * rt + tow_row(r, lane), acc[r]);
-    }
-    if (wave >= 4 && wave < 6) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = tow_row(r, lane);
-        if (m < 17) emit(64 + m, acc[r] + scr[(ct * 17 + m) * 32 + col]);
-      }
-    }
-  }
-  __syncthreads();
-  if constexpr (ACMI_WIDE_PROBE & 2) return;
-
-  // ---- conv3 (waves 0-3, as the 4-wave body) ----
-  {
-    constexpr int NS = 36;
-    const bool active = wave < 4;
-    const int rt = wave & 1;
-    const int ct = C3 == 64 ? ((wave >> 1) & 1) : 0;
-    const int s0 = C3 == 64 ? 0 : 18 * ((wave >> 1) & 1);
-    const int p0 = min(32 * rt + col, 48);
-    const int oh = p0 / 7, ow = p0 - oh * 7;
-    const int pin = oh * 9 + ow;
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    constexpr int NWK = C3 == 64 ? NS : NS / 2;
-    if (active) {
-      TowB<C3, H16, kWideDepth> bw{prep + P::O3};
-#pragma unroll
-      for (int i = 0; i < kWideDepth; ++i) bw.fetch(s0 + i, ct, lane, i);
-#pragma unroll
-      for (int i = 0; i < NWK; ++i) {
-        const int ss = s0 + i;
-        if (i + kWideDepth < NWK) bw.fetch(ss + kWideDepth, ct, lane, (i + kWideDepth) % (kWideDepth + 1));
-        f16x8 b[2];
-        bw.get(i % (kWideDepth + 1), b);
-        const int tap = ss >> 2, kh = tap / 3, kw = tap - kh * 3;
-        const int c8 = 2 * (ss & 3) + kh8;
-        const int p = pin + kh * 9 + kw, x = ow + kw;
-        f16x8 a[2];
-        a[0] = *reinterpret_cast<const f16x8*>(imgL + tow_pos<64, 1>(p, x, c8));
-        if constexpr (!H16) a[1] = *reinterpret_cast<const f16x8*>(imgL + tow_pos<64, 1>(p, x, 8 + c8));
-        if constexpr (H16) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], acc, 0, 0, 0);
-        else acc = mfma_x2(a, b, acc);
-      }
-    }
-    const int c = 32 * ct + col;
-    const float bias = b3[c], inv3 = 1.0f / (sa2 * sw3);
-    float* g = a3g + img * st * (49 * C3);
-    uint32_t* mg = m3g ? m3g + img * st * (49 * C3 / 32) : nullptr;
-    auto emit3 = [&](int p, float v) {
-      v = fmaxf(__builtin_fmaf(v, inv3, bias), 0.f);
-      if constexpr (!(ACMI_WIDE_PROBE & 4)) g[p * C3 + c] = v;
-      const unsigned long long bal = __ballot(v > 0.f);
-      if (mg && col == 0) mg[p * (C3 / 32) + ct] = (uint32_t)(bal >> (lane & 32));
-    };
-    if constexpr (C3 == 32) {
-      float* scr = reinterpret_cast<float*>(a1L);  // [rt][32 rows][32]
-      if (wave >= 2 && wave < 4) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) scr[(rt * 32 + tow_row(r, lane)) * 32 + col] = acc[r];
-      }
-      __syncthreads();
-      if (wave < 2) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int p = 32 * rt + tow_row(r, lane);
-          if (p < 49) emit3(p, acc[r] + scr[(rt * 32 + tow_row(r, lane)) * 32 + col]);
-        }
-      }
-    } else {
-      if (active) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int p = 32 * rt + tow_row(r, lane);
-          if (p < 49) emit3(p, acc[r]);
-        }
-      }
-    }
-  }
-}
-
-// H16 (acmi_set_forward_mode ACMI_FWD_BF16): one f16 MFMA per product on the h
-// parts alone -- every operand rounded once to f16 after its power-of-two scale
-// (11-bit significands, u8 pixels exact; a bf16 forward's precision or better).
 // The tower of image `img` by one 256-thread block over the caller's LDS
 // (kTowLds + kTowScr bytes).  IMG_IN_LDS: the u8 image is already in the
 // image region (written there by the fused rollout tail's env step, which
 // also stored it to obs) and is not loaded again.
-// NW: waves per image.  4 (a 256-thread block, two blocks per CU: the rollout
-// batch of 512 images in one round); 16 (a 1024-thread block, one image per CU:
-// small batches, where the per-image chain and not the CU count sets the time).
-// Both compute every output from the same (row tile, K range) units in the same
-// k order and add split-K halves in the same order: bit-identical activations.
-template <int C3, bool H16, bool IMG_IN_LDS, int NW = 4>
+template <int C3, bool H16, bool IMG_IN_LDS>
 __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_stride, const float* b1,
                                            const float* b2, const float* b3, float* a1g, float* a2g, float* a3g,
                                            long long st, const char* prep, uint32_t* m1g, uint32_t* m2g,
@@ -498,13 +255,9 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
   char* const a1L = lds + kTowObs;  // a1; later conv3 scratch
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kh8 = lane >> 5;
-  if constexpr (NW == 16 && (ACMI_WIDE_PROBE & 32)) {  // probe: an empty block
-    if (tid == 0 && sw1 == 3.f) a1g[img] = sa2;
-    return;
-  }
 
   if constexpr (!IMG_IN_LDS) {  // the u8 image: all of a thread's 16-byte loads before its LDS stores
-    constexpr int NT = 64 * NW;
+    constexpr int NT = 256;
     constexpr int N16 = kTowObs / 16, NPT = (N16 + NT - 1) / NT;
     const uint4* src = reinterpret_cast<const uint4*>(obs + img * img_stride);
     uint4 v[NPT];
@@ -514,16 +267,6 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     for (int q = 0; q < NPT; ++q)
       if (tid + NT * q < N16) reinterpret_cast<uint4*>(imgL)[tid + NT * q] = v[q];
   }
-  if constexpr (NW == 16) {
-    if constexpr (ACMI_WIDE_PROBE & 16) {  // probe: the image load only
-      __syncthreads();
-      if (threadIdx.x == 0 && (unsigned char)lds[threadIdx.x + 7] == 255 && lds[5000] == 3) a1g[img] = 1.f;
-      return;
-    }
-    tower_wide<C3, H16>(b1, b2, b3, a1g, a2g, a3g, st, prep, m1g, m2g, m3g, lds, img);
-    return;
-  }
-
   // ---- conv1: [84][84][4] u8 -> a1 [20][20][32] -------------------------------
   {
     // row tiles w, w+4, w+8 of 13 for logical wave w; the 13th tile (rows
@@ -557,11 +300,19 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       if (s + kTowDepth < 16) bw.fetch(s + kTowDepth, 0, lane, (s + kTowDepth) % kTowSlots);
       f16x8 b[2];
       bw.get(s % kTowSlots, b);
+      if constexpr (ACMI_TOW_PROBE & 64) {  // probe: constant weights (no B dependency)
+        b[0] = f16x8{1, 1, 1, 1, 1, 1, 1, 1};
+        b[1] = b[0];
+      }
       const int koff = (s >> 1) * 336 + 16 * (s & 1);  // kernel row kh = s/2, kw half
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (u == 3 && (w < 2 || (s >> 3) != w - 2)) continue;
         const f16x8 a = u8x8_to_f16(*reinterpret_cast<const uint2*>(imgL + abase[u] + koff));
+        if constexpr (ACMI_TOW_PROBE & 32) {  // probe: no MFMAs (the operands kept live)
+          acc[u][s & 15] += (float)a[s & 7] + (float)b[0][s & 7];
+          continue;
+        }
         if constexpr (!H16) acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[1], acc[u], 0, 0, 0);
         acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[0], acc[u], 0, 0, 0);
       }
@@ -572,6 +323,10 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     // (the callers' active lanes are whole 32-lane halves: lanes 0 / 32 write the
     // ReLU' word of their half's pixel)
     auto emit1 = [&](int p, float v) {
+      if constexpr (ACMI_TOW_PROBE & 16) {  // probe: no conv1 epilogue (one store keeps acc live)
+        if (v == 12345.f) g[p] = v;
+        return;
+      }
       v = fmaxf(__builtin_fmaf(v * inv1, 1.0f / 255.0f, bias), 0.f);
       tow_put<32, 2>(a1L, p, p % 20, col, v, sa1);
       if constexpr (!(ACMI_TOW_PROBE & 4)) g[p * 32 + col] = v;
@@ -765,42 +520,12 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
   tower_body<C3, H16, false>(obs, img_stride, b1, b2, b3, a1g, a2g, a3g, st, prep, m1g, m2g, m3g, lds,
                              blockIdx.x);
 }
-// one image per 16-wave block (small batches)
-template <int C3, bool H16 = false>
-__global__ __launch_bounds__(1024) void tower_wide_kernel(const uint8_t* obs, long long img_stride,
-                                                          const float* b1, const float* b2, const float* b3,
-                                                          float* a1g, float* a2g, float* a3g, long long st,
-                                                          const char* prep, uint32_t* m1g, uint32_t* m2g,
-                                                          uint32_t* m3g) {
-  __shared__ __attribute__((aligned(16))) char lds[kTowLds + kTowScr];
-  tower_body<C3, H16, false, 16>(obs, img_stride, b1, b2, b3, a1g, a2g, a3g, st, prep, m1g, m2g, m3g, lds,
-                                 blockIdx.x);
-}
-
-// images up to which a forward runs the 16-wave tower (one image per CU; the
-// 4-wave blocks hold two images per CU, which only a batch beyond 256 needs):
-// ACMI_WIDE_TOWER_MAX, default 0 (measured no faster: 22.2 vs 22.5 us per launch
-// at 32 images -- the per-image time is not the waves' k-step chains)
-inline int wide_tower_max() {
-  static const int v = getenv("ACMI_WIDE_TOWER_MAX") ? atoi(getenv("ACMI_WIDE_TOWER_MAX")) : 0;
-  return v;
-}
-
 // prep: acmi_conv_prepare's fragments + bounds (required)
 template <int C3>
 inline void launch_tower(const uint8_t* obs, long long img_stride, int B, const float* P,
                          const long long* off, float* a1, float* a2, float* a3, long long st,
                          const void* prep, hipStream_t s, bool h16, uint32_t* m1, uint32_t* m2, uint32_t* m3) {
   const char* pp = static_cast<const char*>(prep);
-  if (B <= wide_tower_max()) {
-    if (h16)
-      hipLaunchKernelGGL((tower_wide_kernel<C3, true>), dim3(B), dim3(1024), 0, s, obs, img_stride, P + off[1],
-                         P + off[3], P + off[5], a1, a2, a3, st, pp, m1, m2, m3);
-    else
-      hipLaunchKernelGGL((tower_wide_kernel<C3, false>), dim3(B), dim3(1024), 0, s, obs, img_stride, P + off[1],
-                         P + off[3], P + off[5], a1, a2, a3, st, pp, m1, m2, m3);
-    return;
-  }
   if (h16)
     hipLaunchKernelGGL((tower_kernel<C3, true>), dim3(B), dim3(256), 0, s, obs, img_stride, P + off[1],
                        P + off[3], P + off[5], a1, a2, a3, st, pp, m1, m2, m3);

@@ -684,37 +684,3 @@ def test_kfac_pack_unpack_round_trip(lib, cuda):
     _lib.call('acmi_kfac_unpack', A, C3, 3, _lib.ptr(pk), _lib.ptr(back), _lib.stream_handle())
     torch.cuda.synchronize()
     assert torch.equal(back.cpu(), stats)
-
-
-@pytest.mark.parametrize('C3,h16', [(32, False), (64, False), (32, True)], ids=['c32', 'c64', 'c32-bf16fwd'])
-def test_wide_tower_bit_identical_to_four_wave_tower(lib, cuda, C3, h16):
-    """Small batches (<= ACMI_WIDE_TOWER_MAX = 128 images) run the conv tower on 16
-    waves per image (tower.hpp tower_wide: one (row tile, K range) unit per wave),
-    the rollout batch on 4 waves per image (two images per CU).  Both compute every
-    output from the same units in the same k order and add the split-K halves in
-    the same order: the first 40 images of a 300-image forward (4-wave blocks) and
-    a 40-image forward of the same images (16-wave blocks) agree bit for bit --
-    a1..a3 and the ReLU' masks."""
-    A, B, Bs = 4, 300, 40
-    assert Bs <= 128 < B
-    params = rand_params(A, C3, cuda, seed=51)
-    g = torch.Generator().manual_seed(52)
-    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
-    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
-    net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr())
-    prev = lib.acmi_get_forward_mode()
-    _lib.call('acmi_set_forward_mode', _lib.FWD_BF16 if h16 else _lib.FWD_F32)
-    try:
-        _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), _lib.stream_handle())
-        out = []
-        for n in (B, Bs):
-            t, acts = alloc_acts(n, A, C3, cuda, masks=True)
-            _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, n, ctypes.byref(acts), 1,
-                      _lib.stream_handle())
-            out.append(t)
-        torch.cuda.synchronize()
-    finally:
-        _lib.call('acmi_set_forward_mode', prev)
-    for k in ('a1', 'a2', 'a3', 'm1', 'm2', 'm3'):  # (fc4's K split differs with the batch)
-        assert torch.equal(out[0][k][:Bs], out[1][k]), k
-    assert out[1]['a3'].abs().sum() > 0
