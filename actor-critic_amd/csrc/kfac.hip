@@ -78,10 +78,11 @@ struct MatSet {
   int count;
   int n[MAXM];        // logical size
   int np[MAXM];       // padded to GJB
-  long long m_off[MAXM];    // np x np doubles in ws
-  long long row_off[MAXM];  // GJB x np doubles (Rrow')
-  long long col_off[MAXM];  // np x GJB doubles (Ccol)
+  long long m_off[MAXM];    // np x np doubles in ws: the matrix before even steps
+  long long m1_off[MAXM];   // np x np doubles: before odd steps (the sweep ping-pongs)
+  long long pi_off[MAXM];   // 2 x GJB x GJB doubles: the pivot inverse of even / odd steps
   int id[MAXM];       // original matrix index (for active subsets)
+  int tile0[MAXM + 1];  // gj_step_kernel: first tile block of each matrix (prefix sums)
 };
 
 // traces of the 11 factors (normalised by dimension) -> tr[f]
@@ -140,15 +141,15 @@ __global__ void damp_kernel(DampSet d, const double* tr, double* ws) {
 }
 
 // Gauss-Jordan (sweep) inverse of the GJB x GJB pivot block in LDS, all 256
-// threads: per sweep t every thread reads the pivot row / column entries of its
+// threads: per sweep every thread reads the pivot row / column entries of its
 // four elements from one LDS image and writes the four updated elements to the
-// other (ping-pong: one barrier per sweep; 32 sweeps end in P).  1/pivot from
-// v_rcp_f64 and two Newton steps (within an ulp of the IEEE quotient, a third
-// of the division sequence's latency).  The sweep was 12 of a panel launch's
-// 22 us with the division and two barriers per sweep.  (One wave doing all
-// 32 x 32 elements without barriers -- 16 per lane -- measured slower: 2.52 vs
-// 1.69 ms per inverse; the longer per-lane LDS chains cost more than the
-// barriers.)
+// other (ping-pong: one barrier per sweep).  1/pivot from v_rcp_f64 and two
+// Newton steps (within an ulp of the IEEE quotient, a third of the division
+// sequence's latency).  The 32 one-pivot sweeps were 12 us of the 22 us panel
+// launch with the division and two barriers per sweep; pairs of pivots per
+// sweep (below) halve the chain.  (One wave doing all 32 x 32 elements without
+// barriers -- 16 per lane -- measured slower: 2.52 vs 1.69 ms per inverse; the
+// longer per-lane LDS chains cost more than the barriers.)
 __device__ __forceinline__ double recip_f64(double d) {
   double r = __builtin_amdgcn_rcp(d);
   double e = fma(-d, r, 1.0);
@@ -156,9 +157,50 @@ __device__ __forceinline__ double recip_f64(double d) {
   e = fma(-d, r, 1.0);
   return fma(r, e, r);
 }
+#ifndef ACMI_GJ_PAIRS
+#define ACMI_GJ_PAIRS 1
+#endif
 __device__ void pivot_inverse(double (*P)[GJB + 1], double (*Q)[GJB + 1]) {
   const int tid = threadIdx.x;
   const int c = tid & (GJB - 1), r0 = tid >> 5;  // rows r0, r0+8, r0+16, r0+24
+#if ACMI_GJ_PAIRS
+  // Two pivots per sweep (16 sweeps, 16 barriers): pivot pair K = {t, t+1} with
+  // its 2 x 2 inverse D (closed form, 1/det by recip_f64):
+  //   M_KK <- D,  M_Kj <- D M_Kj,  M_iK <- -M_iK D,  M_ij <- M_ij - M_iK D M_Kj
+  // -- the composition of the two one-pivot sweeps, with half their dependent
+  // LDS round trips, reciprocals and barriers.  The 2 x 2 diagonal blocks of the
+  // damped SPD factors and of their Schur complements are SPD (det > 0).
+  static_assert(GJB % 4 == 0, "an even number of pair sweeps ends in P");
+  for (int t = 0; t < GJB; t += 4) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double (*src)[GJB + 1] = h ? Q : P;
+      double (*dst)[GJB + 1] = h ? P : Q;
+      const int k0 = t + 2 * h;
+      const double a = src[k0][k0], b = src[k0][k0 + 1], e = src[k0 + 1][k0], d = src[k0 + 1][k0 + 1];
+      const double idet = recip_f64(fma(a, d, -(b * e)));
+      const double D00 = d * idet, D01 = -b * idet, D10 = -e * idet, D11 = a * idet;
+      const double s0 = src[k0][c], s1 = src[k0 + 1][c];
+      const double u0 = fma(D00, s0, D01 * s1), u1 = fma(D10, s0, D11 * s1);  // (D M_Kc)
+      const int ck = c - k0;
+      const double dc0 = ck == 0 ? D00 : D01, dc1 = ck == 0 ? D10 : D11;  // column c of D (c in K)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = r0 + 8 * q;
+        const double m0 = src[r][k0], m1 = src[r][k0 + 1];
+        double v;
+        if (r == k0 || r == k0 + 1) {
+          const double w = r == k0 ? u0 : u1;
+          v = (ck == 0 || ck == 1) ? (r == k0 ? dc0 : dc1) : w;
+        } else {
+          v = (ck == 0 || ck == 1) ? -fma(m0, dc0, m1 * dc1) : src[r][c] - fma(m0, u0, m1 * u1);
+        }
+        dst[r][c] = v;
+      }
+      __syncthreads();
+    }
+  }
+#else
   static_assert(GJB % 2 == 0, "an even number of sweeps ends in P");
   for (int t = 0; t < GJB; t += 2) {
 #pragma unroll
@@ -181,6 +223,7 @@ __device__ void pivot_inverse(double (*P)[GJB + 1], double (*Q)[GJB + 1]) {
       __syncthreads();
     }
   }
+#endif
 }
 
 // Symmetric sweep: the damped factors are symmetric, and the sweep operator
@@ -193,83 +236,119 @@ __device__ __forceinline__ double gj_sym(const double* M, int np, int r, int c) 
   return r <= c ? M[(long long)r * np + c] : M[(long long)c * np + r];
 }
 
-constexpr int PANEL_COLS = 64;
-// grid: (column chunks of PANEL_COLS, active matrices); thread (column j, pivot-row
-// quarter) forms 8 rows of Rrow' = Pinv M[kb.., j] (8 accumulators, 256 LDS reads)
-__global__ __launch_bounds__(256) void gj_panel_kernel(MatSet s, double* ws, int step) {
-  const int mi = blockIdx.y;
+// One kernel per pivot step k (pivot block rows / columns kb = 32k .. kb + 31),
+// reading the matrix M_k and writing M_{k+1} (two buffers, ping-pong), with
+// the pivot inverse Pinv_k already computed -- by the previous step's kernel:
+//   blocks (m, 0): the NEXT pivot block of matrix m -- its 32 x 32 entries of
+//     M_{k+1} (the same sums, in the same order, as the tile block that stores
+//     them) and their 32-sweep inverse into Pinv_{k+1}, concurrently with
+//   blocks (m, 1 + t): upper-triangle 64 x 64 tile t of M_{k+1}: Rrow' =
+//     Pinv_k M_k[kb.., j] for the tile's columns (thread (column, 8 pivot rows)),
+//     the old pivot columns Ccol = M_k[i][kb..] of its rows, and 4 x 4 outputs
+//     per thread.
+// So a step is one launch whose critical path is a tile update or one pivot
+// inverse, not both in sequence: the sweep's 32 dependent barriers (12 us) used
+// to sit in a separate panel launch before every update (50 + 50 launches for the
+// 1568-wide factor, 1.69 ms per inverse).  Blocks (m, 0) come first in dispatch
+// order (grid x = matrix, y = 0 the pivot block).
+__device__ __forceinline__ const double* gj_in(const MatSet& s, int mi, int step, double* ws) {
+  return ws + ((step & 1) ? s.m1_off[mi] : s.m_off[mi]);
+}
+__device__ __forceinline__ double* gj_out(const MatSet& s, int mi, int step, double* ws) {
+  return ws + ((step & 1) ? s.m_off[mi] : s.m1_off[mi]);
+}
+
+// Pinv_0 of every matrix (blocks: matrices)
+__global__ __launch_bounds__(256) void gj_first_kernel(MatSet s, double* ws) {
+  const int mi = blockIdx.x;
   const int np = s.np[mi];
-  const int c0 = blockIdx.x * PANEL_COLS;
-  if (c0 >= np) return;
-  const int kb = step * GJB;
-  double* M = ws + s.m_off[mi];
-  double* R = ws + s.row_off[mi];
-  double* C = ws + s.col_off[mi];
+  const double* M = ws + s.m_off[mi];
   __shared__ double P[GJB][GJB + 1];
   __shared__ double Q[GJB][GJB + 1];
-  for (int e = threadIdx.x; e < GJB * GJB; e += 256)
-    P[e / GJB][e % GJB] = M[(long long)(kb + e / GJB) * np + kb + e % GJB];
-  const int j = c0 + (threadIdx.x & (PANEL_COLS - 1));
-  const int t0 = (threadIdx.x >> 6) * 8;  // this thread's 8 pivot rows
-  const bool jcol = j < np && !(j >= kb && j < kb + GJB);
-  // every load of the panel issued before the pivot sweep (none depends on it):
-  // the column of M this thread transforms, and the old pivot columns of the
-  // chunk's rows (Ccol) -- their latency hides behind the 32 sweeps
-  double col[GJB];
+  for (int e = threadIdx.x; e < GJB * GJB; e += 256) P[e / GJB][e % GJB] = M[(long long)(e / GJB) * np + e % GJB];
+  __syncthreads();
+  pivot_inverse(P, Q);
+  double* PI = ws + s.pi_off[mi];
+  for (int e = threadIdx.x; e < GJB * GJB; e += 256) PI[e] = P[e / GJB][e % GJB];
+}
+
+// LDS of gj_step_kernel (doubles): the tile blocks' Pv [32][33] | Cs [64][33] |
+// Rs [32][65]; the pivot block's four [32][33] arrays over the same words
+constexpr int kGjLds = GJB * (GJB + 1) + 64 * (GJB + 1) + GJB * (64 + 1);
+typedef double GjRow[GJB + 1];
+
+// block (m, 0): Pinv_{k+1} from M_k and Pinv_k
+__device__ void gj_next_pivot(const MatSet& s, double* ws, int step, int mi, double* lds) {
+  const int np = s.np[mi];
+  const int kb = step * GJB, nb = kb + GJB;
+  if (nb >= np) return;
+  const double* M = gj_in(s, mi, step, ws);
+  const double* PIk = ws + s.pi_off[mi] + (step & 1) * GJB * GJB;
+  double* PIn = ws + s.pi_off[mi] + ((step + 1) & 1) * GJB * GJB;
+  GjRow* Pv = reinterpret_cast<GjRow*>(lds);  // Pinv_k; later the sweep's Q
+  GjRow* Mr = Pv + GJB;  // M_k[kb + q][nb + c]: pivot rows over the next block's columns; later P
+  GjRow* Cn = Mr + GJB;  // M_k[nb + r][kb + t]: the next block's rows over the pivot columns
+  GjRow* Rn = Cn + GJB;  // Rrow' over the next block's columns
+  GjRow* P = Mr;
+  GjRow* Q = Pv;
+  const int c = threadIdx.x & (GJB - 1), r0 = threadIdx.x >> 5;
+  double oldv[4];
 #pragma unroll
-  for (int q = 0; q < GJB; ++q) col[q] = jcol ? gj_sym(M, np, kb + q, j) : 0.0;
-  const int rows = min(PANEL_COLS, np - c0);
-  double cold[PANEL_COLS * GJB / 256];
+  for (int u = 0; u < 4; ++u) {
+    const int r = r0 + 8 * u;
+    Pv[r][c] = PIk[r * GJB + c];
+    Mr[r][c] = gj_sym(M, np, kb + r, nb + c);
+    Cn[c][r] = M[(long long)(kb + r) * np + nb + c];  // (the upper element of (nb + c, kb + r))
+    oldv[u] = M[(long long)(nb + r) * np + nb + c];
+  }
+  __syncthreads();
 #pragma unroll
-  for (int u = 0; u < PANEL_COLS * GJB / 256; ++u) {
-    const int e = threadIdx.x + 256 * u;
-    cold[u] = e < rows * GJB ? gj_sym(M, np, c0 + e / GJB, kb + e % GJB) : 0.0;
+  for (int u = 0; u < 4; ++u) {  // the tile blocks' Rrow' sums (q order)
+    const int t = r0 + 8 * u;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int q = 0; q < GJB; ++q) acc += Pv[t][q] * Mr[q][c];
+    Rn[t][c] = acc;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {  // the tile blocks' update sums (t order)
+    const int r = r0 + 8 * u;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int t = 0; t < GJB; ++t) acc += Cn[r][t] * Rn[t][c];
+    P[r][c] = oldv[u] - acc;
   }
   __syncthreads();
   pivot_inverse(P, Q);
-  if (j < np) {
-    if (!jcol) {
 #pragma unroll
-      for (int t = 0; t < 8; ++t) R[(long long)(t0 + t) * np + j] = P[t0 + t][j - kb];
-    } else {
-      double acc[8];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) acc[t] = 0.0;
-#pragma unroll
-      for (int q = 0; q < GJB; ++q)
-#pragma unroll
-        for (int t = 0; t < 8; ++t) acc[t] += P[t0 + t][q] * col[q];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) R[(long long)(t0 + t) * np + j] = acc[t];
-    }
-  }
-  // Ccol[i][t] = M[i][kb + t] for the rows i of this chunk (old values): t
-  // fastest over consecutive threads, so reads and writes are coalesced
-#pragma unroll
-  for (int u = 0; u < PANEL_COLS * GJB / 256; ++u) {
-    const int e = threadIdx.x + 256 * u;
-    if (e < rows * GJB) C[(long long)(c0 + e / GJB) * GJB + e % GJB] = cold[u];
-  }
+  for (int u = 0; u < 4; ++u) PIn[(r0 + 8 * u) * GJB + c] = P[r0 + 8 * u][c];
 }
 
-// grid: (upper-triangle 64x64 tiles of the largest matrix, active matrices);
-// 64x64 tile, 4x4 per thread
-__global__ __launch_bounds__(256) void gj_update_kernel(MatSet s, double* ws, int step) {
-  const int mi = blockIdx.y;
+// grid: the active matrices' pivot blocks, then every matrix's upper-triangle
+// 64x64 tiles (tile0 prefix sums)
+__global__ __launch_bounds__(256) void gj_step_kernel(MatSet s, double* ws, int step) {
+  __shared__ double lds[kGjLds];
+  if ((int)blockIdx.x < s.count) {
+    gj_next_pivot(s, ws, step, blockIdx.x, lds);
+    return;
+  }
+  const int b = blockIdx.x - s.count;
+  int mi = 0;
+  while (mi + 1 < s.count && b >= s.tile0[mi + 1]) ++mi;
   const int np = s.np[mi];
   const int nt = (np + 63) / 64;
-  int ti = 0, rem = blockIdx.x;  // tile (ti, tj), ti <= tj, row-major over the upper triangle
+  int ti = 0, rem = b - s.tile0[mi];  // tile (ti, tj), ti <= tj, row-major over the upper triangle
   while (ti < nt && rem >= nt - ti) rem -= nt - ti, ++ti;
   if (ti >= nt) return;
   const int i0 = ti * 64, j0 = (ti + rem) * 64;
   const int kb = step * GJB;
-  double* M = ws + s.m_off[mi];
-  const double* R = ws + s.row_off[mi];
-  const double* C = ws + s.col_off[mi];
+  const double* M = gj_in(s, mi, step, ws);
+  double* Mo = gj_out(s, mi, step, ws);
+  const double* PIk = ws + s.pi_off[mi] + (step & 1) * GJB * GJB;
   const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
-  // the old value each of this thread's outputs starts from, loaded before the
-  // panel staging (pivot rows: Pinv M_kj from the row panel; other rows M_ij;
-  // pivot columns of other rows need none)
+  // every load issued up front: the old values of the non-pivot outputs, Pinv_k,
+  // this thread's column of the pivot rows, the old pivot columns of the rows
   double old[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
@@ -279,19 +358,45 @@ __global__ __launch_bounds__(256) void gj_update_kernel(MatSet s, double* ws, in
     for (int b = 0; b < 4; ++b) {
       const int j = j0 + tx + 16 * b;
       const bool jpiv = j >= kb && j < kb + GJB;
-      old[a][b] = (i >= np || j >= np) ? 0.0
-                  : ipiv               ? R[(long long)(i - kb) * np + j]
-                  : jpiv               ? 0.0
-                                       : M[(long long)i * np + j];
+      old[a][b] = (i >= np || j >= np || ipiv || jpiv) ? 0.0 : M[(long long)i * np + j];
     }
   }
-  __shared__ double Cs[64][GJB + 1];
-  __shared__ double Rs[GJB][64 + 1];
+  GjRow* Pv = reinterpret_cast<GjRow*>(lds);
+  GjRow* Cs = Pv + GJB;                                         // [64]
+  double (*Rs)[64 + 1] = reinterpret_cast<double (*)[64 + 1]>(Cs + 64);  // [GJB]
+  for (int e = threadIdx.x; e < GJB * GJB; e += 256) Pv[e / GJB][e % GJB] = PIk[e];
+  // (the upper-triangle element of (row, pivot column) / (pivot row, column) is a
+  // row segment of M on one side of the pivot and a column segment on the other:
+  // consecutive threads walk whichever index is contiguous in memory)
+  const bool rows_below = i0 >= kb + GJB, cols_left = j0 + 64 <= kb;
   for (int e = threadIdx.x; e < 64 * GJB; e += 256) {
-    const int r = e / GJB, t = e % GJB;
-    Cs[r][t] = (i0 + r < np) ? C[(long long)(i0 + r) * GJB + t] : 0.0;
-    const int tt = e / 64, c = e % 64;
-    Rs[tt][c] = (j0 + c < np) ? R[(long long)tt * np + j0 + c] : 0.0;
+    const int r = rows_below ? e % 64 : e / GJB, t = rows_below ? e / 64 : e % GJB;
+    Cs[r][t] = (i0 + r < np) ? gj_sym(M, np, i0 + r, kb + t) : 0.0;
+    const int q = cols_left ? e % GJB : e / 64, c = cols_left ? e / GJB : e % 64, jq = j0 + c;
+    Rs[q][c] = (jq < np && !(jq >= kb && jq < kb + GJB)) ? gj_sym(M, np, kb + q, jq) : 0.0;  // pivot rows
+  }
+  __syncthreads();
+  {  // Rrow' in place of the pivot rows: thread (column cj, pivot rows t0 .. t0 + 7)
+    const int cj = threadIdx.x & 63, j = j0 + cj;
+    const int t0 = (threadIdx.x >> 6) * 8;
+    const bool jcol = j < np && !(j >= kb && j < kb + GJB);
+    double acc[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = 0.0;
+    if (jcol) {
+#pragma unroll 8
+      for (int q = 0; q < GJB; ++q) {
+        const double cq = Rs[q][cj];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] += Pv[t0 + t][q] * cq;
+      }
+    } else if (j < np) {  // pivot columns: Rrow' = Pinv
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] = Pv[t0 + t][j - kb];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 8; ++t) Rs[t0 + t][cj] = acc[t];
   }
   __syncthreads();
   // 4x4 outputs per thread, register-blocked: per pivot column t, 4 values of
@@ -320,16 +425,17 @@ __global__ __launch_bounds__(256) void gj_update_kernel(MatSet s, double* ws, in
     const bool ipiv = i >= kb && i < kb + GJB;
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      const int j = j0 + tx + 16 * b;
-      if (j >= np) continue;
-      const bool jpiv = j >= kb && j < kb + GJB;
+      const int jj = j0 + tx + 16 * b;
+      if (jj >= np) continue;
+      const bool jpiv = jj >= kb && jj < kb + GJB;
       double v;
       if (ipiv) {  // pivot rows: Pinv M_kj; the pivot block -Pinv
-        v = jpiv ? -old[a][b] : old[a][b];
+        const double r = Rs[i - kb][tx + 16 * b];
+        v = jpiv ? -r : r;
       } else {     // pivot columns: M_ik Pinv; the rest M_ij - M_ik Pinv M_kj
         v = jpiv ? acc[a][b] : old[a][b] - acc[a][b];
       }
-      M[(long long)i * np + j] = v;
+      Mo[(long long)i * np + jj] = v;
     }
   }
 }
@@ -631,10 +737,10 @@ static void inverse_plan(const KLayout& K, MatSet* s, long long* total) {
     s->id[m] = m;
     s->m_off[m] = o;
     o += (long long)np * np;
-    s->row_off[m] = o;
-    o += (long long)GJB * np;
-    s->col_off[m] = o;
-    o += (long long)np * GJB;
+    s->m1_off[m] = o;
+    o += (long long)np * np;
+    s->pi_off[m] = o;
+    o += 2LL * GJB * GJB;
   }
   *total = o;
 }
@@ -686,31 +792,34 @@ int acmi_kfac_inverse(int A, int C3, const float* factors, float damping, int co
   }
   hipLaunchKernelGGL(damp_kernel, dim3(256, 12), dim3(256), 0, st, d, tr, ws);
   const int maxsteps = maxnp / GJB;
+  hipLaunchKernelGGL(gj_first_kernel, dim3(12), dim3(256), 0, st, s, ws);
   for (int step = 0; step < maxsteps; ++step) {
     MatSet a;
     a.count = 0;
-    int anp = 0;
     for (int m = 0; m < 12; ++m) {
       if (s.np[m] / GJB > step) {
         const int k = a.count++;
         a.n[k] = s.n[m];
         a.np[k] = s.np[m];
         a.m_off[k] = s.m_off[m];
-        a.row_off[k] = s.row_off[m];
-        a.col_off[k] = s.col_off[m];
+        a.m1_off[k] = s.m1_off[m];
+        a.pi_off[k] = s.pi_off[m];
         a.id[k] = m;
-        anp = std::max(anp, s.np[m]);
       }
     }
-    hipLaunchKernelGGL(gj_panel_kernel, dim3(cdiv(anp, PANEL_COLS), a.count), dim3(256), 0, st,
-                       a, ws, step);
-    const int nt = cdiv(anp, 64);
-    hipLaunchKernelGGL(gj_update_kernel, dim3(nt * (nt + 1) / 2, a.count), dim3(256), 0, st, a, ws, step);
+    int tiles = 0;
+    for (int k = 0; k < a.count; ++k) {
+      const int nt = cdiv(a.np[k], 64);
+      a.tile0[k] = tiles;
+      tiles += nt * (nt + 1) / 2;
+    }
+    a.tile0[a.count] = tiles;
+    hipLaunchKernelGGL(gj_step_kernel, dim3(a.count + tiles), dim3(256), 0, st, a, ws, step);
   }
   OutSet o;
   o.ws = ws;
   for (int m = 0; m < 12; ++m) {
-    o.m_off[m] = s.m_off[m];
+    o.m_off[m] = ((s.np[m] / GJB) & 1) ? s.m1_off[m] : s.m_off[m];  // after the last step
     o.n[m] = s.n[m];
     o.np[m] = s.np[m];
     o.ld[m] = (int)K.inv_ld[m];

@@ -69,6 +69,15 @@ __device__ __forceinline__ void tow_put(char* img, int p, int x, int ch, float v
   *reinterpret_cast<_Float16*>(img + tow_elem<C, S>(p, x, ch, 1)) = l;
 }
 
+// a1 / a2 to global memory: read again only by the update, after the rollout
+#ifndef ACMI_TOW_NT
+#define ACMI_TOW_NT 1
+#endif
+__device__ __forceinline__ void tow_store(float* p, float v) {
+  if constexpr (ACMI_TOW_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 // Prepared weights (acmi_conv_prepare): conv1/conv2/conv3 weights split once
 // per parameter version into the f16 h/l parts of every lane's B fragment,
 // fragment-major -- [k16 step][32-col tile][part h,l][lane] x 16 B -- so the
@@ -329,7 +338,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       }
       v = fmaxf(__builtin_fmaf(v * inv1, 1.0f / 255.0f, bias), 0.f);
       tow_put<32, 2>(a1L, p, p % 20, col, v, sa1);
-      if constexpr (!(ACMI_TOW_PROBE & 4)) g[p * 32 + col] = v;
+      if constexpr (!(ACMI_TOW_PROBE & 4)) tow_store(g + p * 32 + col, v);
       const unsigned long long bal = __ballot(v > 0.f);
       if (!(ACMI_TOW_PROBE & 4) && mg && col == 0) mg[p] = (uint32_t)(bal >> (lane & 32));
     };
@@ -415,7 +424,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     auto emit = [&](int p, float v) {
       v = fmaxf(__builtin_fmaf(v, inv2, bias), 0.f);
       tow_put<64, 1>(imgL, p, p % 9, c, v, sa2);
-      if constexpr (!(ACMI_TOW_PROBE & 4)) g[p * 64 + c] = v;
+      if constexpr (!(ACMI_TOW_PROBE & 4)) tow_store(g + p * 64 + c, v);
       const unsigned long long bal = __ballot(v > 0.f);
       if (!(ACMI_TOW_PROBE & 4) && mg && col == 0) mg[2 * p + ct] = (uint32_t)(bal >> (lane & 32));
     };

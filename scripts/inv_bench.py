@@ -1,6 +1,7 @@
 """Time acmi_kfac_inverse (all 12 damped fp64 inverses of the ACKTR factors) on
 random SPD factors of the bench's shapes."""
 import ctypes
+import hashlib
 import json
 import os
 import sys
@@ -41,7 +42,8 @@ def main(iters=10):
         run()
     e1.record()
     torch.cuda.synchronize()
-    print(json.dumps({'ms_per_inverse': e0.elapsed_time(e1) / iters, 'checksum': float(inv.double().sum())}))
+    print(json.dumps({'ms_per_inverse': e0.elapsed_time(e1) / iters, 'checksum': float(inv.double().sum()),
+                      'sha': hashlib.sha1(inv.cpu().numpy().tobytes()).hexdigest()[:16]}))
 
 
 if __name__ == '__main__':
