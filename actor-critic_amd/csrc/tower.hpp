@@ -48,11 +48,17 @@ static_assert(81 * 64 * 4 + 2 * 17 * 32 * 4 <= kTowObs, "a2 + conv2 scratch fit 
 // the f32 value split again by every wave that reads it (a1 pixels feed up to 4
 // conv2 taps x 4 waves, a2 pixels up to 9 conv3 taps): per pixel [part][C] f16
 // = C * 4 bytes, the 16-byte chunk c (8 channels of one part; c < C/8: h, else
-// l) at chunk position c ^ (x / S) % (C/4) -- the fragment reads of one
-// instruction (consecutive output columns, pixel x stepping by S) land on
-// distinct chunk positions (convfwd3.hpp chunk_pos).
+// l) at chunk position c ^ (p / S) % (C/4) -- the fragment reads of one
+// instruction (consecutive output pixels, input pixel p stepping by S within an
+// output row) land on distinct chunk positions.  (Swizzling by the column x = p
+// mod W instead, as convfwd3.hpp chunk_pos does, costs the producing epilogue a
+// mod per row: ~5 of its ~21 VALU per stored row.)
+#ifndef ACMI_TOW_PSWZ  // 1: swizzle by p / S (no p mod W in the producing epilogues); 0: by x / S
+#define ACMI_TOW_PSWZ 1
+#endif
 template <int C, int S>
 __device__ __forceinline__ int tow_pos(int p, int x, int c) {
+  if constexpr (ACMI_TOW_PSWZ) return p * C * 4 + 16 * (c ^ ((p / S) & (C / 4 - 1)));
   return p * C * 4 + 16 * (c ^ ((x / S) & (C / 4 - 1)));
 }
 // byte offset of channel ch's part (0: h, 1: l) of pixel p
@@ -326,7 +332,9 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
         acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[0], acc[u], 0, 0, 0);
       }
     }
-    const float bias = b1[col], inv1 = 16777216.0f / sw1;  // 2^24 (subnormal pixels) / scale: exact
+    // 2^24 (subnormal pixels) / scale / 255: a power of two times f32(1/255), so
+    // fma(v, inv1, bias) == fma(v * 2^24 / sw1, f32(1/255), bias) bit for bit
+    const float bias = b1[col], inv1 = 16777216.0f / sw1 * (1.0f / 255.0f);
     float* g = a1g + img * st * 12800;
     uint32_t* mg = m1g ? m1g + img * st * 400 : nullptr;
     // (the callers' active lanes are whole 32-lane halves: lanes 0 / 32 write the
@@ -336,8 +344,8 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
         if (v == 12345.f) g[p] = v;
         return;
       }
-      v = fmaxf(__builtin_fmaf(v * inv1, 1.0f / 255.0f, bias), 0.f);
-      tow_put<32, 2>(a1L, p, p % 20, col, v, sa1);
+      v = fmaxf(__builtin_fmaf(v, inv1, bias), 0.f);
+      tow_put<32, 2>(a1L, p, ACMI_TOW_PSWZ ? 0 : p % 20, col, v, sa1);
       if constexpr (!(ACMI_TOW_PROBE & 4)) tow_store(g + p * 32 + col, v);
       const unsigned long long bal = __ballot(v > 0.f);
       if (!(ACMI_TOW_PROBE & 4) && mg && col == 0) mg[p] = (uint32_t)(bal >> (lane & 32));
@@ -423,7 +431,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     uint32_t* mg = m2g ? m2g + img * st * 162 : nullptr;
     auto emit = [&](int p, float v) {
       v = fmaxf(__builtin_fmaf(v, inv2, bias), 0.f);
-      tow_put<64, 1>(imgL, p, p % 9, c, v, sa2);
+      tow_put<64, 1>(imgL, p, ACMI_TOW_PSWZ ? 0 : p % 9, c, v, sa2);
       if constexpr (!(ACMI_TOW_PROBE & 4)) tow_store(g + p * 64 + c, v);
       const unsigned long long bal = __ballot(v > 0.f);
       if (!(ACMI_TOW_PROBE & 4) && mg && col == 0) mg[2 * p + ct] = (uint32_t)(bal >> (lane & 32));
