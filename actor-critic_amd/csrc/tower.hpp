@@ -71,19 +71,26 @@ template <int C, int S>
 __device__ __forceinline__ void tow_put(char* img, int p, int x, int ch, float v, float s) {
   const _Float16 h = (_Float16)(v * s);
   const _Float16 l = (_Float16)fmaf(v, s, -(float)h);
-  *reinterpret_cast<_Float16*>(img + tow_elem<C, S>(p, x, ch, 0)) = h;
-  *reinterpret_cast<_Float16*>(img + tow_elem<C, S>(p, x, ch, 1)) = l;
+  // the l chunk's position is the h chunk's XOR C/8 (h chunks c < C/8, a power of
+  // two, so (c + C/8) ^ sw == (c ^ sw) ^ C/8), and the pixel base p*4C keeps that
+  // address bit clear: one XOR instead of a second swizzle
+  const int eh = tow_elem<C, S>(p, x, ch, 0);
+  *reinterpret_cast<_Float16*>(img + eh) = h;
+  *reinterpret_cast<_Float16*>(img + (eh ^ (2 * C))) = l;
 }
 
 // a1 / a2 to global memory: read again only by the update, after the rollout
 #ifndef ACMI_TOW_NT
 #define ACMI_TOW_NT 1
 #endif
-__device__ __forceinline__ void tow_store(float* p, float v) {
-  if constexpr (ACMI_TOW_NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-
+struct TowOut {  // one image's a1 / a2 in global memory as a buffer (SGPR base, 32-bit lane offsets)
+  __amdgpu_buffer_rsrc_t rs;
+  __device__ TowOut(float* base, int nfloats)
+      : rs(__builtin_amdgcn_make_buffer_rsrc(base, (short)0, nfloats * 4, 0x00020000)) {}
+  __device__ __forceinline__ void store(int i, float v) const {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, 4 * i, 0, ACMI_TOW_NT ? 2 : 0);  // aux 2: nt
+  }
+};
 // Prepared weights (acmi_conv_prepare): conv1/conv2/conv3 weights split once
 // per parameter version into the f16 h/l parts of every lane's B fragment,
 // fragment-major -- [k16 step][32-col tile][part h,l][lane] x 16 B -- so the
@@ -335,18 +342,18 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     // 2^24 (subnormal pixels) / scale / 255: a power of two times f32(1/255), so
     // fma(v, inv1, bias) == fma(v * 2^24 / sw1, f32(1/255), bias) bit for bit
     const float bias = b1[col], inv1 = 16777216.0f / sw1 * (1.0f / 255.0f);
-    float* g = a1g + img * st * 12800;
+    const TowOut g(a1g + img * st * 12800, 12800);
     uint32_t* mg = m1g ? m1g + img * st * 400 : nullptr;
     // (the callers' active lanes are whole 32-lane halves: lanes 0 / 32 write the
     // ReLU' word of their half's pixel)
     auto emit1 = [&](int p, float v) {
       if constexpr (ACMI_TOW_PROBE & 16) {  // probe: no conv1 epilogue (one store keeps acc live)
-        if (v == 12345.f) g[p] = v;
+        if (v == 12345.f) g.store(p, v);
         return;
       }
       v = fmaxf(__builtin_fmaf(v, inv1, bias), 0.f);
       tow_put<32, 2>(a1L, p, ACMI_TOW_PSWZ ? 0 : p % 20, col, v, sa1);
-      if constexpr (!(ACMI_TOW_PROBE & 4)) tow_store(g + p * 32 + col, v);
+      if constexpr (!(ACMI_TOW_PROBE & 4)) g.store(p * 32 + col, v);
       const unsigned long long bal = __ballot(v > 0.f);
       if (!(ACMI_TOW_PROBE & 4) && mg && col == 0) mg[p] = (uint32_t)(bal >> (lane & 32));
     };
@@ -427,12 +434,12 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     __syncthreads();
     const int c = 32 * ct + col;
     const float bias = b2[c], inv2 = 1.0f / (sa1 * sw2);  // exact: powers of two
-    float* g = a2g + img * st * 5184;
+    const TowOut g(a2g + img * st * 5184, 5184);
     uint32_t* mg = m2g ? m2g + img * st * 162 : nullptr;
     auto emit = [&](int p, float v) {
       v = fmaxf(__builtin_fmaf(v, inv2, bias), 0.f);
       tow_put<64, 1>(imgL, p, ACMI_TOW_PSWZ ? 0 : p % 9, c, v, sa2);
-      if constexpr (!(ACMI_TOW_PROBE & 4)) tow_store(g + p * 64 + c, v);
+      if constexpr (!(ACMI_TOW_PROBE & 4)) g.store(p * 64 + c, v);
       const unsigned long long bal = __ballot(v > 0.f);
       if (!(ACMI_TOW_PROBE & 4) && mg && col == 0) mg[2 * p + ct] = (uint32_t)(bal >> (lane & 32));
     };
