@@ -70,8 +70,10 @@ class SharedLoss(Node):
         objective._vcoef = self.weight
 
     def _eval(self, ctx):
-        loss = ctx.eval(self.objective._loss_node)
-        return loss[0] + self.weight * loss[1]
+        # the loss vector itself: the update needs only its kernels to have run (the
+        # gradient comes from acmi_a2c_loss's dhead), and a fetched value is formed
+        # by _finalize -- no two device launches per update for the scalar
+        return ctx.eval(self.objective._loss_node)
 
     def _finalize(self, ctx, value):
         loss = self.objective._loss_node.scalars(ctx)

@@ -1343,9 +1343,11 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
   const int ldg = roundup4(L.A + 1) < 8 ? 8 : roundup4(L.A + 1);
   float* ghead = ws;  // [B][ldg]
   float* part = ws + (long long)B * ldg;
-  // the dX chain's scratch (operand-scale maxima) in the workspace's last words
-  const long long cap = ws_cap - (long long)B * ldg - kBandScratch;
-  unsigned* dxs = reinterpret_cast<unsigned*>(ws + ws_cap - kBandScratch);
+  // the dX chain's scratch (operand-scale maxima) in the workspace's last words,
+  // 16-byte aligned (an unaligned hipMemsetAsync runs as three fill kernels)
+  const long long dxo = (ws_cap - kBandScratch) & ~3LL;
+  const long long cap = dxo - (long long)B * ldg;
+  unsigned* dxs = reinterpret_cast<unsigned*>(ws + dxo);
   hipLaunchKernelGGL(sampled_head_grad_kernel, dim3(cdiv(B, 128)), dim3(128), 0, s,
                      a->logits, a->ld_logits, B, L.A, seed, row0, ctr, ghead, ldg);
   bool g1_done = false;
@@ -1508,6 +1510,15 @@ int64_t acmi_conv_prep_bytes(int C3) {
                     : -1;
 }
 
+// two zeroed runs of 16-byte words in one launch
+__global__ __launch_bounds__(256) void zero2_kernel(uint4* a, long long na, uint4* b, long long nb) {
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < na + nb; i += (long long)gridDim.x * 256) {
+    if (i < na) a[i] = z;
+    else b[i - na] = z;
+  }
+}
+
 int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
   Layout L;
   ACMI_REQUIRE(net && net->params && prep && make_layout(net->num_actions, net->conv3_filters, &L),
@@ -1515,16 +1526,17 @@ int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
   ACMI_REQUIRE((uintptr_t)prep % 16 == 0, ACMI_ERR_ARG, "acmi_conv_prepare: prep must be 16-byte aligned");
   const long long o2 = L.C3 == 32 ? TowerPrep<32>::BYTES : TowerPrep<64>::BYTES;
   const long long oh = L.C3 == 32 ? TowerPrep<32>::HDR : TowerPrep<64>::HDR;
-  // the tower's bounds header (atomicMax targets), then its f16x2 fragments
-  ACMI_REQUIRE(hipMemsetAsync(static_cast<char*>(prep) + oh, 0, TowerPrep<32>::HDR_BYTES, (hipStream_t)stream) ==
-                   hipSuccess,
-               ACMI_ERR_HIP, "acmi_conv_prepare: memset failed");
+  // the atomicMax targets -- the tower's bounds header and conv2 input gradient's
+  // max |W2| words -- zeroed by one launch, then the tower's f16x2 fragments
+  static_assert(TowerPrep<32>::HDR_BYTES % 16 == 0 && (CT2::BYTES - CT2::FRAG_BYTES) % 16 == 0 &&
+                    TowerPrep<32>::HDR % 16 == 0 && TowerPrep<64>::HDR % 16 == 0 && CT2::FRAG_BYTES % 16 == 0,
+                "16-byte runs");
+  hipLaunchKernelGGL(zero2_kernel, dim3(64), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<uint4*>(static_cast<char*>(prep) + oh), TowerPrep<32>::HDR_BYTES / 16,
+                     reinterpret_cast<uint4*>(static_cast<char*>(prep) + o2 + CT2::FRAG_BYTES),
+                     (CT2::BYTES - CT2::FRAG_BYTES) / 16);
   launch_tower_prep(net->params, L.off, L.C3, prep, (hipStream_t)stream);
   // conv2's input-gradient weights: max |W2| (the f16x2 scale), then the split
-  ACMI_REQUIRE(hipMemsetAsync(static_cast<char*>(prep) + o2 + CT2::FRAG_BYTES, 0, CT2::BYTES - CT2::FRAG_BYTES,
-                              (hipStream_t)stream) ==
-                   hipSuccess,
-               ACMI_ERR_HIP, "acmi_conv_prepare: memset failed");
   hipLaunchKernelGGL(convt2_wmax_kernel, dim3(32), dim3(256), 0, (hipStream_t)stream, net->params + L.off[2],
                      static_cast<char*>(prep) + o2);
   hipLaunchKernelGGL(convt2_prep_kernel, dim3(CT2::NKS * 4 * 64 / 256), dim3(256), 0, (hipStream_t)stream,

@@ -230,6 +230,25 @@ __global__ void tower_prep_kernel(const float* w1, const float* w2, const float*
 
 // row of the 32x32 C/D fragment element r of `lane`
 __device__ __forceinline__ int tow_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+// the ReLU' words of element R's two rows (ballot halves: rows tow_row(R, 0) and
+// tow_row(R, 32)) written into the lanes of the same index of mw
+template <int R>
+__device__ __forceinline__ uint32_t tow_mword(uint32_t mw, unsigned long long bal) {
+  constexpr int rr = (R & 3) + 8 * (R >> 2);
+  const uint32_t lo = (uint32_t)bal, hi = (uint32_t)(bal >> 32);
+  asm volatile("v_writelane_b32 %0, %1, %2\n\tv_writelane_b32 %0, %3, %4"
+               : "+v"(mw)
+               : "s"(lo), "n"(rr), "s"(hi), "n"(rr + 4));
+  return mw;
+}
+// f(std::integral_constant<int, I>) for I = B .. E-1
+template <int B, int E, class F>
+__device__ __forceinline__ void tow_static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    tow_static_for<B + 1, E>(f);
+  }
+}
 
 // a layer's B fragments from the prepared weights, kTowDepth k-steps ahead of
 // the one computed (slot = k-step mod kTowDepth + 1, a compile-time index in the
@@ -344,23 +363,29 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     const float bias = b1[col], inv1 = 16777216.0f / sw1 * (1.0f / 255.0f);
     const TowOut g(a1g + img * st * 12800, 12800);
     uint32_t* mg = m1g ? m1g + img * st * 400 : nullptr;
-    // (the callers' active lanes are whole 32-lane halves: lanes 0 / 32 write the
-    // ReLU' word of their half's pixel)
-    auto emit1 = [&](int p, float v) {
+    // one row of the tile: returns the ReLU' ballot (bit = lane: the low word row
+    // p of the lower half's pixel, the high word the upper half's)
+    auto emit1 = [&](int p, float v) -> unsigned long long {
       if constexpr (ACMI_TOW_PROBE & 16) {  // probe: no conv1 epilogue (one store keeps acc live)
         if (v == 12345.f) g.store(p, v);
-        return;
+        return 0;
       }
       v = fmaxf(__builtin_fmaf(v, inv1, bias), 0.f);
       tow_put<32, 2>(a1L, p, ACMI_TOW_PSWZ ? 0 : p % 20, col, v, sa1);
       if constexpr (!(ACMI_TOW_PROBE & 4)) g.store(p * 32 + col, v);
-      const unsigned long long bal = __ballot(v > 0.f);
-      if (!(ACMI_TOW_PROBE & 4) && mg && col == 0) mg[p] = (uint32_t)(bal >> (lane & 32));
+      return __ballot(v > 0.f);
     };
+    // the tile's ReLU' words gathered by v_writelane (lane j: the tile's row j) and
+    // stored by one instruction per tile instead of a masked store per row
 #pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) emit1(32 * tile_of(u) + tow_row(r, lane), acc[u][r]);  // rows < 384
+    for (int u = 0; u < 3; ++u) {
+      uint32_t mw = 0;
+      tow_static_for<0, 16>([&](auto R) {  // rows < 384
+        constexpr int r = decltype(R)::value;
+        mw = tow_mword<r>(mw, emit1(32 * tile_of(u) + tow_row(r, lane), acc[u][r]));
+      });
+      if (!(ACMI_TOW_PROBE & 4) && mg && lane < 32) mg[32 * tile_of(u) + lane] = mw;
+    }
     float* scr12 = reinterpret_cast<float*>(lds + kTowLds);  // [16 rows][32]
     if (w == 3) {
 #pragma unroll
@@ -368,12 +393,14 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
         if (tow_row(r, lane) < 16) scr12[tow_row(r, lane) * 32 + col] = acc[3][r];
     }
     __syncthreads();
-    if (w == 2) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
+    if (w == 2) {  // rows 384..399: r < 8 (tow_row(r, .) < 16 on every lane)
+      uint32_t mw = 0;
+      tow_static_for<0, 8>([&](auto R) {
+        constexpr int r = decltype(R)::value;
         const int m = tow_row(r, lane);
-        if (m < 16) emit1(384 + m, acc[3][r] + scr12[m * 32 + col]);
-      }
+        mw = tow_mword<r>(mw, emit1(384 + m, acc[3][r] + scr12[m * 32 + col]));
+      });
+      if (!(ACMI_TOW_PROBE & 4) && mg && lane < 16) mg[384 + lane] = mw;
     }
   }
   __syncthreads();
@@ -436,24 +463,32 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     const float bias = b2[c], inv2 = 1.0f / (sa1 * sw2);  // exact: powers of two
     const TowOut g(a2g + img * st * 5184, 5184);
     uint32_t* mg = m2g ? m2g + img * st * 162 : nullptr;
-    auto emit = [&](int p, float v) {
+    // (act: the lane's row exists; the ballot runs on every lane)
+    auto emit = [&](int p, float v, bool act) -> unsigned long long {
       v = fmaxf(__builtin_fmaf(v, inv2, bias), 0.f);
-      tow_put<64, 1>(imgL, p, ACMI_TOW_PSWZ ? 0 : p % 9, c, v, sa2);
-      if constexpr (!(ACMI_TOW_PROBE & 4)) g.store(p * 64 + c, v);
-      const unsigned long long bal = __ballot(v > 0.f);
-      if (!(ACMI_TOW_PROBE & 4) && mg && col == 0) mg[2 * p + ct] = (uint32_t)(bal >> (lane & 32));
-    };
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int p = 32 * rtf + tow_row(r, lane);
-      emit(p, accF[r]);  // rows 0..63 are all valid
-    }
-    if (wave < 2) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = tow_row(r, lane);
-        if (m < 17) emit(64 + m, accH[r] + scr[(ct * 17 + m) * 32 + col]);
+      if (act) {
+        tow_put<64, 1>(imgL, p, ACMI_TOW_PSWZ ? 0 : p % 9, c, v, sa2);
+        if constexpr (!(ACMI_TOW_PROBE & 4)) g.store(p * 64 + c, v);
       }
+      return __ballot(act && v > 0.f);
+    };
+    {
+      uint32_t mw = 0;
+      tow_static_for<0, 16>([&](auto R) {  // rows 0..63 are all valid
+        constexpr int r = decltype(R)::value;
+        mw = tow_mword<r>(mw, emit(32 * rtf + tow_row(r, lane), accF[r], true));
+      });
+      if (!(ACMI_TOW_PROBE & 4) && mg && lane < 32) mg[2 * (32 * rtf + lane) + ct] = mw;
+    }
+    if (wave < 2) {  // rows 64..80: r < 8 on every lane, r = 8 (row 80) on the lower half
+      uint32_t mw = 0;
+      tow_static_for<0, 9>([&](auto R) {
+        constexpr int r = decltype(R)::value;
+        const int m = tow_row(r, lane);
+        const bool act = m < 17;
+        mw = tow_mword<r>(mw, emit(64 + m, act ? accH[r] + scr[(ct * 17 + m) * 32 + col] : 0.f, act));
+      });
+      if (!(ACMI_TOW_PROBE & 4) && mg && lane < 17) mg[2 * (64 + lane) + ct] = mw;
     }
   }
   __syncthreads();
