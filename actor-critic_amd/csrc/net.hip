@@ -788,6 +788,59 @@ __global__ void finalize_cov_elem_kernel(const float* part, int nchunk, int n,
   if (lane == 0) out[0] = s * (1.0f / (float)rows);
 }
 
+// The sampled-loss chain's G-factor finalizes as ONE launch after all its Grams
+// (each Gram's partials in its own workspace range): task k owns blocks
+// [blk0, blk0 of k+1) and runs the body of finalize_cov_thread_kernel (kind 0),
+// finalize_cov_kernel (1) or finalize_cov_elem_kernel (2) -- the same sums.
+struct CovTask {
+  const float* part;
+  float* out;
+  int nchunk, n, sub, rows, kind, a, blk0;
+};
+constexpr int kCovTasks = 8;
+struct CovSet {
+  int n = 0;
+  int blocks = 0;
+  CovTask t[kCovTasks];
+  void add(const float* part, int nchunk, int n_, int sub, float* out, int rows, int kind, int a = 0) {
+    const int nb = kind == 0 ? cdiv(sub * sub, 256) : kind == 1 ? cdiv(sub * sub, 4) : 1;
+    t[n++] = CovTask{part, out, nchunk, n_, sub, rows, kind, a, blocks};
+    blocks += nb;
+  }
+};
+__global__ __launch_bounds__(256) void finalize_cov_multi_kernel(CovSet S) {
+  int k = 0;
+  while (k + 1 < S.n && (int)blockIdx.x >= S.t[k + 1].blk0) ++k;
+  const CovTask& T = S.t[k];
+  const int b = blockIdx.x - T.blk0;
+  const long long cs = (long long)(T.n + 1) * T.n;
+  if (T.kind == 0) {
+    const int idx = b * 256 + threadIdx.x;
+    if (idx >= T.sub * T.sub) return;
+    const int a = idx / T.sub, c = idx - a * T.sub;
+    if (a > c) return;
+    const float v = chunk_sum(T.part + (long long)a * T.n + c, T.nchunk, cs) * (1.0f / (float)T.rows);
+    T.out[a * T.sub + c] = v;
+    T.out[c * T.sub + a] = v;
+  } else {
+    const int idx = T.kind == 1 ? b * 4 + (threadIdx.x >> 6) : 0;
+    const int lane = threadIdx.x & 63;
+    if (idx >= T.sub * T.sub || (T.kind == 2 && threadIdx.x >= 64)) return;
+    int lo, hi;
+    if (T.kind == 1) {
+      const int a = idx / T.sub, c = idx - a * T.sub;
+      lo = a < c ? a : c, hi = a < c ? c : a;
+    } else {
+      lo = hi = T.a;
+    }
+    const float* p = T.part + (long long)lo * T.n + hi;
+    float v = 0.f;
+    for (int c = lane; c < T.nchunk; c += 64) v += p[c * cs];
+    v = wave_sum(v);
+    if (lane == 0) T.out[idx] = v * (1.0f / (float)T.rows);
+  }
+}
+
 // G = D^T D for narrow D (n <= NP, NP in {32, 64}) straight from global memory:
 // each wave streams row pairs (lane l: row 2q + (l>>5), column l&31 [+32]) as
 // the A and B fragments of v_mfma_f32_32x32x2_f32 (the Gram tile is D^T D of
@@ -1019,10 +1072,12 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
 // G = g^T g / rows for g [rows][ld] (first n columns), via split-K; gmax: the
 // published max |g| (bit pattern) -- the wide Grams then run on f16x2 split
 // operands (three MFMAs per product instead of bf16x3's six)
+// defer: append the finalize to this set instead of launching it (the caller
+// launches the set once; *used: the partial floats this Gram wrote)
 static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
                       float* part, long long part_cap, float* out,
                       hipStream_t s, float* out_v = nullptr, int v_index = -1,
-                      const unsigned* gmax = nullptr) {
+                      const unsigned* gmax = nullptr, CovSet* defer = nullptr, long long* used = nullptr) {
   int np, nc;
   if (n <= 32) {  // narrow: streaming Gram kernel (f32 MFMA; 64 wide runs faster on the split-K
                   // bf16x3 GEMM below: conv2's G factor 82 + 25 -> 59 + 16 us)
@@ -1046,6 +1101,13 @@ static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
       launch_gemm3_f16_splitk<64, 64, 16, 1, 1>(op, op, epi, np, np, (int)rows, nc, (int)pl.ch, gmax, gmax, s, np);
     else
       launch_mm<64, 64, 32, 1, 1, true, false, 16>(op, op, epi, np, np, (int)rows, nc, pl.ch, s, np);
+  }
+  if (used) *used = (long long)nc * (np + 1) * np;
+  if (defer) {
+    defer->add(part, nc, np, sub, out, (int)rows, nc <= 64 ? 0 : 1);
+    if (out_v) defer->add(part, nc, np, 1, out_v, (int)rows, 2, v_index);
+    ACMI_LAUNCH_CHECK("gcov_layer");
+    return ACMI_OK;
   }
   if (nc <= 64)
     hipLaunchKernelGGL(finalize_cov_thread_kernel, dim3(cdiv((long long)sub * sub, 256)), dim3(256), 0,
@@ -1354,26 +1416,49 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
   const bool g1_fits = (long long)convt2_gram_blocks(B) * 33 * 32 <= cap;
   int rc = dx_chain<C3>(L, P, B, a, bw, ghead, ldg, s, prep, g1_fits ? part : nullptr, &g1_done, dxs);
   if (rc) return rc;
+  // the G factors' finalizes deferred into one launch: every Gram's partials in
+  // their own range of the workspace (while they fit; else the set so far is
+  // finalized and the ranges start over)
+  CovSet fin;
+  long long off = 0;
+  auto flush = [&]() {
+    if (fin.n) hipLaunchKernelGGL(finalize_cov_multi_kernel, dim3(fin.blocks), dim3(256), 0, s, fin);
+    fin = CovSet();
+    off = 0;
+  };
   if (g1_done) {  // G of conv1's output from the conv2 dX kernel's per-block Gram partials
-    hipLaunchKernelGGL(finalize_cov_kernel, dim3(cdiv(32 * 32, 4)), dim3(256), 0, s, part,
-                       convt2_gram_blocks(B), 32, 32, gstat + L.stat_off[5 + 0], (int)(400LL * B));
-    ACMI_LAUNCH_CHECK("conv1 G factor");
+    fin.add(part, convt2_gram_blocks(B), 32, 32, gstat + L.stat_off[5 + 0], (int)(400LL * B), 1);
+    off = ((long long)convt2_gram_blocks(B) * 33 * 32 + 3) / 4 * 4;
   }
+  // one Gram into the next free range: its worst case is the whole remaining cap
+  // (gcov_layer checks); retried from offset 0 after a flush when it does not fit
+  auto gram = [&](const float* g, int ld, int n, long long rows, int sub, float* out, float* out_v, int vi,
+                  const unsigned* gmax) {
+    long long used = 0;
+    if (fin.n + 2 > kCovTasks) flush();
+    int r = gcov_layer(g, ld, n, rows, sub, part + off, cap - off, out, s, out_v, vi, gmax, &fin, &used);
+    if (r == ACMI_ERR_WS && off > 0) {
+      flush();
+      r = gcov_layer(g, ld, n, rows, sub, part, cap, out, s, out_v, vi, gmax, &fin, &used);
+    }
+    off += (used + 3) / 4 * 4;
+    return r;
+  };
   // heads: G_pi (A x A) from the first A columns, G_v = element (A, A)
-  rc = gcov_layer(ghead, ldg, L.A + 1, B, L.A, part, cap, gstat + L.stat_off[5 + 4], s,
-                  gstat + L.stat_off[5 + 5], L.A);
+  rc = gram(ghead, ldg, L.A + 1, B, L.A, gstat + L.stat_off[5 + 4], gstat + L.stat_off[5 + 5], L.A, nullptr);
   if (rc) return rc;
   // (the dX chain above published max |d4| and max |d2| into dxs)
-  rc = gcov_layer(bw->d4, 512, 512, B, 512, part, cap, gstat + L.stat_off[5 + 3], s, nullptr, -1,
-                  dxs + kBsMaxD4);
+  rc = gram(bw->d4, 512, 512, B, 512, gstat + L.stat_off[5 + 3], nullptr, -1, dxs + kBsMaxD4);
   if (rc) return rc;
-  rc = gcov_layer(bw->d3, C3, C3, 49LL * B, C3, part, cap, gstat + L.stat_off[5 + 2], s);
+  rc = gram(bw->d3, C3, C3, 49LL * B, C3, gstat + L.stat_off[5 + 2], nullptr, -1, nullptr);
   if (rc) return rc;
-  rc = gcov_layer(bw->d2, 64, 64, 81LL * B, 64, part, cap, gstat + L.stat_off[5 + 1], s, nullptr, -1,
-                  dxs + kBsMaxD2);
+  rc = gram(bw->d2, 64, 64, 81LL * B, 64, gstat + L.stat_off[5 + 1], nullptr, -1, dxs + kBsMaxD2);
   if (rc) return rc;
-  if (!g1_done) rc = gcov_layer(bw->d1, 32, 32, 400LL * B, 32, part, cap, gstat + L.stat_off[5 + 0], s);
-  return rc;
+  if (!g1_done) rc = gram(bw->d1, 32, 32, 400LL * B, 32, gstat + L.stat_off[5 + 0], nullptr, -1, nullptr);
+  if (rc) return rc;
+  flush();
+  ACMI_LAUNCH_CHECK("G factor finalize");
+  return ACMI_OK;
 }
 
 }  // namespace acmi
