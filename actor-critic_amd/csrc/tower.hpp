@@ -535,11 +535,31 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     const float bias = b3[c], inv3 = 1.0f / (sa2 * sw3);
     float* g = a3g + img * st * (49 * C3);
     uint32_t* mg = m3g ? m3g + img * st * (49 * C3 / 32) : nullptr;
-    auto emit3 = [&](int p, float v) {  // (active lanes: whole 32-lane halves)
+    // (act: the lane's row exists; the ballot runs on every lane)
+    auto emit3 = [&](int p, float v, bool act) -> unsigned long long {
       v = fmaxf(__builtin_fmaf(v, inv3, bias), 0.f);
-      if constexpr (!(ACMI_TOW_PROBE & 4)) g[p * C3 + c] = v;
-      const unsigned long long bal = __ballot(v > 0.f);
-      if (!(ACMI_TOW_PROBE & 4) && mg && col == 0) mg[p * (C3 / 32) + ct] = (uint32_t)(bal >> (lane & 32));
+      if (!(ACMI_TOW_PROBE & 4) && act) g[p * C3 + c] = v;
+      return __ballot(act && v > 0.f);
+    };
+    // rows 32 rt + tow_row(r, lane) < 49: row tile 0 all 16 r; row tile 1 r < 8 on
+    // every lane and r = 8 (row 48) on the lower half; the ReLU' words gathered by
+    // v_writelane and stored once per tile
+    auto emit_tile = [&](auto get) {
+      uint32_t mw = 0;
+      if (rt == 0) {
+        tow_static_for<0, 16>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          mw = tow_mword<r>(mw, emit3(tow_row(r, lane), get(r), true));
+        });
+      } else {
+        tow_static_for<0, 9>([&](auto R) {
+          constexpr int r = decltype(R)::value;
+          const int p = 32 + tow_row(r, lane);
+          const bool act = p < 49;
+          mw = tow_mword<r>(mw, emit3(p, act ? get(r) : 0.f, act));
+        });
+      }
+      if (!(ACMI_TOW_PROBE & 4) && mg && lane < (rt ? 17 : 32)) mg[(32 * rt + lane) * (C3 / 32) + ct] = mw;
     };
     if constexpr (C3 == 32) {  // the second K half (waves 2, 3) through LDS to the first
       float* scr = reinterpret_cast<float*>(a1L);  // [rt][32 rows][32]
@@ -548,19 +568,9 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
         for (int r = 0; r < 16; ++r) scr[(rt * 32 + tow_row(r, lane)) * 32 + col] = acc[r];
       }
       __syncthreads();
-      if (wave < 2) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int p = 32 * rt + tow_row(r, lane);
-          if (p < 49) emit3(p, acc[r] + scr[(rt * 32 + tow_row(r, lane)) * 32 + col]);
-        }
-      }
+      if (wave < 2) emit_tile([&](int r) { return acc[r] + scr[(rt * 32 + tow_row(r, lane)) * 32 + col]; });
     } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int p = 32 * rt + tow_row(r, lane);
-        if (p < 49) emit3(p, acc[r]);
-      }
+      emit_tile([&](int r) { return acc[r]; });
     }
   }
 }
