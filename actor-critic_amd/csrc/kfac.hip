@@ -145,7 +145,7 @@ __global__ void damp_kernel(DampSet d, const double* tr, double* ws) {
 // four elements from one LDS image and writes the four updated elements to the
 // other (ping-pong: one barrier per sweep).  1/pivot from v_rcp_f64 and two
 // Newton steps (within an ulp of the IEEE quotient, a third of the division
-// sequence's latency).  The 32 one-pivot sweeps were 12 us of the 22 us panel
+// sequence's latency).  The 32 one-pivot sweeps were 12 us of the former 22 us panel
 // launch with the division and two barriers per sweep; pairs of pivots per
 // sweep (below) halve the chain.  (One wave doing all 32 x 32 elements without
 // barriers -- 16 per lane -- measured slower: 2.52 vs 1.69 ms per inverse; the
@@ -229,7 +229,7 @@ __device__ void pivot_inverse(double (*P)[GJB + 1], double (*Q)[GJB + 1]) {
 // Symmetric sweep: the damped factors are symmetric, and the sweep operator
 //   M_kk <- -P^-1,  M_kj <- P^-1 M_kj,  M_ik <- M_ik P^-1,  M_ij <- M_ij - M_ik P^-1 M_kj
 // keeps every intermediate matrix symmetric (sweeping all pivots leaves -M^-1),
-// so gj_update_kernel computes the 64x64 tiles on and above the diagonal only
+// so gj_step_kernel computes the 64x64 tiles on and above the diagonal only
 // (half the work and traffic of the plain Gauss-Jordan update) and everything
 // reads element (r, c) from the upper triangle (gj_sym).
 __device__ __forceinline__ double gj_sym(const double* M, int np, int r, int c) {
