@@ -651,13 +651,12 @@ __device__ __forceinline__ float chunk_sum_group(const float* p, int n, long lon
   return s;
 }
 
-__global__ __launch_bounds__(256) void finalize_wgrad_kernel(WgradDesc d) {
-  __shared__ float red[kFinGroups][32];
+__device__ __forceinline__ void finalize_wgrad_body(const WgradDesc& d, int bx, float (*red)[32]) {
   const int K = d.I;
   const long long ngrad = (long long)(K + 1) * d.cout;
   const long long nstat = d.astat ? (long long)(K + 1) * (K + 1) : 0;
   const int el = threadIdx.x & 31, g = threadIdx.x >> 5;
-  const long long idx = (long long)blockIdx.x * 32 + el;
+  const long long idx = (long long)bx * 32 + el;
   const long long cs = (long long)(d.I + 1) * d.J;  // chunk stride
   // the partial this output sums (nullptr: nothing to sum)
   const float* p = nullptr;
@@ -693,17 +692,21 @@ __global__ __launch_bounds__(256) void finalize_wgrad_kernel(WgradDesc d) {
   }
 }
 
+__global__ __launch_bounds__(256) void finalize_wgrad_kernel(WgradDesc d) {
+  __shared__ float red[kFinGroups][32];
+  finalize_wgrad_body(d, blockIdx.x, red);
+}
+
 // The A factor of a split-K wgrad partial ((K+1)^2, symmetric): one block per
 // 32x32 tile of the upper triangle; each element sums its chunks in exactly
 // finalize_wgrad_kernel's order (chunk group g = c mod 8 in chunk order, then
 // the groups in order), is stored at (a, b) and, through an LDS transpose, at
 // (b, a) -- both halves written by coalesced rows (the element-per-thread
 // mirror store of finalize_wgrad_kernel is a 4-byte scatter with stride K+1).
-__global__ __launch_bounds__(256) void finalize_afactor_kernel(WgradDesc d, int ntile) {
-  __shared__ float tr[32][33];
+__device__ __forceinline__ void finalize_afactor_body(const WgradDesc& d, int ntile, int bx, float (*tr)[33]) {
   const int K = d.I, K1 = K + 1;
-  // upper-triangle tile (ta <= tb) of linear index blockIdx.x
-  int t = blockIdx.x, ta = 0;
+  // upper-triangle tile (ta <= tb) of linear index bx
+  int t = bx, ta = 0;
   while (t >= ntile - ta) t -= ntile - ta, ++ta;
   const int tb = ta + t;
   const long long cs = (long long)(d.I + 1) * d.J;
@@ -738,6 +741,39 @@ __global__ __launch_bounds__(256) void finalize_afactor_kernel(WgradDesc d, int 
     const int b = 32 * tb + r, a = 32 * ta + c;
     if (a < K1 && b < K1 && a < b) d.astat[(long long)b * K1 + a] = tr[c][r];
   }
+}
+__global__ __launch_bounds__(256) void finalize_afactor_kernel(WgradDesc d, int ntile) {
+  __shared__ float tr[32][33];
+  finalize_afactor_body(d, ntile, blockIdx.x, tr);
+}
+
+// Several layers' weight-gradient / A-factor finalizes as one launch (each
+// layer's split-K partials in their own workspace range): task k owns blocks
+// [blk0, blk0 of k+1) and runs finalize_wgrad_kernel's (kind 0) or
+// finalize_afactor_kernel's (kind 1) body -- the same sums.
+struct WgradTask {
+  WgradDesc d;
+  int kind, ntile, blk0;
+};
+constexpr int kWgradTasks = 6;
+struct WgradSet {
+  int n = 0;
+  int blocks = 0;
+  WgradTask t[kWgradTasks];
+  void add(const WgradDesc& d, int kind, int ntile, int nblocks) {
+    t[n++] = WgradTask{d, kind, ntile, blocks};
+    blocks += nblocks;
+  }
+};
+__global__ __launch_bounds__(256) void finalize_wgrad_multi_kernel(WgradSet S) {
+  __shared__ float red[kFinGroups][32];
+  __shared__ float tr[32][33];
+  int k = 0;
+  while (k + 1 < S.n && (int)blockIdx.x >= S.t[k + 1].blk0) ++k;
+  const WgradTask& T = S.t[k];
+  const int b = blockIdx.x - T.blk0;
+  if (T.kind == 0) finalize_wgrad_body(T.d, b, red);
+  else finalize_afactor_body(T.d, T.ntile, b, tr);
 }
 
 // G factor: part [nchunk][I+1][J] (I == J == n, no colsum row used); one
@@ -1025,7 +1061,8 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
                        int ldy, int cout, bool with_stats, float* part,
                        long long part_cap, float* gradA, int nsplit,
                        float* gradB, float* astat, hipStream_t s, int site = 0,
-                       float wscale = 1.f, const unsigned* pmax = nullptr, const unsigned* ymax = nullptr) {
+                       float wscale = 1.f, const unsigned* pmax = nullptr, const unsigned* ymax = nullptr,
+                       WgradSet* defer = nullptr, long long* used = nullptr) {
   constexpr bool kU8 = !std::is_same<typename Src::elem_t, float>::value;
   const int mode = g_gemm_mode;
   const WgradPlan pl = wgrad_plan(K, cout, with_stats, rows, kU8, mode);
@@ -1059,6 +1096,17 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
   const bool tiles = astat && nc <= kFinGroups;
   WgradDesc d{part, nc, I, J, kp, cout, gradA, nsplit, gradB, tiles ? nullptr : astat, (int)rows, wscale};
   const long long total = (long long)(K + 1) * cout + (d.astat ? (long long)(K + 1) * (K + 1) : 0);
+  if (used) *used = pl.floats;
+  if (defer) {
+    defer->add(d, 0, 0, (int)cdiv(total, 32));
+    if (tiles) {
+      d.astat = astat;
+      const int nt = cdiv(K + 1, 32);
+      defer->add(d, 1, nt, nt * (nt + 1) / 2);
+    }
+    ACMI_LAUNCH_CHECK("wgrad_layer");
+    return ACMI_OK;
+  }
   hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(total, 32)), dim3(256), 0, s, d);
   if (tiles) {
     d.astat = astat;
@@ -1300,37 +1348,63 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
     hipEvent_t* ev = dx_done_event();
     ACMI_REQUIRE(ev && hipEventRecord(*ev, s) == hipSuccess, ACMI_ERR_HIP, "acmi_backward: dX event record failed");
   }
+  float* wpart_c1 = nullptr;  // conv1's fused weight-gradient partials (in the A-factor workspace)
   if (st) {
     const long long pcap = bwd_partial_cap(B, L.A, L.C3);
     prof_begin(ACMI_PROF_CONV1_AFACTOR, s);
-    float* wpart = nullptr;
     const int rc0 = conv1_afactor_u8(obs, img_stride, B, astat + L.stat_off[0],
                                      reinterpret_cast<int*>(ws + pcap), afactor_ws_floats(B), s,
-                                     fuse_c1 ? bw->d1 : nullptr, &wpart, bscr + kBsMaxD1);
+                                     fuse_c1 ? bw->d1 : nullptr, &wpart_c1, bscr + kBsMaxD1);
     prof_end(ACMI_PROF_CONV1_AFACTOR, s);
     if (rc0) return rc0;
-    if (fuse_c1) {  // the conv1 weight gradient came with the A factor: reduce its chunks
-      const long long rows = 400LL * B;
-      WgradDesc d{wpart, conv1_afactor_fused_chunks(rows), 256, 32, 0, 32, grads + L.off[0], 32,
-                  nullptr, nullptr, (int)rows, 1.0f / 255.0f};
-      hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(257 * 32, 32)), dim3(256), 0, s, d);
-      ACMI_LAUNCH_CHECK("conv1 fused weight gradient");
-    }
+  }
+  // the conv1, heads and fc4 finalizes deferred into one launch: each layer's
+  // partials in their own range of the partial region (below the band scratch;
+  // a layer that does not fit after the others finalizes the set so far first)
+  WgradSet fin;
+  long long off = 0;
+  const long long avail = pcap_all - kBandScratch;
+  auto flush = [&]() {
+    if (fin.n) hipLaunchKernelGGL(finalize_wgrad_multi_kernel, dim3(fin.blocks), dim3(256), 0, s, fin);
+    fin = WgradSet();
+    off = 0;
+  };
+  if (st && fuse_c1) {  // the conv1 weight gradient came with the A factor: reduce its chunks
+    const long long rows = 400LL * B;
+    WgradDesc d{wpart_c1, conv1_afactor_fused_chunks(rows), 256, 32, 0, 32, grads + L.off[0], 32,
+                nullptr, nullptr, (int)rows, 1.0f / 255.0f};
+    fin.add(d, 0, 0, (int)cdiv(257 * 32, 32));
   }
   float* part = ws;
+  auto layer = [&](auto&& run) {
+    long long used = 0;
+    if (fin.n + 2 > kWgradTasks) flush();
+    int r = run(part + off, avail - off, &used);
+    if (r == ACMI_ERR_WS && off > 0) {
+      flush();
+      r = run(part, avail, &used);
+    }
+    off += (used + 3) / 4 * 4;
+    return r;
+  };
   // heads: X = a4 (512), dY = dhead (A+1 columns: pi | v)
-  rc = wgrad_layer(DenseRows{a->a4, 512, B, 512}, 512, B, bw->dhead, bw->ldh, L.A + 1, st,
-                   part, ws_cap, grads + L.off[8], L.A, grads + L.off[10],
-                   st ? astat + L.stat_off[4] : nullptr, s);
+  rc = layer([&](float* pt, long long cap, long long* used) {
+    return wgrad_layer(DenseRows{a->a4, 512, B, 512}, 512, B, bw->dhead, bw->ldh, L.A + 1, st, pt, cap,
+                       grads + L.off[8], L.A, grads + L.off[10], st ? astat + L.stat_off[4] : nullptr, s, 0, 1.f,
+                       nullptr, nullptr, &fin, used);
+  });
   if (rc) return rc;
   // fc4: X = a3 flat; f16x2 with the prepared weights' a3 bound and max |d4|
   // (published by the dX chain's heads kernel)
   const unsigned* a3b =
       prep ? reinterpret_cast<const unsigned*>(prep + TowerPrep<C3>::HDR) + kTowMaxA3 : nullptr;
-  rc = wgrad_layer(DenseRows{a->a3, 49 * C3, B, 49 * C3}, 49 * C3, B, bw->d4, 512, 512, st,
-                   part, ws_cap, grads + L.off[6], 512, nullptr,
-                   st ? astat + L.stat_off[3] : nullptr, s, 0, 1.f, a3b, a3b ? bscr + kBsMaxD4 : nullptr);
+  rc = layer([&](float* pt, long long cap, long long* used) {
+    return wgrad_layer(DenseRows{a->a3, 49 * C3, B, 49 * C3}, 49 * C3, B, bw->d4, 512, 512, st, pt, cap,
+                       grads + L.off[6], 512, nullptr, st ? astat + L.stat_off[3] : nullptr, s, 0, 1.f, a3b,
+                       a3b ? bscr + kBsMaxD4 : nullptr, &fin, used);
+  });
   if (rc) return rc;
+  flush();
   // conv3 / conv2: pixel-pair band reductions over the dense activation rows
   // (band.hpp), or the patches of a2 / a1
   const long long band_cap = pcap_all - kBandScratch;
