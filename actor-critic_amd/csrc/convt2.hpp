@@ -47,9 +47,10 @@ struct CT2 {
 };
 
 // max |W2| into the prepared block's scale word (zeroed by the caller)
-__global__ __launch_bounds__(256) void convt2_wmax_kernel(const float* w2, char* out) {
+// (block b of nb; 256 threads)
+__device__ __forceinline__ void convt2_wmax_body(const float* w2, char* out, int b, int nb) {
   float m = 0.f;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < 16 * CT2::CIN * CT2::COUT; i += gridDim.x * 256)
+  for (int i = b * 256 + threadIdx.x; i < 16 * CT2::CIN * CT2::COUT; i += nb * 256)
     m = fmaxf(m, fabsf(w2[i]));
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) amax_update(reinterpret_cast<unsigned*>(out + CT2::FRAG_BYTES), m);
@@ -57,8 +58,9 @@ __global__ __launch_bounds__(256) void convt2_wmax_kernel(const float* w2, char*
 
 // prepared weights: fragment (ks, phase) lane l holds W[py+2a][px+2b][ci][co..co+7],
 // ci = l & 31, tap t = ks >> 2 = (a, b), co = 16 (ks & 3) + 8 (l >> 5)
-__global__ void convt2_prep_kernel(const float* w2, char* out) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;  // (ks, phase, lane)
+// (block b; 256 threads)
+__device__ __forceinline__ void convt2_prep_body(const float* w2, char* out, int blk) {
+  const int g = blk * 256 + threadIdx.x;  // (ks, phase, lane)
   if (g >= CT2::NKS * 4 * 64) return;
   const int lane = g & 63, ph = (g >> 6) & 3, ks = g >> 8;
   const int py = ph >> 1, px = ph & 1, t = ks >> 2, a = t >> 1, b = t & 1;

@@ -30,8 +30,9 @@ constexpr int kFc4Depth = ACMI_FC4_DEPTH;  // k-steps in flight ahead of the one
 
 // W4 [K][512] -> [K/16 steps][16 col tiles][part h, l][64 lanes] x 16 B, scaled
 // by the power of two of hdr[kTowMaxW4] (the tower's header)
-__global__ void fc4_prep_kernel(const float* w4, int K, char* out, const unsigned* hdr) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+// (block b; 256 threads)
+__device__ __forceinline__ void fc4_prep_body(const float* w4, int K, char* out, const unsigned* hdr, int b) {
+  const int g = b * 256 + threadIdx.x;
   const int lane = g & 63, f = g >> 6;  // f = step * 16 + col tile
   if (f >= (K / 16) * 16) return;
   const float sw = f16x2_scale_of_bits(hdr + kTowMaxW4);

@@ -1678,6 +1678,42 @@ __global__ __launch_bounds__(256) void zero2_kernel(uint4* a, long long na, uint
   }
 }
 
+// acmi_conv_prepare's two dependent passes, each one launch over block ranges:
+//   bounds: the tower's header (tower_stats_body, 64 blocks) and max |W2| of conv2's
+//     input-gradient weights (convt2_wmax_body, kPrepWmaxBlocks), atomicMax into
+//     the zeroed words;
+//   split: the a3 bound from the final a2 bound (tower_stats3_body, four columns per
+//     block), then the f16x2 fragments of the tower, of conv2's input gradient and
+//     of fc4 (each scaled by a bound of the first pass)
+constexpr int kPrepWmaxBlocks = 32;
+struct PrepArgs {
+  const float *w1, *b1, *w2, *b2, *w3, *b3, *w4;
+  int C3, K4;
+  char* tower;       // TowerPrep<C3>
+  unsigned* hdr;     // its bounds header
+  char* ct2;         // CT2 block
+  char* fc4;         // fc4 fragments
+  int nb3, nbt, nbc;  // split-pass block counts: stats3, tower, convt2 (fc4 after)
+};
+__global__ __launch_bounds__(256) void conv_prep_bounds_kernel(PrepArgs a) {
+  const int b = blockIdx.x;
+  if (b < 64) tower_stats_body(a.w1, a.b1, a.w2, a.b2, a.w3, 576 * a.C3, a.w4, a.K4 * 512, a.hdr, b);
+  else convt2_wmax_body(a.w2, a.ct2, b - 64, kPrepWmaxBlocks);
+}
+__global__ __launch_bounds__(256) void conv_prep_split_kernel(PrepArgs a) {
+  int b = blockIdx.x;
+  if (b < a.nb3) {
+    const int co = 4 * b + (threadIdx.x >> 6);
+    if (co < a.C3) tower_stats3_body(a.w3, a.b3, a.C3, a.hdr, co);
+  } else if ((b -= a.nb3) < a.nbt) {
+    tower_prep_body(a.w1, a.w2, a.w3, a.C3, a.tower, a.hdr, b);
+  } else if ((b -= a.nbt) < a.nbc) {
+    convt2_prep_body(a.w2, a.ct2, b);
+  } else {
+    fc4_prep_body(a.w4, a.K4, a.fc4, a.hdr, b - a.nbc);
+  }
+}
+
 int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
   Layout L;
   ACMI_REQUIRE(net && net->params && prep && make_layout(net->num_actions, net->conv3_filters, &L),
@@ -1694,16 +1730,15 @@ int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
                      reinterpret_cast<uint4*>(static_cast<char*>(prep) + oh), TowerPrep<32>::HDR_BYTES / 16,
                      reinterpret_cast<uint4*>(static_cast<char*>(prep) + o2 + CT2::FRAG_BYTES),
                      (CT2::BYTES - CT2::FRAG_BYTES) / 16);
-  launch_tower_prep(net->params, L.off, L.C3, prep, (hipStream_t)stream);
-  // conv2's input-gradient weights: max |W2| (the f16x2 scale), then the split
-  hipLaunchKernelGGL(convt2_wmax_kernel, dim3(32), dim3(256), 0, (hipStream_t)stream, net->params + L.off[2],
-                     static_cast<char*>(prep) + o2);
-  hipLaunchKernelGGL(convt2_prep_kernel, dim3(CT2::NKS * 4 * 64 / 256), dim3(256), 0, (hipStream_t)stream,
-                     net->params + L.off[2], static_cast<char*>(prep) + o2);
-  const int K4 = 49 * L.C3;
-  hipLaunchKernelGGL(fc4_prep_kernel, dim3(K4 / 16 * 16 * 64 / 256), dim3(256), 0, (hipStream_t)stream,
-                     net->params + L.off[6], K4, static_cast<char*>(prep) + o2 + CT2::BYTES,
-                     reinterpret_cast<const unsigned*>(static_cast<char*>(prep) + oh));
+  const float* P = net->params;
+  char* base = static_cast<char*>(prep);
+  PrepArgs a{P + L.off[0], P + L.off[1], P + L.off[2], P + L.off[3], P + L.off[4], P + L.off[5], P + L.off[6],
+             L.C3, 49 * L.C3, base, reinterpret_cast<unsigned*>(base + oh), base + o2, base + o2 + CT2::BYTES,
+             L.C3 / 4, (16 + 64 + 36 * (L.C3 / 32)) * 64 / 256 + 1, CT2::NKS * 4 * 64 / 256};
+  const int nbf = a.K4 / 16 * 16 * 64 / 256;
+  hipLaunchKernelGGL(conv_prep_bounds_kernel, dim3(64 + kPrepWmaxBlocks), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(conv_prep_split_kernel, dim3(a.nb3 + a.nbt + a.nbc + nbf), dim3(256), 0, (hipStream_t)stream,
+                     a);
   ACMI_LAUNCH_CHECK("acmi_conv_prepare");
   return ACMI_OK;
 }

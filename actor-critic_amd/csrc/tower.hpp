@@ -115,13 +115,14 @@ enum {
 
 // the header's bounds (zeroed by the caller): 64 blocks of band.hpp's a1 / a2
 // bounds (block c' takes conv2's column c') plus max |W| over all four layers
-__global__ __launch_bounds__(256) void tower_stats_kernel(const float* w1, const float* b1, const float* w2,
-                                                         const float* b2, const float* w3, int n3,
-                                                         const float* w4, int n4, unsigned* hdr) {
+// (block co of 64; 256 threads)
+__device__ __forceinline__ void tower_stats_body(const float* w1, const float* b1, const float* w2, const float* b2,
+                                                 const float* w3, int n3, const float* w4, int n4, unsigned* hdr,
+                                                 int co) {
   __shared__ float part[8][32];
   __shared__ float B1[32];
   __shared__ float red[4];
-  const int t = threadIdx.x, co = blockIdx.x;
+  const int t = threadIdx.x;
   {
     const int c = t & 31, q = t >> 5;
     float acc = 0.f;
@@ -187,10 +188,9 @@ __global__ __launch_bounds__(256) void tower_stats_kernel(const float* w1, const
 }
 
 // the a3 bound from the final a2 bound: block co takes conv3's column co,
-// a3 <= sum_k max(W3[k][co], 0) * max a2 + max(b3[co], 0)
-__global__ __launch_bounds__(64) void tower_stats3_kernel(const float* w3, const float* b3, int C3,
-                                                          unsigned* hdr) {
-  const int co = blockIdx.x, t = threadIdx.x;
+// a3 <= sum_k max(W3[k][co], 0) * max a2 + max(b3[co], 0)  (one wave per column)
+__device__ __forceinline__ void tower_stats3_body(const float* w3, const float* b3, int C3, unsigned* hdr, int co) {
+  const int t = threadIdx.x & 63;
   float acc = 0.f;
   for (int k = t; k < 576; k += 64) acc += fmaxf(w3[k * C3 + co], 0.f);
   acc = wave_sum(acc);
@@ -198,9 +198,10 @@ __global__ __launch_bounds__(64) void tower_stats3_kernel(const float* w3, const
   if (t == 0) amax_update(hdr + kTowMaxA3, acc * a2 + fmaxf(b3[co], 0.f));
 }
 
-__global__ void tower_prep_kernel(const float* w1, const float* w2, const float* w3, int C3, char* out,
-                                  const unsigned* hdr) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;  // (layer, step, tile, lane)
+// (block b; 256 threads: four fragments)
+__device__ __forceinline__ void tower_prep_body(const float* w1, const float* w2, const float* w3, int C3, char* out,
+                                                const unsigned* hdr, int b) {
+  const int g = b * 256 + threadIdx.x;  // (layer, step, tile, lane)
   const int lane = g & 63;
   int f = g >> 6;  // fragment index over the three layers
   const int n3 = 36 * (C3 / 32);
@@ -601,18 +602,6 @@ inline void launch_tower(const uint8_t* obs, long long img_stride, int B, const 
   else
     hipLaunchKernelGGL((tower_kernel<C3, false>), dim3(B), dim3(256), 0, s, obs, img_stride, P + off[1],
                        P + off[3], P + off[5], a1, a2, a3, st, pp, m1, m2, m3);
-}
-
-// the header must be zero before the stats kernel's atomicMax (memset by the caller)
-inline void launch_tower_prep(const float* P, const long long* off, int C3, void* prep, hipStream_t s) {
-  const long long hdr = C3 == 32 ? TowerPrep<32>::HDR : TowerPrep<64>::HDR;
-  unsigned* h = reinterpret_cast<unsigned*>(static_cast<char*>(prep) + hdr);
-  hipLaunchKernelGGL(tower_stats_kernel, dim3(64), dim3(256), 0, s, P + off[0], P + off[1], P + off[2],
-                     P + off[3], P + off[4], 576 * C3, P + off[6], 49 * C3 * 512, h);
-  hipLaunchKernelGGL(tower_stats3_kernel, dim3(C3), dim3(64), 0, s, P + off[4], P + off[5], C3, h);
-  const int frags = 16 + 64 + 36 * (C3 / 32);
-  hipLaunchKernelGGL(tower_prep_kernel, dim3(frags * 64 / 256 + 1), dim3(256), 0, s, P + off[0], P + off[2],
-                     P + off[4], C3, static_cast<char*>(prep), h);
 }
 
 }  // namespace acmi
