@@ -33,15 +33,21 @@ def main(path, marker='returns_kernel', skip=0):
     win = [(b, e, n) for b, e, n in ev if w0 <= b < w1]
     busy, cur_b, cur_e = 0, None, None
     gaps = []
+    where = {}  # (kernel before, kernel after) -> idle ns
+    short = lambda n: n.split('(')[0].split('<')[0].replace('void ', '').replace('acmi::', '')[:40]
+    prev = None
     for b, e, n in win:
         if cur_e is None:
             cur_b, cur_e = b, e
         elif b > cur_e:
             busy += cur_e - cur_b
             gaps.append(b - cur_e)
+            key = (short(prev), short(n))
+            where[key] = where.get(key, 0) + (b - cur_e)
             cur_b, cur_e = b, e
         else:
             cur_e = max(cur_e, e)
+        prev = n
     busy += min(cur_e, w1) - cur_b
     if w1 > cur_e:  # the idle time before the next iteration's first kernel
         gaps.append(w1 - cur_e)
@@ -63,6 +69,10 @@ def main(path, marker='returns_kernel', skip=0):
         big = [g for g in gaps if g > 20000]
         print('| gaps > 20 us: count / total per iteration | {:.1f} / {:.3f} ms |'.format(
             len(big) / iters, sum(big) / iters / 1e6))
+    print('\n| idle before | after | us / iter |')
+    print('|---|---|---|')
+    for k in sorted(where, key=lambda x: -where[x])[:12]:
+        print('| `{}` | `{}` | {:.1f} |'.format(k[0], k[1], per(where[k])))
     tot = {}
     cnt = {}
     for b, e, n in win:
