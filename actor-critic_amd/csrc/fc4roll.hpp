@@ -14,7 +14,7 @@
 // (590 KB) and a3 columns (400 KB at B = 512).
 //
 // Arithmetic: f16x2 (f16x2.hpp) -- W4 scaled by its max |W4|, a3 by the weight-
-// derived a3 bound of the tower's header (tower_stats3_kernel), three MFMAs per
+// derived a3 bound of the tower's header (tower_stats3_body), three MFMAs per
 // k16-step and tile, the slabs unscaled before they are stored: f32-class like
 // the staged bf16x3 launch (test_fc4_rollout_matches_gemm3), not bit-identical.
 #pragma once

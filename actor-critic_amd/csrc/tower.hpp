@@ -14,7 +14,7 @@
 // per-layer kernels instead.)
 //
 // Arithmetic: f16x2 split operands (f16x2.hpp), each tensor scaled by a power of
-// two from a bound the prepare step computes (tower_stats_kernel): the weights'
+// two from a bound the prepare step computes (tower_stats_body, in acmi_conv_prepare's first launch): the weights'
 // max |W|, and the a1 / a2 bounds of band.hpp (ReLU outputs of [0,1] pixels
 // under the positive weight mass).  conv1: u8 pixels exact as f16 subnormals
 // (one byte permute per two), two MFMAs per k16 against the weights' h/l (bf16x3
@@ -96,7 +96,7 @@ struct TowOut {  // one image's a1 / a2 in global memory as a buffer (SGPR base,
 // fragment-major -- [k16 step][32-col tile][part h,l][lane] x 16 B -- so the
 // tower loads them with one 16-byte load per part instead of 8 scalar loads and
 // a split per k-step and wave; then a header of bounds (bit patterns, for the
-// atomicMax of tower_stats_kernel): max |W1|, |W2|, |W3|, the a1, a2 and a3
+// atomicMax of tower_stats_body): max |W1|, |W2|, |W3|, the a1, a2 and a3
 // bounds, max |W4| (fc4roll.hpp's prepared fc4 reads the last two).
 template <int C3>
 struct TowerPrep {
