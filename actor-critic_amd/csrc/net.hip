@@ -1408,12 +1408,18 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // conv3 / conv2: pixel-pair band reductions over the dense activation rows
   // (band.hpp), or the patches of a2 / a1
   const long long band_cap = pcap_all - kBandScratch;
+  // a1 / a2 bounds from the weights (max |d2|, |d3| came with the dX chain): the
+  // prepared weights' header holds them (tower_stats_body, the same sums as
+  // band_bounds_kernel), else computed here
+  const unsigned* xb = prep ? reinterpret_cast<const unsigned*>(prep + TowerPrep<C3>::HDR) : nullptr;
+  const unsigned* a1b = xb ? xb + kTowMaxA1 : bscr + kBsMaxA1;
+  const unsigned* a2b = xb ? xb + kTowMaxA2 : bscr + kBsMaxA2;
   if (band) {
-    // a1 / a2 bounds from the weights (max |d2|, |d3| came with the dX chain)
-    hipLaunchKernelGGL(band_bounds_kernel, dim3(64), dim3(256), 0, s, P + L.off[0], P + L.off[1], P + L.off[2],
-                       P + L.off[3], bscr);
+    if (!xb)
+      hipLaunchKernelGGL(band_bounds_kernel, dim3(64), dim3(256), 0, s, P + L.off[0], P + L.off[1], P + L.off[2],
+                         P + L.off[3], bscr);
     rc = band_layer(a->a2, 9, 9, 64, 3, 3, 1, bw->d3, C3, B, part, band_cap, grads + L.off[4],
-                    astat + L.stat_off[2], 1.f, bscr + kBsMaxA2, bscr + kBsMaxD3, s);
+                    astat + L.stat_off[2], 1.f, a2b, bscr + kBsMaxD3, s);
   } else
     rc = wgrad_layer(ConvRows<float, 9, 9, 64, 3, 3, 1>{a->a2, 81 * 64, B * 49}, 576, 49LL * B,
                      bw->d3, C3, C3, st, part, ws_cap, grads + L.off[4], C3, nullptr,
@@ -1421,7 +1427,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   if (rc) return rc;
   if (band)
     rc = band_layer(a->a1, 20, 20, 32, 4, 4, 2, bw->d2, 64, B, part, band_cap, grads + L.off[2],
-                    astat + L.stat_off[1], 1.f, bscr + kBsMaxA1, bscr + kBsMaxD2, s, ACMI_PROF_CONV2_WGRAD);
+                    astat + L.stat_off[1], 1.f, a1b, bscr + kBsMaxD2, s, ACMI_PROF_CONV2_WGRAD);
   else
     rc = wgrad_layer(ConvRows<float, 20, 20, 32, 4, 4, 2>{a->a1, 400 * 32, B * 81}, 512,
                      81LL * B, bw->d2, 64, 64, st, part, ws_cap, grads + L.off[2], 64, nullptr,
