@@ -541,14 +541,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   }
 }
 
-// chunks for the one-block-per-chunk kernel: 2 blocks per CU resident
-// chunk count a multiple of `slots` (ACMI_AF_SLOTS; default one block per CU per
-// round: 256 against 512 measured configs[2] 477-480 K -> 490-491 K env-steps/s, the
-// default config unchanged -- the chunk partials' reduction and the fused weight
-// gradient's finalize halve; 384 and 1024 slower, profiles/r04_ab/af_slots.txt)
+// chunks for the one-block-per-chunk kernel: the chunk count is a multiple of
+// 256 slots, one block per CU per round (against 512: configs[2] 477-480 K ->
+// 490-491 K env-steps/s, the default config unchanged -- the chunk partials'
+// reduction and the fused weight gradient's finalize halve; 128 / 384 / 1024
+// slower, profiles/r04_ab/af_slots.txt)
 static void af_plan_tri(long long rows, int* nchunk, int* chunk) {
-  static const long long forced = getenv("ACMI_AF_SLOTS") ? atoll(getenv("ACMI_AF_SLOTS")) : 0;
-  const long long slots = forced > 0 ? forced : 256;
+  const long long slots = 256;
   const long long nc0 = std::max<long long>(1, (rows + AF_CHUNK - 1) / AF_CHUNK);
   const long long rounds = (nc0 + slots - 1) / slots;
   const long long nc = std::max<long long>(nc0, rounds * slots);

@@ -127,12 +127,11 @@ inline const BandDev* band_dev(int H, int W, int C, int KH, int KW, int S, int C
   return d;
 }
 
-// Chunks of the M image rows: ACMI_BAND_CHUNKS forces the count; by default
-// about three items per CU over the whole grid (the groups differ in work, so
-// shorter items late in the grid fill the CUs), chunks >= 512 rows.
+// Chunks of the M image rows: about three items per CU over the whole grid (the
+// groups differ in work, so shorter items late in the grid fill the CUs), chunks
+// >= 512 rows (2 / 3 / 5 / 6 / 8 chunks measured slower than 4 at conv2, M = 10240)
 inline void band_chunks(long long rows, int ngroups, int* nc, int* ch) {
-  static const int forced = getenv("ACMI_BAND_CHUNKS") ? atoi(getenv("ACMI_BAND_CHUNKS")) : 0;
-  long long n = forced > 0 ? forced : std::max(1, (3 * 256 + ngroups / 2) / std::max(1, ngroups));
+  long long n = std::max(1, (3 * 256 + ngroups / 2) / std::max(1, ngroups));
   n = std::max(1LL, std::min(n, rows / 512 > 0 ? rows / 512 : 1));
   long long c = (rows + n - 1) / n;
   c = (c + 15) / 16 * 16;

@@ -435,10 +435,9 @@ int g_forward_mode = [] {
 // split factor for fc4 at small batch (64 x 128 tiles over 512 columns; 4 / 6 /
 // 12 / 16 chunks measured no better than 8)
 static void fc4_plan(int B, int K, int* nz, int* chunk) {
-  // ACMI_FC4_SPLIT_SMALL: the split cap at batches <= 128 (default 16: the chain
-  // of k-steps per chunk, not the slab traffic, sets fc4's time there)
-  static const int small_sp = getenv("ACMI_FC4_SPLIT_SMALL") ? atoi(getenv("ACMI_FC4_SPLIT_SMALL")) : 16;
-  const int maxsp = B <= 128 ? std::max(1, std::min(16, small_sp)) : 8;
+  // the split cap at batches <= 128 is 16: the chain of k-steps per chunk, not
+  // the slab traffic, sets fc4's time there (14 / 16 measured best)
+  const int maxsp = B <= 128 ? 16 : 8;
   const int blocks = cdiv(B, 64) * 4;
   int sp = blocks >= 256 ? 1 : std::min(maxsp, cdiv(256 * maxsp / 8, blocks));
   const int q = g_gemm_mode == ACMI_GEMM_X3 ? 16 : 32;  // the split GEMM's K-tile

@@ -99,6 +99,9 @@ def parse():
                         'needs --num-actions 18); default: every env synthetic Breakout')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-iters', type=int, default=3, help='timed CPU-baseline iterations (at most ~20 s)')
+    p.add_argument('--no-configs2', action='store_true',
+                   help='skip the nested BASELINE configs[2] line (ACKTR 32 envs x 20 steps) timed after the headline')
+    p.add_argument('--configs2-steps', type=int, default=60)
     p.add_argument('--quiet', action='store_true')
     return p.parse_args()
 
@@ -154,7 +157,11 @@ def main():
     run(args)
 
 
-def run(args):
+def _measure(args, N, T, A, algo, games, steps, warmup, prof_site=None):
+    """Build the reference training graph for one workload and time `steps`
+    iterations after `warmup` (barrier + synchronize on both sides; wall time is
+    the max over ranks).  prof_site: the libacmi HIP-event profiling site of the
+    roofline kernel (timed only for the headline workload)."""
     from actorcritic import _lib, parallel
     from actorcritic import session as sess
     from actorcritic.agents import MultiEnvAgent
@@ -165,23 +172,14 @@ def run(args):
     from actorcritic.nn import linear_decay
     from actorcritic.objectives import A2CObjective
 
-    world, rank = parallel.init_from_env()
-    if args.forward is not None:
-        _lib.call('acmi_set_forward_mode', _lib.FWD_BF16 if args.forward == 'bf16' else _lib.FWD_F32)
-    args.forward = 'bf16' if _lib.load().acmi_get_forward_mode() == _lib.FWD_BF16 else 'f32'
-    if world != args.gpus:
-        raise SystemExit('bench: --gpus {} but the process group has {} ranks (WORLD_SIZE={})'.format(
-            args.gpus, world, os.environ.get('WORLD_SIZE')))
+    world, rank = parallel.world_size(), parallel.rank()
     dev = torch.device('cuda', torch.cuda.current_device())
-    acktr = args.algo == 'acktr'
-    N = args.envs_per_gpu
-    T = args.nsteps or (20 if acktr else 5)
+    acktr = algo == 'acktr'
     C3 = 32 if acktr else 64
-    A = args.num_actions
 
     sess.reset_default_graph()
     env = MultiEnv(SyntheticAtariEnvs(N, num_actions=A, seed=1234, env_offset=rank * N, device=dev,
-                                      games=args.games))
+                                      games=games))
     model = AtariModel(env.observation_space, env.action_space, C3, random_seed=7, device=dev)
     agent = MultiEnvAgent(env, model, T)
     objective = A2CObjective(model, discount_factor=0.99, entropy_regularization_strength=0.01)
@@ -205,40 +203,94 @@ def run(args):
         if marks is not None:
             marks[2].record()
 
+    tot_ms, cnt = ctypes.c_double(), ctypes.c_int()
     with sess.Session(dev) as s:
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             iteration(s)
         torch.cuda.synchronize()
         parallel.barrier()
         torch.cuda.synchronize()
-        site = _lib.PROF_CONV2_WGRAD
-        _lib.call('acmi_prof_enable', site, max(1, args.steps))
+        if prof_site is not None:
+            _lib.call('acmi_prof_enable', prof_site, max(1, steps))
         model.engine.comm_timing(True)
-        marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
         inv_flags = []
         t0 = time.perf_counter()
-        for k in range(args.steps):
+        for k in range(steps):
             iteration(s, marks[k])
             inv_flags.append(bool(getattr(optimizer, 'last_flags', (0, 0, 0))[2]) if acktr else False)
         torch.cuda.synchronize()
         parallel.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        tot_ms, cnt = ctypes.c_double(), ctypes.c_int()
-        _lib.call('acmi_prof_collect', ctypes.byref(tot_ms), ctypes.byref(cnt))
-        _lib.call('acmi_prof_enable', 0, 0)
+        if prof_site is not None:
+            _lib.call('acmi_prof_collect', ctypes.byref(tot_ms), ctypes.byref(cnt))
+            _lib.call('acmi_prof_enable', 0, 0)
         comm_ms, comm_bytes, comm_n = model.engine.comm_collect()
         model.engine.comm_timing(False)
     elapsed = parallel.max_over_ranks(elapsed, dev)
     comm_ms_max = parallel.max_over_ranks(comm_ms, dev)
     roll_ms = [m[0].elapsed_time(m[1]) for m in marks]
     upd_ms = [m[1].elapsed_time(m[2]) for m in marks]
-    env_steps = N * T * args.steps * world
-    value = env_steps / elapsed
-    ms_per_step = 1e3 * elapsed / args.steps
-    upd_inv = [u for u, f in zip(upd_ms, inv_flags) if f]
-    upd_plain = [u for u, f in zip(upd_ms, inv_flags) if not f]
     mean = lambda xs: (sum(xs) / len(xs)) if xs else None
+    return dict(value=N * T * steps * world / elapsed, ms_per_step=1e3 * elapsed / steps, elapsed=elapsed,
+                update_ms=mean(upd_ms), update_ms_inverse_iters=mean([u for u, f in zip(upd_ms, inv_flags) if f]),
+                update_ms_plain_iters=mean([u for u, f in zip(upd_ms, inv_flags) if not f]),
+                rollout_ms=mean(roll_ms), comm_ms=comm_ms_max, comm_bytes=comm_bytes, comm_n=comm_n,
+                prof_ms=tot_ms.value, prof_n=cnt.value)
+
+
+def _cpu_leg(N, T, A, C3, algo, games, iters):
+    """The CPU baseline (oracle/cpu_baseline.py: measurement infrastructure, run
+    after the timed GPU region) on the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import cpu_baseline
+    r = cpu_baseline.run(n_envs=N, n_steps=T, iters=iters, A=A, C3=C3, algo=algo, games=games)
+    return {'value': r['env_steps_per_s'], 'unit': 'env-steps/s', 'cores': r['threads'], 'kind': 'port',
+            'sample': '{} timed iterations (after one warm-up; per iteration min {:.2f} s, max {:.2f} s) of '
+                      'the same {} workload ({} envs x {} steps): torch-CPU fp32 restatement, {}{}'.format(
+                          r['iters'], min(r['iter_s']), max(r['iter_s']), algo.upper(), r['n_envs'],
+                          r['n_steps'], r['structure'],
+                          ', K-FAC inverse timed once and amortised 1/10' if algo == 'acktr' else ''),
+            'iter_s': r['iter_s'], 'update_ms': r['update_ms'], 'rollout_ms': r['rollout_ms']}
+
+
+def run(args):
+    from actorcritic import _lib, parallel
+
+    world, rank = parallel.init_from_env()
+    if args.forward is not None:
+        _lib.call('acmi_set_forward_mode', _lib.FWD_BF16 if args.forward == 'bf16' else _lib.FWD_F32)
+    args.forward = 'bf16' if _lib.load().acmi_get_forward_mode() == _lib.FWD_BF16 else 'f32'
+    if world != args.gpus:
+        raise SystemExit('bench: --gpus {} but the process group has {} ranks (WORLD_SIZE={})'.format(
+            args.gpus, world, os.environ.get('WORLD_SIZE')))
+    acktr = args.algo == 'acktr'
+    N = args.envs_per_gpu
+    T = args.nsteps or (20 if acktr else 5)
+    C3 = 32 if acktr else 64
+    A = args.num_actions
+    r = _measure(args, N, T, A, args.algo, args.games, args.steps, args.warmup, prof_site=_lib.PROF_CONV2_WGRAD)
+    value, ms_per_step = r['value'], r['ms_per_step']
+    tot_ms = ctypes.c_double(r['prof_ms'])
+    cnt = ctypes.c_int(r['prof_n'])
+
+    # BASELINE configs[2] (the reference's own ACKTR config, a2c_acktr.py:306-310:
+    # 32 envs x 20 steps, Breakout, f32) -- the config north_star's ">=10x the
+    # reference CPU at 1 GPU" target is stated on -- timed by the same clock in the
+    # same run, with its SubprocessEnv CPU leg (32 Pipe children)
+    c2 = None
+    if (world == 1 and not args.no_configs2
+            and not (acktr and N == 32 and T == 20 and A == 4 and args.forward == 'f32' and not args.games)):
+        fwd_mode = _lib.load().acmi_get_forward_mode()
+        _lib.call('acmi_set_forward_mode', _lib.FWD_F32)
+        c2r = _measure(args, 32, 20, 4, 'acktr', None, args.configs2_steps, max(5, args.warmup))
+        _lib.call('acmi_set_forward_mode', fwd_mode)
+        c2 = {'workload': workload_name('acktr', 32, 20, 4, 'f32', 1), 'envs': 32, 'num_steps': 20,
+              'num_actions': 4, 'forward': 'f32', 'steps': args.configs2_steps, 'warmup': max(5, args.warmup),
+              'value': c2r['value'], 'unit': 'env-steps/s', 'ms_per_step': c2r['ms_per_step'],
+              'update_ms': c2r['update_ms'], 'update_ms_inverse_iters': c2r['update_ms_inverse_iters'],
+              'update_ms_plain_iters': c2r['update_ms_plain_iters'], 'rollout_ms': c2r['rollout_ms']}
 
     # dominant kernel: conv2 weight gradient fused with the K-FAC A factor,
     # [P;1]^T [P | dY] over the M*81 conv2 output pixels, P = 4x4x32 patches.
@@ -302,19 +354,12 @@ def run(args):
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, 'oracle'))
-        import cpu_baseline
         # the same workload as the GPU line (envs, steps, algorithm, actions, C3)
-        r = cpu_baseline.run(n_envs=N, n_steps=T, iters=args.cpu_iters, A=A, C3=C3, algo=args.algo,
-                             games=args.games)
-        cpu = {'value': r['env_steps_per_s'], 'unit': 'env-steps/s', 'cores': r['threads'], 'kind': 'port',
-               'sample': '{} timed iterations (after one warm-up; per iteration min {:.2f} s, max {:.2f} s) of '
-                         'the same {} workload ({} envs x {} steps): torch-CPU fp32 restatement, {}{}'.format(
-                             r['iters'], min(r['iter_s']), max(r['iter_s']), args.algo.upper(), r['n_envs'],
-                             r['n_steps'], r['structure'],
-                             ', K-FAC inverse timed once and amortised 1/10' if acktr else ''),
-               'iter_s': r['iter_s'],
-               'update_ms': r['update_ms'], 'rollout_ms': r['rollout_ms']}
+        cpu = _cpu_leg(N, T, A, C3, args.algo, args.games, args.cpu_iters)
+        if c2 is not None:
+            # configs[2]'s CPU leg: 32 SubprocessEnv children behind the Pipe protocol
+            c2['cpu_baseline'] = _cpu_leg(32, 20, 4, 32, 'acktr', None, args.cpu_iters)
+            c2['speedup_vs_cpu'] = c2['value'] / c2['cpu_baseline']['value']
 
     if rank == 0:
         out = {
@@ -327,13 +372,15 @@ def run(args):
                        'envs_per_gpu': N, 'num_steps': T,
                 'global_envs': N * world, 'num_actions': A, 'conv3_filters': C3, 'forward': args.forward,
                 'parallelism': 'dp{}'.format(world)},
-            'update_ms': mean(upd_ms), 'update_ms_inverse_iters': mean(upd_inv),
-            'update_ms_plain_iters': mean(upd_plain), 'rollout_ms': mean(roll_ms),
+            'update_ms': r['update_ms'], 'update_ms_inverse_iters': r['update_ms_inverse_iters'],
+            'update_ms_plain_iters': r['update_ms_plain_iters'], 'rollout_ms': r['rollout_ms'],
             # communication: compute-stream stall on the per-update all-reduce
             # (NetEngine.comm_timing; max over ranks), bytes summed per update
-            'allreduce_ms': comm_ms_max if world > 1 else 0.0, 'allreduce_bytes': comm_bytes,
-            'allreduce_updates_timed': comm_n, 'dist_backend': parallel.backend_name(),
+            'allreduce_ms': r['comm_ms'] if world > 1 else 0.0, 'allreduce_bytes': r['comm_bytes'],
+            'allreduce_updates_timed': r['comm_n'], 'dist_backend': parallel.backend_name(),
             'roofline': roofline, 'cpu_baseline': cpu,
+            # BASELINE configs[2] on the same clock (null at N > 1 or with --no-configs2)
+            'configs2': c2,
         }
         if cpu:
             out['speedup_vs_cpu'] = value / cpu['value']

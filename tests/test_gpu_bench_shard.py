@@ -86,13 +86,23 @@ class _Ref(object):
         d1 = _conv_input_grad(d2, w2, 2, m1.shape) * m1
         return [d1.reshape(-1, 32), d2.reshape(-1, 64), d3.reshape(-1, self.C3), d4, dlogits, dvalue[:, None]]
 
-    def add(self, obs, gpu_acts, dlogits, dvalue, g_pi, g_v):
+    def _inputs(self, obs, gpu_acts):
+        """The layer inputs from the GPU's own forward (a1..a4 in float64): what the
+        update is fed (a2c_acktr.py:243-247) when the forward is not float64-exact
+        (the bf16 tower of BASELINE configs[4])."""
+        a1, a2, a3, a4 = [a.to(self.dt) for a in gpu_acts]
+        x = obs.to(self.dt) / 255.0
+        return [_patches(x, 8, 4), _patches(a1, 4, 2), _patches(a2, 3, 1), a3.reshape(a3.shape[0], -1), a4]
+
+    def add(self, obs, gpu_acts, dlogits, dvalue, g_pi, g_v, gpu_inputs=False):
         """gpu_acts: the kernel forward's f32 a1..a4 of these images, whose ReLU
         masks the chains use: a pre-activation within f32 rounding of 0 may have
         the other sign in float64, and at 10240 rows such flips (one whole term of
         a cancelling sum each) would dominate the comparison of the backward's
-        arithmetic.  The forward itself is compared with float64 elsewhere."""
-        ins, _ = self._forward(obs)
+        arithmetic.  The forward itself is compared with float64 elsewhere.
+        gpu_inputs: take the layer inputs from gpu_acts too (else the float64
+        forward's)."""
+        ins = self._inputs(obs, gpu_acts) if gpu_inputs else self._forward(obs)[0]
         ins = ins + [ins[4]]
         masks = [(a > 0).to(self.dt) for a in gpu_acts]
         douts = self._chain(masks, dlogits, dvalue)
@@ -232,3 +242,144 @@ def test_update_statistics_with_tiny_output_gradients(lib, cuda):
     for k, (v, v32) in errs.items():
         tol = 5e-5 if k[0] == 'G' else 2e-5
         assert v < max(tol, 4 * v32), (k, v, v32)
+
+
+_SHARD_CASES = [
+    # (N, T, A, games, forward): the per-GPU shards of BASELINE configs[3] and configs[4]
+    (512, 20, 4, None, 'f32'),
+    (1024, 20, 18, 'atari57', 'bf16'),
+]
+
+
+@pytest.mark.parametrize('N,T,A,games,fwd', _SHARD_CASES, ids=['configs3-shard-512x20', 'configs4-shard-1024x20-a18-bf16'])
+def test_acktr_update_at_shard_size_matches_float64(lib, cuda, N, T, A, games, fwd):
+    """One steady-state ACKTR update at gs = 40 -- covariance EMA (first step, zero-
+    debiased: the batch statistics), the damped inverses (acmi_kfac_inverse), the
+    preconditioned trust-region momentum step (acmi_kfac_step) -- through the
+    reference's graph (objectives.optimize_shared, kfac_utils.py:38-53) at the
+    per-GPU shard sizes of BASELINE configs[3] (512 envs x 20 steps, M = 10240) and
+    configs[4] (1024 x 20 = 20480 rows, A = 18, mixed Atari-57 games, bf16 forward /
+    fp32 K-FAC): the production band plans, the 19-column heads and
+    kfac_narrow_kernel at their own sizes.
+
+    The float64 side (torch.float64 on the GPU for the 20480-row sums, numpy for the
+    inverses and the step: oracle.damped_inverses / kfac_step) is fed the GPU's own
+    forward -- activations, logits, values, targets (a2c_acktr.py:243-247) -- so it
+    checks the update's arithmetic on identical inputs.  Per K-FAC block: gradients
+    and A factors within 2e-5 (or 4x plain-f32 arithmetic of the same sums), G
+    factors 5e-5 (or 4x f32), damped inverses rel 1e-3, preconditioned gradient and
+    step rel-L2 1e-3 (north_star), the trust-region coefficient rel 1e-3.
+    References: kfac_utils.py:38-53, a2c_acktr.py:243-247, policies.py:146-158,
+    baselines.py:55-69."""
+    from actorcritic import session as sess
+    from actorcritic.agents import MultiEnvAgent
+    from actorcritic.envs.atari.model import AtariModel
+    from actorcritic.envs.atari.wrappers import SyntheticAtariEnvs
+    from actorcritic.examples.atari.a2c_acktr import create_optimizer
+    from actorcritic.multi_env import MultiEnv
+    from actorcritic.nn import linear_decay
+    from actorcritic.objectives import A2CObjective
+    C3 = 32
+    prev_mode = lib.acmi_get_forward_mode()
+    _lib.call('acmi_set_forward_mode', _lib.FWD_BF16 if fwd == 'bf16' else _lib.FWD_F32)
+    try:
+        sess.reset_default_graph()
+        kw = {} if games is None else dict(games=games)
+        env = MultiEnv(SyntheticAtariEnvs(N, num_actions=A, seed=11, device=cuda, **kw))
+        params = oracle.init_params(A, C3, seed=1)
+        model = AtariModel(env.observation_space, env.action_space, C3, params=params, random_seed=3, device=cuda)
+        agent = MultiEnvAgent(env, model, T)
+        obj = A2CObjective(model)
+        gs = sess.get_or_create_global_step()
+        opt = create_optimizer(True, model, linear_decay(0.25, 0.025, gs, 1000))
+        op = obj.optimize_shared(opt, 0.5, global_step=gs)
+        gs.assign(40)
+        M = N * T
+        with sess.Session() as s:
+            data = agent.interact(s)
+            feed = {model.observations_placeholder: data[0], model.bootstrap_observations_placeholder: data[4],
+                    model.actions_placeholder: data[1], model.rewards_placeholder: data[2],
+                    model.terminals_placeholder: data[3]}
+            fwd_out = model.engine.lookup_rollout(data[0])
+            acts = fwd_out.acts
+            gpu_acts = [acts.a1[:M].clone(), acts.a2[:M].clone(), acts.a3[:M].clone(), acts.a4[:M].clone()]
+            logits32 = fwd_out.flat_logits.cpu().numpy().copy()
+            value64 = fwd_out.flat_value.cpu().double().numpy()
+            p_before = model.params.cpu().numpy().astype(np.float64)
+            tg = np.asarray(s.run(obj.target_values, feed_dict=feed), np.float64).reshape(-1)
+            s.run(op, feed_dict=feed)
+            torch.cuda.synchronize()
+        assert opt.last_flags == (False, True, True), opt.last_flags  # K-FAC step + covariance + inverse
+        grads_gpu = model.engine.update_state(M).grads.cpu().numpy().astype(np.float64)
+        st = opt.state
+        fac = st['factors'].cpu().numpy().astype(np.float64)
+        got_pre = st['precon'].cpu().numpy().astype(np.float64)
+        got_p = model.params.cpu().numpy().astype(np.float64)
+        coeff_gpu = float(st['coeff'][0])
+        inv_got = st['inv']
+        obs = data[0].reshape(M, 84, 84, 4)
+        act = data[1].cpu().numpy().reshape(-1)
+        if games is not None:
+            assert act.max() >= 4  # the draws reach actions beyond Breakout's four
+    finally:
+        _lib.call('acmi_set_forward_mode', prev_mode)
+
+    # float64: head gradients of the loss and the sampled losses from the GPU's logits
+    lg = oracle.a2c_loss_and_head_grads(logits32.astype(np.float64), value64, act, tg)
+    g_pi, g_v, _ = oracle.sampled_head_grads(logits32, 0x4b464143, 0, 40)
+    blocks = [torch.from_numpy(b).to(cuda) for b in oracle.unpack(p_before, A, C3)]
+    ref = _Ref(blocks, A, C3, cuda)
+    ref32 = _Ref(blocks, A, C3, cuda, torch.float32)
+    dl = torch.from_numpy(np.asarray(lg['dlogits'])).to(cuda)
+    dv = torch.from_numpy(np.asarray(lg['dvalue'])).to(cuda)
+    gp = torch.from_numpy(np.asarray(g_pi, np.float64)).to(cuda)
+    gv = torch.from_numpy(np.asarray(g_v, np.float64)).to(cuda)
+    chunk = 1024
+    for i in range(0, M, chunk):
+        j = min(M, i + chunk)
+        for r in (ref, ref32):
+            r.add(obs[i:j], [a[i:j] for a in gpu_acts], dl[i:j].to(r.dt), dv[i:j].to(r.dt), gp[i:j].to(r.dt),
+                  gv[i:j].to(r.dt), gpu_inputs=True)
+    g_ref, a_ref, gf_ref = ref.result()
+    g_32, a_32, gf_32 = ref32.result()
+    L = model.engine.layout
+    names = ['conv1', 'conv2', 'conv3', 'fc4', 'fc_policy', 'fc_baseline']
+    off, nparams = oracle.param_offsets(A, C3)
+    spans = [(names[l], off[2 * l], off[2 * l + 2] if l < 5 else nparams) for l in range(6)]
+    g_ref_np = g_ref.cpu().numpy()
+    for name, lo, hi in spans:
+        v = np.abs(grads_gpu[lo:hi] - g_ref_np[lo:hi]).max() / np.abs(g_ref_np[lo:hi]).max()
+        v32 = _rel(g_32[lo:hi], g_ref[lo:hi])
+        print('grad %-11s kernel %.2e  plain f32 %.2e' % (name, v, v32))
+        assert v < max(2e-5, 4 * v32), ('grad', name, v, v32)
+    afac, gfac = [a.cpu().numpy() for a in a_ref], [g.cpu().numpy() for g in gf_ref]
+    for f in range(5):
+        d = L.din[f]
+        got = fac[L.stat_off[f]:L.stat_off[f] + d * d].reshape(d, d)
+        v, v32 = np.abs(got - afac[f]).max() / np.abs(afac[f]).max(), _rel(a_32[f], a_ref[f])
+        print('A %d kernel %.2e  plain f32 %.2e' % (f, v, v32))
+        assert v < max(2e-5, 4 * v32), ('A', f, v, v32)
+    for l in range(6):
+        d = L.dout[l]
+        got = fac[L.stat_off[5 + l]:L.stat_off[5 + l] + d * d].reshape(d, d)
+        v, v32 = np.abs(got - gfac[l]).max() / np.abs(gfac[l]).max(), _rel(gf_32[l], gf_ref[l])
+        print('G %d kernel %.2e  plain f32 %.2e' % (l, v, v32))
+        assert v < max(5e-5, 4 * v32), ('G', l, v, v32)
+    inv = oracle.damped_inverses(afac, gfac, 0.01)
+    for l in range(6):
+        for m, r in ((2 * l, inv[l][0]), (2 * l + 1, inv[l][1])):
+            got = L.inverse_block(inv_got, m).cpu().numpy().astype(np.float64)
+            rel = np.abs(got - r).max() / np.abs(r).max()
+            print('inverse %-11s %s rel %.2e' % (names[l], 'AG'[m % 2], rel))
+            assert rel < 1e-3, ('inverse', l, m % 2, rel)
+    new_p, _, precon, coeff = oracle.kfac_step(p_before, np.zeros_like(p_before), g_ref_np, inv,
+                                               oracle.linear_decay(0.25, 0.025, 40, 1000), 0.9, 1e-4, A, C3)
+    for name, lo, hi in spans:
+        e_pre = np.linalg.norm(got_pre[lo:hi] - precon[lo:hi]) / np.linalg.norm(precon[lo:hi])
+        e_step = np.linalg.norm(got_p[lo:hi] - new_p[lo:hi]) / np.linalg.norm(new_p[lo:hi] - p_before[lo:hi])
+        print('block %-11s precon rel-L2 %.2e  step rel-L2 %.2e' % (name, e_pre, e_step))
+        assert e_pre < 1e-3, (name, 'precon', e_pre)
+        assert e_step < 1e-3, (name, 'step', e_step)
+    print('coeff gpu %.6e float64 %.6e' % (coeff_gpu, coeff))
+    assert coeff_gpu == pytest.approx(coeff, rel=1e-3)
+    assert np.linalg.norm(got_pre - precon) / np.linalg.norm(precon) < 1e-3
