@@ -1053,6 +1053,17 @@ static GcovPlan gcov_plan(int n, long long rows) {
   return p;
 }
 
+// the partial floats gcov_layer will need (its two paths' plans)
+static long long gcov_need(int n, long long rows) {
+  if (n <= 32) {
+    int nc;
+    long long ch;
+    gram_plan(rows, &nc, &ch);
+    return (long long)nc * 33 * 32;
+  }
+  return gcov_plan(n, rows).floats;
+}
+
 // Launch [P;1]^T [P | dY] (with_stats; the 1 row is the column-sum row) or
 // [P;1]^T [dY] over rows.
 template <class Src>
@@ -1375,19 +1386,17 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
     fin.add(d, 0, 0, (int)cdiv(257 * 32, 32));
   }
   float* part = ws;
-  auto layer = [&](auto&& run) {
+  // need: the layer's partial floats (its plan), checked here so that a layer
+  // that does not fit after the others starts a new range instead of failing
+  auto layer = [&](long long need, auto&& run) {
     long long used = 0;
-    if (fin.n + 2 > kWgradTasks) flush();
-    int r = run(part + off, avail - off, &used);
-    if (r == ACMI_ERR_WS && off > 0) {
-      flush();
-      r = run(part, avail, &used);
-    }
+    if (fin.n + 2 > kWgradTasks || (off > 0 && need > avail - off)) flush();
+    const int r = run(part + off, avail - off, &used);
     off += (used + 3) / 4 * 4;
     return r;
   };
   // heads: X = a4 (512), dY = dhead (A+1 columns: pi | v)
-  rc = layer([&](float* pt, long long cap, long long* used) {
+  rc = layer(wgrad_plan(512, L.A + 1, st, B).floats, [&](float* pt, long long cap, long long* used) {
     return wgrad_layer(DenseRows{a->a4, 512, B, 512}, 512, B, bw->dhead, bw->ldh, L.A + 1, st, pt, cap,
                        grads + L.off[8], L.A, grads + L.off[10], st ? astat + L.stat_off[4] : nullptr, s, 0, 1.f,
                        nullptr, nullptr, &fin, used);
@@ -1397,7 +1406,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // (published by the dX chain's heads kernel)
   const unsigned* a3b =
       prep ? reinterpret_cast<const unsigned*>(prep + TowerPrep<C3>::HDR) + kTowMaxA3 : nullptr;
-  rc = layer([&](float* pt, long long cap, long long* used) {
+  rc = layer(wgrad_plan(49 * C3, 512, st, B).floats, [&](float* pt, long long cap, long long* used) {
     return wgrad_layer(DenseRows{a->a3, 49 * C3, B, 49 * C3}, 49 * C3, B, bw->d4, 512, 512, st, pt, cap,
                        grads + L.off[6], 512, nullptr, st ? astat + L.stat_off[3] : nullptr, s, 0, 1.f, a3b,
                        a3b ? bscr + kBsMaxD4 : nullptr, &fin, used);
@@ -1509,17 +1518,13 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
     fin.add(part, convt2_gram_blocks(B), 32, 32, gstat + L.stat_off[5 + 0], (int)(400LL * B), 1);
     off = ((long long)convt2_gram_blocks(B) * 33 * 32 + 3) / 4 * 4;
   }
-  // one Gram into the next free range: its worst case is the whole remaining cap
-  // (gcov_layer checks); retried from offset 0 after a flush when it does not fit
+  // one Gram into the next free range, or -- when its plan's partials do not fit
+  // after the others -- into a new range after the set so far is finalized
   auto gram = [&](const float* g, int ld, int n, long long rows, int sub, float* out, float* out_v, int vi,
                   const unsigned* gmax) {
     long long used = 0;
-    if (fin.n + 2 > kCovTasks) flush();
-    int r = gcov_layer(g, ld, n, rows, sub, part + off, cap - off, out, s, out_v, vi, gmax, &fin, &used);
-    if (r == ACMI_ERR_WS && off > 0) {
-      flush();
-      r = gcov_layer(g, ld, n, rows, sub, part, cap, out, s, out_v, vi, gmax, &fin, &used);
-    }
+    if (fin.n + 2 > kCovTasks || (off > 0 && gcov_need(n, rows) > cap - off)) flush();
+    const int r = gcov_layer(g, ld, n, rows, sub, part + off, cap - off, out, s, out_v, vi, gmax, &fin, &used);
     off += (used + 3) / 4 * 4;
     return r;
   };

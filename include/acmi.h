@@ -293,6 +293,12 @@ int acmi_a2c_loss(const float* logits, int ld, const float* values,
  *            rows = B*locations; fc: x = the input row; A_4 = fc4 output).
  * dhead: [B][ldh] from acmi_a2c_loss.  d1..d4 are [B]x(layer output) scratch.
  * ws: >= acmi_backward_ws_floats(B, A, C3) floats.
+ * net->conv_prep (when non-null) must have been prepared (acmi_conv_prepare)
+ * from the same parameters as net->params: its header supplies the a1 / a2 /
+ * a3 bounds that scale the f16x2 operands of the conv2 / conv3 / fc4
+ * reductions, and the pre-split weights of the input-gradient chain.  Callers
+ * re-prepare after every parameter update (NetEngine does, keyed by its
+ * parameter version); a stale prep gives wrong scales, not an error.
  * ---------------------------------------------------------------------- */
 typedef struct acmi_bwd {
   float* d1; /* [B][20][20][32] */

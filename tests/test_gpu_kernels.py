@@ -346,6 +346,55 @@ def test_band_backward_deterministic_and_symmetric(lib, cuda):
         assert torch.equal(F, F.t()), f
 
 
+def test_kfac_inverse_badly_conditioned(lib, cuda):
+    """The pair sweep (two pivots per sweep, each 2 x 2 pivot block inverted in
+    closed form, kfac.hip pivot_inverse) on damped factors of condition ~1e7:
+    eigenvalues logspace(-9, 1) in a random basis, damping 1e-12 (sqrt 1e-6).
+    Every 2 x 2 Schur-complement block of such an SPD matrix is SPD, and the fp64
+    sweep keeps f32-output accuracy (max-abs error 1e-4 of max-abs value against
+    numpy's float64 inverse of the same f32 factors)."""
+    A, C3 = 4, 32
+    din = (ctypes.c_int64 * 6)()
+    dout = (ctypes.c_int64 * 6)()
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, din, dout, so, ctypes.byref(tot))
+    rng = np.random.default_rng(17)
+    fac = np.zeros(tot.value, np.float32)
+    mats = []
+    for f in range(11):
+        n = din[f] if f < 5 else dout[f - 5]
+        q, _ = np.linalg.qr(rng.standard_normal((n, n)))
+        m = (q * np.logspace(-9, 1, n)) @ q.T
+        m = ((m + m.T) / 2).astype(np.float32)
+        fac[so[f]:so[f] + n * n] = m.ravel()
+        mats.append(m.astype(np.float64))
+    fac_d = torch.from_numpy(fac).to(cuda)
+    inv = torch.zeros(lib.acmi_kfac_inverse_floats(A, C3), device=cuda)
+    ws = torch.zeros(lib.acmi_kfac_inverse_ws_doubles(A, C3), dtype=torch.float64, device=cuda)
+    damping = 1e-12
+    _lib.call('acmi_kfac_inverse', A, C3, _lib.ptr(fac_d), ctypes.c_float(damping), 0, _lib.ptr(inv), _lib.ptr(ws),
+              _lib.stream_handle())
+    torch.cuda.synchronize()
+    inv_h = inv.cpu().numpy().astype(np.float64)
+    assert np.isfinite(inv_h).all()
+    ioff = (ctypes.c_int64 * 12)()
+    ild = (ctypes.c_int64 * 12)()
+    _lib.call('acmi_kfac_inverse_layout', A, C3, ioff, ild)
+    for l in range(6):
+        Am, Gm = mats[min(l, 4)], mats[5 + l]
+        da, dg = Am.shape[0], Gm.shape[0]
+        lam = np.float64(np.float32(damping))
+        pi = np.sqrt((np.trace(Am) / da) / (np.trace(Gm) / dg))
+        for m, M, add in ((2 * l, Am, pi * np.sqrt(lam)), (2 * l + 1, Gm, np.sqrt(lam) / pi)):
+            n = M.shape[0]
+            ref = np.linalg.inv(M + add * np.eye(n))
+            got = inv_h[ioff[m]:ioff[m] + n * ild[m]].reshape(n, ild[m])[:, :n]
+            rel = np.abs(got - ref).max() / np.abs(ref).max()
+            print('layer', l, 'AG'[m % 2], 'cond %.1e' % np.linalg.cond(M + add * np.eye(n)), 'rel %.2e' % rel)
+            assert rel < 1e-4, (l, m % 2, rel)
+
+
 def test_kfac_inverse_matches_numpy(lib, cuda):
     A, C3 = 4, 32
     din = (ctypes.c_int64 * 6)()
