@@ -490,6 +490,59 @@ def test_acktr_update_matches_oracle(lib, cuda, forward_mode, N, T, A, games, fw
     assert gs.value == 41
 
 
+@pytest.mark.parametrize('fwd', ['f32', 'bf16'])
+def test_acktr_update_end_to_end_vs_float64_forward(lib, cuda, forward_mode, fwd):
+    """End to end at BASELINE configs[2] (32 envs x 20 steps, A = 4): the float64
+    oracle runs its OWN forward on the rollout's observations (oracle.forward) and
+    everything after it -- targets, losses, backward, A / G factors, damped
+    inverses, the K-FAC step -- so the forward's error is carried into the update
+    (test_acktr_update_matches_oracle feeds the oracle the GPU's forward instead
+    and checks the update's arithmetic alone).  The sampled-loss draws are the
+    GPU's (a draw at a CDF boundary may flip between f32 and float64 logits); their
+    probabilities are the oracle's.
+
+    f32: preconditioned gradient and step within 1e-3 rel-L2 per K-FAC block
+    (north_star).  bf16 forward (configs[4]'s "bf16 forward / fp32 K-FAC"): the
+    tower rounds conv2 / conv3 inputs to 16 bits (range-relative error ~1e-3,
+    test_bf16_forward_mode), which reaches the update -- the per-block errors are
+    printed as the tracked end-to-end number and bounded at 5e-2."""
+    from actorcritic import session as sess
+    forward_mode(fwd)
+    N, T, A, C3 = 32, 20, 4, 32
+    env, model, agent, obj, gs, opt, op, params = _build(N, T, A, C3)
+    gs.assign(40)
+    with sess.Session() as s:
+        data = agent.interact(s)
+        feed = _feed(model, data)
+        logits32 = model.engine.lookup_rollout(data[0]).flat_logits.cpu().numpy().copy()
+        p_before = model.params.cpu().numpy().astype(np.float64)
+        s.run(op, feed_dict=feed)
+        torch.cuda.synchronize()
+    obs, act, rew, term, nxt, _ = data
+    M = N * T
+    full = oracle.forward(p_before, obs.cpu().numpy().reshape(M, 84, 84, 4), A, C3)
+    vb = oracle.forward(p_before, nxt.cpu().numpy(), A, C3)['value']
+    tg = oracle.targets_f64(rew.cpu().numpy(), term.cpu().numpy(), vb, 0.99).reshape(-1)
+    lg = oracle.a2c_loss_and_head_grads(full['logits'], full['value'], act.cpu().numpy().reshape(-1), tg)
+    grads, _, afac = oracle.backward(p_before, full, lg['dlogits'], lg['dvalue'], A, C3, with_a_factors=True)
+    _, g_v, y = oracle.sampled_head_grads(logits32, 0x4b464143, 0, 40)
+    g_pi = np.exp(oracle.log_softmax(full['logits'])) - np.eye(A)[y]
+    gfac = oracle.g_factors(p_before, full, g_pi, g_v, A, C3)
+    inv = oracle.damped_inverses(afac, gfac, 0.01)
+    new_p, _, precon, coeff = oracle.kfac_step(p_before, np.zeros_like(p_before), grads, inv,
+                                               oracle.linear_decay(0.25, 0.025, 40, 1000), 0.9, 1e-4, A, C3)
+    got_pre = opt.state['precon'].cpu().numpy().astype(np.float64)
+    got_p = model.params.cpu().numpy().astype(np.float64)
+    tol = 1e-3 if fwd == 'f32' else 5e-2
+    for name, lo, hi in _blocks(A, C3):
+        e_pre = np.linalg.norm(got_pre[lo:hi] - precon[lo:hi]) / np.linalg.norm(precon[lo:hi])
+        e_step = np.linalg.norm(got_p[lo:hi] - new_p[lo:hi]) / np.linalg.norm(new_p[lo:hi] - p_before[lo:hi])
+        print('%s forward, end to end: block %-11s precon rel-L2 %.2e  step rel-L2 %.2e' % (fwd, name, e_pre, e_step))
+        assert e_pre < tol, (name, 'precon', e_pre)
+        assert e_step < tol, (name, 'step', e_step)
+    assert float(opt.state['coeff'][0]) == pytest.approx(coeff, rel=tol)
+
+
 def test_cold_start_schedule(lib, cuda):
     from actorcritic import session as sess
     env, model, agent, obj, gs, opt, op, params = _build(2, 3)
