@@ -245,7 +245,11 @@ class NetEngine(object):
                   ctypes.byref(bwd), seed, self.rank * fwd.M, counter, _lib.ptr(st.gstat), _lib.ptr(ws),
                   self.stream())
 
-    concurrent_stats = os.environ.get('ACMI_CONCURRENT_STATS', '0') != '0'
+    # the G chain on a side stream: '1' always, '0' never, unset: at small batches
+    # (M <= CONCURRENT_STATS_ROWS), where each of its launches fills a fraction of
+    # the chip; at the bench shard one stream measured faster
+    concurrent_stats = {'1': True, '0': False}.get(os.environ.get('ACMI_CONCURRENT_STATS', ''))
+    CONCURRENT_STATS_ROWS = 2048
     # measured (ACKTR 512x20, one box): plain update 5.25 ms with the G chain started
     # next to the whole backward, 5.16 ms started after the backward's dX chain
     stats_after_dx = os.environ.get('ACMI_STATS_AFTER_DX', '1') != '0'
@@ -255,7 +259,8 @@ class NetEngine(object):
         starts the data-parallel all-reduce of the backward's prefix of ``red`` as soon
         as it is enqueued and returns its handle (allreduce_end completes it).  With
         ``concurrent_stats`` the G chain runs on a side stream next to the backward."""
-        if not (with_stats and self.concurrent_stats):
+        conc = self.concurrent_stats if self.concurrent_stats is not None else fwd.M <= self.CONCURRENT_STATS_ROWS
+        if not (with_stats and conc):
             self.backward(fwd, st, with_stats)
             pending = self.allreduce_begin(st, with_stats)
             if with_stats:

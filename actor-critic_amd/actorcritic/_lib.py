@@ -64,6 +64,8 @@ _SIGS = {
     'acmi_get_gemm_mode': (c_int, []),
     'acmi_set_conv_stats_mode': (c_int, [c_int]),
     'acmi_get_conv_stats_mode': (c_int, []),
+    'acmi_set_backward_streams': (c_int, [c_int]),
+    'acmi_get_backward_streams': (c_int, []),
     'acmi_band_info': (c_int, [c_int, c_int, c_i64, ctypes.POINTER(c_i64)]),
     'acmi_param_count': (c_i64, [c_int, c_int]),
     'acmi_conv_prep_bytes': (c_i64, [c_int]),
