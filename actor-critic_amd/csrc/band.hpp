@@ -43,7 +43,7 @@
 #include <tuple>
 
 #include "bandplan.hpp"
-#include "f16x2.hpp"  // f16x2_scale, ds_tr16, cat8h
+#include "f16x2.hpp"  // split2, f16x2_scale, ds_tr16, stage_f4, zero_run
 
 namespace acmi {
 
@@ -201,6 +201,17 @@ __global__ __launch_bounds__(256) void band_bounds_kernel(const float* w1, const
 // ---------------------------------------------------------------------------
 // the band kernel
 // ---------------------------------------------------------------------------
+#ifndef ACMI_BAND_DEPTH
+#define ACMI_BAND_DEPTH 2
+#endif
+constexpr int kBandDepth = ACMI_BAND_DEPTH;  // stages of loads in flight (register sets)
+#ifndef ACMI_BAND_PIPE  // 1: fragment reads one sub-tile ahead of the MFMAs (see the loop); 0: plain order
+#define ACMI_BAND_PIPE 1
+#endif
+#ifndef ACMI_BAND_PROBE  // timing probes (wrong results): 1 no split, 2 no column sums, 4 no loads,
+                         // 8 no LDS stores, 16 no MFMAs, 32 no LDS fragment reads
+#define ACMI_BAND_PROBE 0
+#endif
 constexpr int kBandRows = 16;                         // k-rows (images) per stage
 constexpr int kBandRowBytes = kBandSlabs * 64 * 2;    // 1024: one f16 row of the staged columns
 constexpr int kBandPart = kBandRows * kBandRowBytes;  // 16 KB
@@ -221,267 +232,358 @@ struct BandArgs {
   int ntiles, ncols;
 };
 
-// (a, b) s = h + l on v_fma_mix: h = f16_rn(a s) written straight from the f32
-// product (mixlo / mixhi into the two halves), l = f16_rn(a s - h) with h read as
-// f16 from its half -- four VALU per two values where pk_f16 of products takes
-// six (two muls, two cvt_pk, two fma); bit-identical to split2 (a s is exact, and
-// a s - h is exact in f32, so the single rounding to f16 is split2's)
-__device__ __forceinline__ void split2_mix(float a, float b, float s, uint32_t& h, uint32_t& l) {
-  uint32_t hh, ll;
-  asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "=v"(hh) : "v"(a), "v"(s));
-  asm("v_fma_mixhi_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "+v"(hh) : "v"(b), "v"(s));
-  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(ll) : "v"(a), "v"(s), "v"(hh));
-  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(ll) : "v"(b), "v"(s), "v"(hh));
-  h = hh;
-  l = ll;
-}
-
-// Staging: wave w stages slab w of its group (w < nslab): per 16-row stage, rows
-// 4r + (lane >> 4) (r = 0..3) and columns 4 (lane & 15) .. + 3 of the slab, one
-// buffer_load_dwordx4 each, through a wave-uniform buffer descriptor over the
-// chunk's rows of X or dY (rows past the chunk end and columns past the tensor's
-// width read as zeros: the descriptor's range, no per-element select); the stage
-// advance is the scalar offset.  The split, the LDS stores and -- for the one group
-// that owns the slab (csown) -- the column sums are per-wave uniform work.
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void band_kernel(BandArgs p) {
   __shared__ __attribute__((aligned(16))) char lds[2 * kBandBuf];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave = tid >> 6;
+  // staging: thread -> rows 2*rp, 2*rp + 1 of the stage; columns 4*lane .. +3
+  // (staged slab lane / 16) and 256 + 4*lane .. +3 (slab 4 + lane / 16)
+  const int rp = wave;
   const int q = (lane >> 2) & 3, pl = lane & 3, g = (lane >> 4) & 1, kh = lane >> 5;
-  const int rq = lane >> 4, c4 = lane & 15;
   const float sx = f16x2_scale_of_bits(p.xmax), sy = f16x2_scale_of_bits(p.ymax);
-  // item: XCD x = b & 7 (the blocks b, b + 8, ... share an XCD under the
-  // round-robin dispatch), its j-th (group, chunk) in the region's list
-  const int x = blockIdx.x & 7;
-  const int it = blockIdx.x >> 3;
-  if (it >= (p.xoff[x + 1] - p.xoff[x]) * p.nc) return;
-  const int ngx = p.xoff[x + 1] - p.xoff[x];
-  const int chunk = it / ngx;
-  const BandGroup& G = p.groups[p.xlist[p.xoff[x] + (it - chunk * ngx)]];
-  const int kbeg = chunk * p.k_chunk;
-  const int kend = min(p.M, kbeg + p.k_chunk);
-  const int nk = (kend - kbeg + kBandRows - 1) / kBandRows;
-  const int nslab = G.nslab;
+  {
+    // item: XCD x = b & 7 (the blocks b, b + 8, ... share an XCD under the
+    // round-robin dispatch), its j-th (group, chunk) in the region's list
+    const int x = blockIdx.x & 7;
+    const int it = blockIdx.x >> 3;
+    if (it >= (p.xoff[x + 1] - p.xoff[x]) * p.nc) return;
+    const int ngx = p.xoff[x + 1] - p.xoff[x];
+    const int chunk = it / ngx;
+    const BandGroup& G = p.groups[p.xlist[p.xoff[x] + (it - chunk * ngx)]];
+    const int kbeg = chunk * p.k_chunk;
+    const int kend = min(p.M, kbeg + p.k_chunk);
+    const int nk = (kend - kbeg + kBandRows - 1) / kBandRows;
+    const int nslab = G.nslab;
 
-  // this wave's staged slab (wave-uniform)
-  const bool stager = wave < nslab;
-  const int sbase = stager ? G.base[wave] : 0;
-  const bool isx = sbase < p.kp;
-  const uint32_t ld = isx ? (uint32_t)p.kp : (uint32_t)p.ldy;
-  const int col0 = isx ? sbase : sbase - p.kp;
-  const float sc = isx ? sx : sy;
-  const bool own = stager && ((G.csown >> wave) & 1);
-  const float* rbase = (isx ? p.X : p.dy) + (long long)kbeg * ld;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(rbase), (short)0, stager ? (int)((uint32_t)(kend - kbeg) * ld * 4u) : 0, 0x00020000);
-  const bool cok = col0 + 4 * c4 < (int)ld;
-  uint32_t voff[4];
+    // this thread's two staged column runs: base pointer, row stride, scale
+    const float* cptr[2];
+    uint32_t cld[2];
+    bool cok[2];
+    float cscale[2];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) voff[r] = cok ? ((uint32_t)(4 * r + rq) * ld + (uint32_t)(col0 + 4 * c4)) * 4u : 0x80000000u;
-  const uint32_t sstep = (uint32_t)kBandRows * ld * 4u;
-  uint32_t soff = 0;  // byte offset of the next stage to fetch (scalar)
+    for (int u = 0; u < 2; ++u) {
+      const int si = 4 * u + (lane >> 4);
+      const int col = (si < nslab ? G.base[si] : p.J) + 4 * (lane & 15);
+      cok[u] = si < nslab && col < p.J;
+      const bool isx = col < p.kp;
+      cptr[u] = isx ? p.X + col : p.dy + (col - p.kp);
+      cld[u] = isx ? (uint32_t)p.kp : (uint32_t)p.ldy;
+      cscale[u] = ((G.xmask >> (si & 7)) & 1) ? sx : sy;
+    }
+    float4 ra[kBandDepth][4];
+    float csum[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+    // element offsets of this thread's first row in the next stage to fetch
+    // (stages are fetched in order: advanced by 16 rows per fetch)
+    uint32_t foff[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) foff[u] = (uint32_t)(kbeg + 2 * rp) * cld[u];
 
-  float4 ra[4];
-  float csum[4] = {0.f, 0.f, 0.f, 0.f};
-  auto fetch = [&]() {
+    auto fetch = [&](int k0, auto S) {
+      constexpr int set = decltype(S)::value;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      ra[r] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff[r], soff, 0));
-    soff += sstep;
-  };
-  // staged row 4r + rq of the fetched stage: split, LDS image (h | l parts, 8-byte
-  // slots of 4 columns XOR-swizzled by 8 (row & 3) = 8 rq), owner's column sums
-  auto commit1 = [&](int buf, int r) {
-    if (stager) {
-      const float4 v = ra[r];
-      uint2 h, l;
-      split2_mix(v.x, v.y, sc, h.x, l.x);
-      split2_mix(v.z, v.w, sc, h.y, l.y);
-      char* sp = lds + buf * kBandBuf + (4 * r + rq) * kBandRowBytes + 8 * ((16 * wave + c4) ^ (8 * rq));
-      *reinterpret_cast<uint2*>(sp) = h;
-      *reinterpret_cast<uint2*>(sp + kBandPart) = l;
-      if (own) {
-        csum[0] += v.x;
-        csum[1] += v.y;
-        csum[2] += v.z;
-        csum[3] += v.w;
+      for (int r = 0; r < 2; ++r) {
+        const bool rok = k0 + 2 * rp + r < kend;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if constexpr (ACMI_BAND_PROBE & 4)
+            ra[set][2 * r + u] = make_float4((float)(k0 + r), (float)u, (float)lane, 1.f);
+          else
+            ra[set][2 * r + u] = stage_f4(cptr[u] + foff[u] + r * cld[u], rok && cok[u]);
+        }
       }
-    }
-  };
-  auto commit = [&](int buf) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) commit1(buf, r);
-  };
-
-  auto slot_off = [&](int colblock) {
-    const int slot = (colblock >> 2) + 4 * g + pl;
-    return (8 * kh + q) * kBandRowBytes + 8 * (slot ^ (8 * q));
-  };
-  int aoff[2][2], boff[2][2];
-  float inv[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int sa = G.ra[wave][t] < 0 ? 0 : G.ra[wave][t];
-    const int sb = G.cb[wave][t] < 0 ? 0 : G.cb[wave][t];
-    aoff[t][0] = slot_off(64 * sa);
-    aoff[t][1] = slot_off(64 * sa + 32);
-    boff[t][0] = slot_off(64 * sb);
-    boff[t][1] = slot_off(64 * sb + 32);
-    const float s_a = ((G.xmask >> sa) & 1) ? sx : sy, s_b = ((G.xmask >> sb) & 1) ? sx : sy;
-    inv[t] = 1.f / (s_a * s_b);  // powers of two: exact
-  }
-  const int ntile = (G.ra[wave][0] >= 0) + (G.ra[wave][1] >= 0);
-
-  f32x16 acc[2][2][2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[t][a][b][r] = 0.f;
-
-  // Software-pipelined fragment reads.  Each wave's sub-tiles of stage kt are
-  // read from LDS one sub-tile AHEAD of their MFMAs, and the last sub-tile of a
-  // stage is multiplied after the barrier, while the next stage's first
-  // fragments are in flight:
-  //   barrier(kt-1) | read (kt,0) | mma (kt-1,last) + commit of stage kt+1
-  //   (split and LDS stores interleaved with those MFMAs) | fetch kt+2 |
-  //   read (kt,1) | mma (kt,0) | barrier(kt) | read (kt+1,0) | ...
-  // so no MFMA block waits for a burst of LDS reads issued right before it.
-  // Fragment sets: F[t] for tile t when a wave has two sub-tiles; by stage parity
-  // when it has one.  Stages past the chunk end stage zeros (the descriptor's
-  // range), so the commit is unconditional and the trailing read is harmless.
-  struct Frag {
-    f16x8 a[2][2], b[2][2];  // [32-column block][part h, l]
-  };
-  Frag F[2];
-#pragma unroll
-  for (int f = 0; f < 2; ++f)
-#pragma unroll
-    for (int xx = 0; xx < 2; ++xx)
-#pragma unroll
-      for (int y = 0; y < 2; ++y) F[f].a[xx][y] = F[f].b[xx][y] = f16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  auto fread = [&](const char* s, int t, Frag& f) {
-#pragma unroll
-    for (int pt = 0; pt < 2; ++pt) {
-      const char* sp = s + pt * kBandPart;
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        f.a[cb][pt] = cat8h(ds_tr16(sp + aoff[t][cb]), ds_tr16(sp + aoff[t][cb] + 4 * kBandRowBytes));
-        f.b[cb][pt] = cat8h(ds_tr16(sp + boff[t][cb]), ds_tr16(sp + boff[t][cb] + 4 * kBandRowBytes));
+      for (int u = 0; u < 2; ++u) foff[u] += (uint32_t)kBandRows * cld[u];
+    };
+    // one staged float4 (row 2 rp + r, run u) of register set `set` into LDS buffer buf
+    auto commit1 = [&](int buf, auto S, int r, int u) {
+      constexpr int set = decltype(S)::value;
+      {
+        const int krow = 2 * rp + r;
+        char* s = lds + buf * kBandBuf + krow * kBandRowBytes;
+        const int q8 = 8 * (krow & 3);
+        {
+          const float4 v = ra[set][2 * r + u];
+          if constexpr (!(ACMI_BAND_PROBE & 2)) {
+            csum[4 * u] += v.x;
+            csum[4 * u + 1] += v.y;
+            csum[4 * u + 2] += v.z;
+            csum[4 * u + 3] += v.w;
+          }
+          uint2 h, l;
+          if constexpr (ACMI_BAND_PROBE & 1) {
+            h.x = __float_as_uint(v.x) ^ __float_as_uint(v.y);
+            h.y = __float_as_uint(v.z) ^ __float_as_uint(v.w);
+            l = h;
+          } else {
+            split2(v.x, v.y, cscale[u], h.x, l.x);
+            split2(v.z, v.w, cscale[u], h.y, l.y);
+          }
+          const int off = 8 * ((64 * u + lane) ^ q8);  // 8-byte slot (4 columns) of column 4*(64u + lane)
+          if constexpr (ACMI_BAND_PROBE & 8) {
+            csum[4 * u] += __uint_as_float(h.x ^ l.y);
+          } else {
+            *reinterpret_cast<uint2*>(s + off) = h;
+            *reinterpret_cast<uint2*>(s + kBandPart + off) = l;
+          }
+        }
       }
-    }
-  };
-  // one 32x32 block (tm, tn) of sub-tile t: the three f16x2 MFMAs
-  auto fmma1 = [&](auto T, const Frag& f, int tm, int tn) {
-    constexpr int t = decltype(T)::value;
-    f32x16 c = acc[t][tm][tn];
-    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[tm][1], f.b[tn][0], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[tm][0], f.b[tn][1], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[tm][0], f.b[tn][0], c, 0, 0, 0);
-    acc[t][tm][tn] = c;
-  };
-  auto fmma = [&](auto T, const Frag& f) {
+    };
+    auto commit = [&](int buf, auto S) {
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
+      for (int r = 0; r < 2; ++r)
 #pragma unroll
-      for (int tn = 0; tn < 2; ++tn) fmma1(T, f, tm, tn);
-  };
-  // sub-tile t's MFMAs with the commit of LDS buffer buf interleaved: block
-  // (tm, tn) = p's three MFMAs, then staged row p's split + stores (they issue
-  // while the third MFMA runs)
-  auto fmma_commit = [&](auto T, const Frag& f, int buf) {
+        for (int u = 0; u < 2; ++u) commit1(buf, S, r, u);
+    };
+
+    auto slot_off = [&](int colblock) {
+      const int slot = (colblock >> 2) + 4 * g + pl;
+      return (8 * kh + q) * kBandRowBytes + 8 * (slot ^ (8 * q));
+    };
+    int aoff[2][2], boff[2][2];
+    float inv[2];
 #pragma unroll
-    for (int p4 = 0; p4 < 4; ++p4) {
-      fmma1(T, f, p4 >> 1, p4 & 1);
-      commit1(buf, p4);
-      __builtin_amdgcn_sched_barrier(0);
+    for (int t = 0; t < 2; ++t) {
+      const int sa = G.ra[wave][t] < 0 ? 0 : G.ra[wave][t];
+      const int sb = G.cb[wave][t] < 0 ? 0 : G.cb[wave][t];
+      aoff[t][0] = slot_off(64 * sa);
+      aoff[t][1] = slot_off(64 * sa + 32);
+      boff[t][0] = slot_off(64 * sb);
+      boff[t][1] = slot_off(64 * sb + 32);
+      const float s_a = ((G.xmask >> sa) & 1) ? sx : sy, s_b = ((G.xmask >> sb) & 1) ? sx : sy;
+      inv[t] = 1.f / (s_a * s_b);  // powers of two: exact
     }
-  };
-  using T0 = std::integral_constant<int, 0>;
-  using T1 = std::integral_constant<int, 1>;
-  // one register set of staged loads: stage kt+1 is committed at the start of
-  // step kt and stage kt+2 fetched into the same registers right after
-  if (nk > 0) {
-    fetch();
-    commit(0);
-    fetch();
-  }
-  __syncthreads();
-  if (ntile > 0) fread(lds, 0, F[0]);
-  auto pstep = [&](auto I, auto NT) {
-    constexpr int nt = decltype(NT)::value;
-    constexpr int i = decltype(I)::value;
-    const int cur = i & 1;
-    const char* s = lds + cur * kBandBuf;
-    // the previous stage's last sub-tile (zero fragments before the first
-    // stage) with the commit of stage kt+1 interleaved
-    if constexpr (nt == 2) fmma_commit(T1{}, F[1], cur ^ 1);
-    if constexpr (nt == 1) fmma_commit(T0{}, F[(i + 1) & 1], cur ^ 1);
-    if constexpr (nt == 0) commit(cur ^ 1);
-    fetch();
-    if constexpr (nt == 2) {
-      fread(s, 1, F[1]);
-      fmma(T0{}, F[0]);
+    const int ntile = (G.ra[wave][0] >= 0) + (G.ra[wave][1] >= 0);
+
+    f32x16 acc[2][2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[t][a][b][r] = 0.f;
+
+    using S0 = std::integral_constant<int, 0>;
+#if ACMI_BAND_PIPE
+    // Software-pipelined fragment reads.  Each wave's sub-tiles of stage kt are
+    // read from LDS one sub-tile AHEAD of their MFMAs, and the last sub-tile of a
+    // stage is multiplied after the barrier, while the next stage's first
+    // fragments are in flight:
+    //   barrier(kt-1) | read (kt,0) | mma (kt-1,last) + commit of stage kt+1
+    //   (VALU split and LDS stores interleaved with those MFMAs) | fetch kt+2 |
+    //   read (kt,1) | mma (kt,0) | barrier(kt) | read (kt+1,0) | ...
+    // so no MFMA block waits for a burst of LDS reads issued right before it (in
+    // the plain order every wave of the CU reads at the same time after each
+    // barrier and the matrix pipes idle until the fragments return).  Fragment
+    // sets: F[t] for tile t when a wave has two sub-tiles; by stage parity when
+    // it has one.  Stages past the chunk end stage zeros (masked loads), so the
+    // commit is unconditional and the trailing read is harmless.
+    struct Frag {
+      f16x8 a[2][2], b[2][2];  // [32-column block][part h, l]
+    };
+    Frag F[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) F[f].a[x][y] = F[f].b[x][y] = f16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    auto fread = [&](const char* s, int t, Frag& f) {
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) {
+        const char* sp = s + pt * kBandPart;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          f.a[cb][pt] = cat8h(ds_tr16(sp + aoff[t][cb]), ds_tr16(sp + aoff[t][cb] + 4 * kBandRowBytes));
+          f.b[cb][pt] = cat8h(ds_tr16(sp + boff[t][cb]), ds_tr16(sp + boff[t][cb] + 4 * kBandRowBytes));
+        }
+      }
+    };
+    // one 32x32 block (tm, tn) of sub-tile t: the three f16x2 MFMAs
+    auto fmma1 = [&](auto T, const Frag& f, int tm, int tn) {
+      constexpr int t = decltype(T)::value;
+      f32x16 c = acc[t][tm][tn];
+      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[tm][1], f.b[tn][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[tm][0], f.b[tn][1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.a[tm][0], f.b[tn][0], c, 0, 0, 0);
+      acc[t][tm][tn] = c;
+    };
+    auto fmma = [&](auto T, const Frag& f) {
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) fmma1(T, f, tm, tn);
+    };
+    // sub-tile t's MFMAs with the commit of LDS buffer buf interleaved: block
+    // (tm, tn) = p's three MFMAs, then staged float4 p's split + stores (they
+    // issue while the third MFMA runs)
+    auto fmma_commit = [&](auto T, const Frag& f, int buf) {
+#pragma unroll
+      for (int p4 = 0; p4 < 4; ++p4) {
+        fmma1(T, f, p4 >> 1, p4 & 1);
+        commit1(buf, S0{}, p4 >> 1, p4 & 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    using T0 = std::integral_constant<int, 0>;
+    using T1 = std::integral_constant<int, 1>;
+    // one register set of staged loads: stage kt+1 is committed at the start of
+    // step kt and stage kt+2 fetched into the same registers right after (one
+    // stage of latency, as with two sets committed mid-step)
+    if (nk > 0) {
+      fetch(kbeg, S0{});
+      commit(0, S0{});
+      fetch(kbeg + kBandRows, S0{});
     }
-    // (the MFMAs stay before the barrier: sunk past it, they would leave the
-    // tile-1 reads just issued exposed at the barrier's wait)
-    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
-    const char* sn = lds + (cur ^ 1) * kBandBuf;
-    if constexpr (nt == 2) fread(sn, 0, F[0]);
-    if constexpr (nt == 1) fread(sn, 0, F[(i + 1) & 1]);
-  };
-  auto prun = [&](auto NT) {
-    for (int kt = 0; kt < nk; kt += 2) {
-      pstep(std::integral_constant<int, 0>{}, NT);
-      if (kt + 1 < nk) pstep(std::integral_constant<int, 1>{}, NT);
-    }
-    // the last stage's deferred sub-tile
-    constexpr int nt = decltype(NT)::value;
-    if constexpr (nt == 2) fmma(T1{}, F[1]);
-    if constexpr (nt == 1) {
-      if (nk > 0) {
-        if ((nk - 1) & 1) fmma(T0{}, F[1]);
-        else fmma(T0{}, F[0]);
+    if (ntile > 0) fread(lds, 0, F[0]);
+    auto pstep = [&](int kt, auto I, auto NT) {
+      constexpr int nt = decltype(NT)::value;
+      constexpr int i = decltype(I)::value;
+      const int cur = i & 1;
+      const char* s = lds + cur * kBandBuf;
+      // the previous stage's last sub-tile (zero fragments before the first
+      // stage) with the commit of stage kt+1 interleaved
+      if constexpr (nt == 2) fmma_commit(T1{}, F[1], cur ^ 1);
+      if constexpr (nt == 1) fmma_commit(T0{}, F[(i + 1) & 1], cur ^ 1);
+      if constexpr (nt == 0) commit(cur ^ 1, S0{});
+      fetch(kbeg + (kt + 2) * kBandRows, S0{});
+      if constexpr (nt == 2) {
+        fread(s, 1, F[1]);
+        fmma(T0{}, F[0]);
       }
+      // (the MFMAs stay before the barrier: sunk past it, they would leave the
+      // tile-1 reads just issued exposed at the barrier's wait)
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+      const char* sn = lds + (cur ^ 1) * kBandBuf;
+      if constexpr (nt == 2) fread(sn, 0, F[0]);
+      if constexpr (nt == 1) fread(sn, 0, F[(i + 1) & 1]);
+    };
+    auto prun = [&](auto NT) {
+      for (int kt = 0; kt < nk; kt += 2) {
+        pstep(kt, std::integral_constant<int, 0>{}, NT);
+        if (kt + 1 < nk) pstep(kt + 1, std::integral_constant<int, 1>{}, NT);
+      }
+      // the last stage's deferred sub-tile
+      constexpr int nt = decltype(NT)::value;
+      if constexpr (nt == 2) fmma(T1{}, F[1]);
+      if constexpr (nt == 1) {
+        if (nk > 0) {
+          if ((nk - 1) & 1) fmma(T0{}, F[1]);
+          else fmma(T0{}, F[0]);
+        }
+      }
+    };
+    if (ntile == 0) prun(std::integral_constant<int, 0>{});
+    else if (ntile == 1) prun(std::integral_constant<int, 1>{});
+    else prun(std::integral_constant<int, 2>{});
+#else
+    if (nk > 0) {
+      fetch(kbeg, S0{});
+      fetch(kbeg + kBandRows, std::integral_constant<int, 1>{});
+      if constexpr (kBandDepth > 2) fetch(kbeg + 2 * kBandRows, std::integral_constant<int, 2 % kBandDepth>{});
+      commit(0, S0{});
     }
-  };
-  if (ntile == 0) prun(std::integral_constant<int, 0>{});
-  else if (ntile == 1) prun(std::integral_constant<int, 1>{});
-  else prun(std::integral_constant<int, 2>{});
+    __syncthreads();
 
-  // tiles, unscaled, into their compact slots of this chunk
-  const int khalf = lane >> 5;
+    auto tile = [&](const char* s, int t) {
+      f16x8 a[2][2], b[2][2];  // [32-column block][part h, l]
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    if (t >= ntile) break;
-    float* dst = p.part + ((long long)chunk * p.ntiles + G.tile[wave][t]) * 4096;
+      for (int pt = 0; pt < 2; ++pt) {
+        const char* sp = s + pt * kBandPart;
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
+        for (int cb = 0; cb < 2; ++cb) {
+          if constexpr (ACMI_BAND_PROBE & 32) {
+            a[cb][pt] = b[cb][pt] = f16x8{(_Float16)(float)(aoff[t][cb] + pt), (_Float16)(float)cb, 0, 0, 0, 0, 0, 0};
+          } else {
+            a[cb][pt] = cat8h(ds_tr16(sp + aoff[t][cb]), ds_tr16(sp + aoff[t][cb] + 4 * kBandRowBytes));
+            b[cb][pt] = cat8h(ds_tr16(sp + boff[t][cb]), ds_tr16(sp + boff[t][cb] + 4 * kBandRowBytes));
+          }
+        }
+      }
 #pragma unroll
-      for (int tn = 0; tn < 2; ++tn)
+      for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          dst[(32 * tm + (r & 3) + 8 * (r >> 2) + 4 * khalf) * 64 + 32 * tn + (lane & 31)] =
-              acc[t][tm][tn][r] * inv[t];
-  }
-  // column sums of the owned slab: the four row classes (lane >> 4) added in a
-  // fixed order across lanes c4, c4 + 16, c4 + 32, c4 + 48
-  if (own) {
+        for (int tn = 0; tn < 2; ++tn) {
+          f32x16 c = acc[t][tm][tn];
+          if constexpr (ACMI_BAND_PROBE & 16) {
+            c[0] += (float)a[tm][1][0] + (float)b[tn][0][1] + (float)a[tm][0][2] + (float)b[tn][1][3];
+          } else {
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][1], b[tn][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][0], b[tn][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][0], b[tn][0], c, 0, 0, 0);
+          }
+          acc[t][tm][tn] = c;
+        }
+    };
+    // step kt: loads of kt + kBandDepth into the register set that held kt,
+    // tile 0 from stage kt, the commit of kt + 1 (its set) into the other LDS
+    // stage, tile 1, barrier.  I = kt mod the unroll (compile-time sets, stages).
+    constexpr int U = kBandDepth == 3 ? 6 : 2;
+    auto step = [&](int kt, auto I, auto NT) {
+      constexpr int nt = decltype(NT)::value;
+      constexpr int i = decltype(I)::value;
+      const int cur = i & 1;
+      const char* s = lds + cur * kBandBuf;
+      fetch(kbeg + (kt + kBandDepth) * kBandRows, std::integral_constant<int, i % kBandDepth>{});
+      if constexpr (nt >= 1) tile(s, 0);
+      if (kt + 1 < nk) commit(cur ^ 1, std::integral_constant<int, (i + 1) % kBandDepth>{});
+      if constexpr (nt >= 2) tile(s, 1);
+      __syncthreads();
+    };
+    auto run = [&](auto NT) {
+      for (int kt = 0; kt < nk; kt += U) {
+        step(kt, std::integral_constant<int, 0>{}, NT);
+        if (kt + 1 < nk) step(kt + 1, std::integral_constant<int, 1>{}, NT);
+        if constexpr (U > 2) {
+          if (kt + 2 < nk) step(kt + 2, std::integral_constant<int, 2>{}, NT);
+          if (kt + 3 < nk) step(kt + 3, std::integral_constant<int, 3>{}, NT);
+          if (kt + 4 < nk) step(kt + 4, std::integral_constant<int, 4>{}, NT);
+          if (kt + 5 < nk) step(kt + 5, std::integral_constant<int, 5>{}, NT);
+        }
+      }
+    };
+    if (ntile == 0) run(std::integral_constant<int, 0>{});
+    else if (ntile == 1) run(std::integral_constant<int, 1>{});
+    else run(std::integral_constant<int, 2>{});
+
+#endif
+
+    // tiles, unscaled, into their compact slots of this chunk
+    const int khalf = lane >> 5;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      csum[e] += __shfl_xor(csum[e], 16);
-      csum[e] += __shfl_xor(csum[e], 32);
+    for (int t = 0; t < 2; ++t) {
+      if (t >= ntile) break;
+      float* dst = p.part + ((long long)chunk * p.ntiles + G.tile[wave][t]) * 4096;
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            dst[(32 * tm + (r & 3) + 8 * (r >> 2) + 4 * khalf) * 64 + 32 * tn + (lane & 31)] =
+                acc[t][tm][tn][r] * inv[t];
     }
-    if (rq == 0) {
+    // column sums: [8 row-pair threads][512 staged columns] through the free LDS
+    float* cl = reinterpret_cast<float*>(lds);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int j = sbase + 4 * c4 + e;
-        if (j < p.J) p.cs[(long long)chunk * p.ncols + j] = csum[e];
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cl[rp * 512 + 256 * u + 4 * lane + e] = csum[4 * u + e];
+    __syncthreads();
+    {
+      const int col = tid, si = col >> 6;
+      if (si < nslab && ((G.csown >> si) & 1)) {
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v += cl[r * 512 + col];
+        const int j = G.base[si] + (col & 63);
+        if (j < p.J) p.cs[(long long)chunk * p.ncols + j] = v;
       }
     }
   }
@@ -611,10 +713,9 @@ inline int band_layer(const float* X, int H, int W, int C, int KH, int KW, int S
   const long long tile_f = (long long)p.ntiles * 4096, ncols = (long long)g.ns * 64;
   ACMI_REQUIRE((long long)nc * (tile_f + ncols) <= ws_cap, ACMI_ERR_WS,
                "band workspace too small (%lld > %lld)", (long long)nc * (tile_f + ncols), ws_cap);
-  // 32-bit byte offsets inside the kernel: a chunk's rows (plus the two stages
-  // fetched past its end) of the wider operand within one buffer descriptor
-  ACMI_REQUIRE((long long)(ch + 2 * kBandRows) * std::max(g.kp, g.L * CO) * 4 < (1LL << 31), ACMI_ERR_ARG,
-               "band_layer: %d-image chunks exceed 32-bit offsets", ch);
+  // 32-bit element offsets inside the kernel
+  ACMI_REQUIRE((long long)M * g.kp < (1LL << 31) && (long long)M * g.L * CO < (1LL << 31), ACMI_ERR_ARG,
+               "band_layer: %d images exceed 32-bit offsets", M);
   float* part = ws;
   float* cs = ws + (long long)nc * tile_f;
   BandArgs a;

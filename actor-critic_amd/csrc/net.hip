@@ -1180,29 +1180,6 @@ static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
   return ACMI_OK;
 }
 
-// Small batches run the loss backward's weight-gradient / A-factor reductions
-// side by side on library-owned streams (BwdAux): at M = 640 (BASELINE
-// configs[2]) each fills a fraction of the 256 CUs -- band conv2 190 blocks, band
-// conv3 88, the conv1 A factor, the heads + fc4 six-slab groups -- and one stream
-// ran them back to back (~0.27 ms).  Each reduction then needs its own partial
-// region: [heads + fc4 | band conv3 | band conv2].  (At the bench shard each of
-// them fills the chip on its own; a side stream there measured slower, round 1.)
-constexpr int kConcBwdRows = 2048;
-static int g_backward_streams = 1;  // acmi_set_backward_streams
-struct ConcRegions {
-  long long h, b3, b2, total;  // region offsets (floats) and the sum
-};
-static ConcRegions conc_regions(int B, int A, int C3) {
-  ConcRegions r;
-  auto up = [](long long x) { return (x + 3) / 4 * 4; };
-  const long long hcap = up(wgrad_plan(512, A + 1, true, B).floats) + up(wgrad_plan(49 * C3, 512, true, B).floats);
-  r.h = 0;
-  r.b3 = hcap;
-  r.b2 = r.b3 + up(band_ws_floats(band_host_plan(9, 9, 64, 3, 3, 1, C3), B));
-  r.total = r.b2 + up(band_ws_floats(band_host_plan(20, 20, 32, 4, 4, 2, 64), B));
-  return r;
-}
-
 static long long bwd_partial_cap(int B, int A, int C3) {
   // the largest split-K partial over all layers (with stats)
   long long m = 0;
@@ -1227,35 +1204,8 @@ static long long bwd_partial_cap(int B, int A, int C3) {
   // band reductions of conv2 / conv3 (rows = images)
   m = std::max(m, band_ws_floats(band_host_plan(20, 20, 32, 4, 4, 2, 64), B));
   m = std::max(m, band_ws_floats(band_host_plan(9, 9, 64, 3, 3, 1, C3), B));
-  // the concurrent small-batch reductions' three regions
-  if (B <= kConcBwdRows) m = std::max(m, conc_regions(B, A, C3).total);
   // + the band reductions' scratch (operand-scale maxima, band.hpp) at the end
   return (m + 3) / 4 * 4 + kBandScratch;
-}
-
-// library-owned streams of the concurrent reductions (per device, created on
-// first use) and their fork / join events; stream-ordered with the caller's
-// stream through the events (host threads must not run two backwards at once on
-// one device -- dx_done_event has the same contract)
-struct BwdAux {
-  hipStream_t s[2] = {};
-  hipEvent_t join[2] = {};
-  bool ok = false;
-};
-static BwdAux* bwd_aux() {
-  static BwdAux aux[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  BwdAux& a = aux[dev];
-  if (!a.ok) {
-    for (int i = 0; i < 2; ++i) {
-      if ((!a.s[i] && hipStreamCreateWithFlags(&a.s[i], hipStreamNonBlocking) != hipSuccess) ||
-          (!a.join[i] && hipEventCreateWithFlags(&a.join[i], hipEventDisableTiming) != hipSuccess))
-        return nullptr;
-    }
-    a.ok = true;
-  }
-  return &a;
 }
 
 static long long afactor_ws_floats(int B) { return conv1_afactor_ws_ints(400LL * B); }
@@ -1408,69 +1358,26 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
     hipEvent_t* ev = dx_done_event();
     ACMI_REQUIRE(ev && hipEventRecord(*ev, s) == hipSuccess, ACMI_ERR_HIP, "acmi_backward: dX event record failed");
   }
-  // small batches: the reductions below on three streams (kConcBwdRows): the
-  // conv1 A factor (+ its fused weight gradient) and band conv3 on the library's
-  // streams, the heads / fc4 reductions and band conv2 here; joined before the
-  // finalize that reads conv1's partials and at the end
-  BwdAux* aux = (g_backward_streams && st && band && fuse_c1 && prep && B <= kConcBwdRows) ? bwd_aux() : nullptr;
-  const bool conc = aux != nullptr;
-  const ConcRegions cr = conc ? conc_regions(B, L.A, L.C3) : ConcRegions{};
-  hipStream_t s_af = s, s_b3 = s;
-  if (conc) {
-    hipEvent_t* ev = dx_done_event();
-    ACMI_REQUIRE(ev && hipStreamWaitEvent(aux->s[0], *ev, 0) == hipSuccess &&
-                     hipStreamWaitEvent(aux->s[1], *ev, 0) == hipSuccess,
-                 ACMI_ERR_HIP, "acmi_backward: fork failed");
-    s_af = aux->s[0];
-    s_b3 = aux->s[1];
-  }
-  auto join = [&](int i, hipStream_t from) {
-    return hipEventRecord(aux->join[i], from) == hipSuccess && hipStreamWaitEvent(s, aux->join[i], 0) == hipSuccess;
-  };
-  bool af_joined = !conc;
   float* wpart_c1 = nullptr;  // conv1's fused weight-gradient partials (in the A-factor workspace)
   if (st) {
     const long long pcap = bwd_partial_cap(B, L.A, L.C3);
-    prof_begin(ACMI_PROF_CONV1_AFACTOR, s_af);
+    prof_begin(ACMI_PROF_CONV1_AFACTOR, s);
     const int rc0 = conv1_afactor_u8(obs, img_stride, B, astat + L.stat_off[0],
-                                     reinterpret_cast<int*>(ws + pcap), afactor_ws_floats(B), s_af,
+                                     reinterpret_cast<int*>(ws + pcap), afactor_ws_floats(B), s,
                                      fuse_c1 ? bw->d1 : nullptr, &wpart_c1, bscr + kBsMaxD1);
-    prof_end(ACMI_PROF_CONV1_AFACTOR, s_af);
+    prof_end(ACMI_PROF_CONV1_AFACTOR, s);
     if (rc0) return rc0;
-  }
-  // conv3 / conv2: pixel-pair band reductions over the dense activation rows
-  // (band.hpp), or the patches of a2 / a1
-  const long long band_cap = pcap_all - kBandScratch;
-  // a1 / a2 bounds from the weights (max |d2|, |d3| came with the dX chain): the
-  // prepared weights' header holds them (tower_stats_body, the same sums as
-  // band_bounds_kernel), else computed here
-  const unsigned* xb = prep ? reinterpret_cast<const unsigned*>(prep + TowerPrep<C3>::HDR) : nullptr;
-  const unsigned* a1b = xb ? xb + kTowMaxA1 : bscr + kBsMaxA1;
-  const unsigned* a2b = xb ? xb + kTowMaxA2 : bscr + kBsMaxA2;
-  if (band && !xb)
-    hipLaunchKernelGGL(band_bounds_kernel, dim3(64), dim3(256), 0, s, P + L.off[0], P + L.off[1], P + L.off[2],
-                       P + L.off[3], bscr);
-  if (conc) {  // band conv3 on its stream, in its own region (the bounds came from the header)
-    ACMI_REQUIRE(xb, ACMI_ERR_ARG, "acmi_backward: concurrent reductions need conv_prep");
-    rc = band_layer(a->a2, 9, 9, 64, 3, 3, 1, bw->d3, C3, B, ws + cr.b3, cr.b2 - cr.b3, grads + L.off[4],
-                    astat + L.stat_off[2], 1.f, a2b, bscr + kBsMaxD3, s_b3);
-    if (rc) return rc;
   }
   // the conv1, heads and fc4 finalizes deferred into one launch: each layer's
   // partials in their own range of the partial region (below the band scratch;
   // a layer that does not fit after the others finalizes the set so far first)
   WgradSet fin;
   long long off = 0;
-  const long long avail = conc ? cr.b3 : pcap_all - kBandScratch;
+  const long long avail = pcap_all - kBandScratch;
   auto flush = [&]() {
-    if (fin.n && !af_joined) {  // conv1's weight-gradient partials come from the A-factor stream
-      ACMI_REQUIRE(join(0, s_af), ACMI_ERR_HIP, "acmi_backward: join failed");
-      af_joined = true;
-    }
     if (fin.n) hipLaunchKernelGGL(finalize_wgrad_multi_kernel, dim3(fin.blocks), dim3(256), 0, s, fin);
     fin = WgradSet();
     off = 0;
-    return ACMI_OK;
   };
   if (st && fuse_c1) {  // the conv1 weight gradient came with the A factor: reduce its chunks
     const long long rows = 400LL * B;
@@ -1483,10 +1390,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // that does not fit after the others starts a new range instead of failing
   auto layer = [&](long long need, auto&& run) {
     long long used = 0;
-    if (fin.n + 2 > kWgradTasks || (off > 0 && need > avail - off)) {
-      const int rf = flush();
-      if (rf) return rf;
-    }
+    if (fin.n + 2 > kWgradTasks || (off > 0 && need > avail - off)) flush();
     const int r = run(part + off, avail - off, &used);
     off += (used + 3) / 4 * 4;
     return r;
@@ -1508,21 +1412,23 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
                        a3b ? bscr + kBsMaxD4 : nullptr, &fin, used);
   });
   if (rc) return rc;
-  if (conc) {  // band conv2 here, in its region, beside the A factor and band conv3
-    rc = band_layer(a->a1, 20, 20, 32, 4, 4, 2, bw->d2, 64, B, ws + cr.b2, band_cap - cr.b2, grads + L.off[2],
-                    astat + L.stat_off[1], 1.f, a1b, bscr + kBsMaxD2, s, ACMI_PROF_CONV2_WGRAD);
-    if (rc) return rc;
-    rc = flush();
-    if (rc) return rc;
-    ACMI_REQUIRE(join(1, s_b3), ACMI_ERR_HIP, "acmi_backward: join failed");
-    return ACMI_OK;
-  }
-  rc = flush();
-  if (rc) return rc;
-  if (band)
+  flush();
+  // conv3 / conv2: pixel-pair band reductions over the dense activation rows
+  // (band.hpp), or the patches of a2 / a1
+  const long long band_cap = pcap_all - kBandScratch;
+  // a1 / a2 bounds from the weights (max |d2|, |d3| came with the dX chain): the
+  // prepared weights' header holds them (tower_stats_body, the same sums as
+  // band_bounds_kernel), else computed here
+  const unsigned* xb = prep ? reinterpret_cast<const unsigned*>(prep + TowerPrep<C3>::HDR) : nullptr;
+  const unsigned* a1b = xb ? xb + kTowMaxA1 : bscr + kBsMaxA1;
+  const unsigned* a2b = xb ? xb + kTowMaxA2 : bscr + kBsMaxA2;
+  if (band) {
+    if (!xb)
+      hipLaunchKernelGGL(band_bounds_kernel, dim3(64), dim3(256), 0, s, P + L.off[0], P + L.off[1], P + L.off[2],
+                         P + L.off[3], bscr);
     rc = band_layer(a->a2, 9, 9, 64, 3, 3, 1, bw->d3, C3, B, part, band_cap, grads + L.off[4],
                     astat + L.stat_off[2], 1.f, a2b, bscr + kBsMaxD3, s);
-  else
+  } else
     rc = wgrad_layer(ConvRows<float, 9, 9, 64, 3, 3, 1>{a->a2, 81 * 64, B * 49}, 576, 49LL * B,
                      bw->d3, C3, C3, st, part, ws_cap, grads + L.off[4], C3, nullptr,
                      st ? astat + L.stat_off[2] : nullptr, s);
@@ -1686,12 +1592,6 @@ int acmi_set_conv_stats_mode(int mode) {
 }
 int acmi_get_conv_stats_mode(void) { return g_conv_stats_mode; }
 
-int acmi_set_backward_streams(int on) {
-  ACMI_REQUIRE(on == 0 || on == 1, ACMI_ERR_ARG, "acmi_set_backward_streams: 0 or 1, not %d", on);
-  g_backward_streams = on;
-  return ACMI_OK;
-}
-int acmi_get_backward_streams(void) { return g_backward_streams; }
 
 int acmi_band_info(int layer, int C3, int64_t rows, int64_t* info) {
   ACMI_REQUIRE(info && (layer == 1 || layer == 2) && (C3 == 32 || C3 == 64) && rows > 0, ACMI_ERR_ARG,

@@ -98,19 +98,6 @@ int acmi_get_forward_mode(void);
 #define ACMI_CONV_STATS_BAND 1
 int acmi_set_conv_stats_mode(int mode);
 int acmi_get_conv_stats_mode(void);
-/* Streams of acmi_backward's weight-gradient / A-factor reductions at small
- * batches (B <= 2048 images, with a_stats, band mode, conv_prep set):
- *   1 (default)  the conv1 A factor and band conv3 on two library-owned
- *                streams beside the heads / fc4 reductions and band conv2 on
- *                the caller's stream (forked after the input-gradient chain,
- *                joined before acmi_backward's last launch: still
- *                stream-ordered on the caller's stream; one host thread per
- *                device at a time)
- *   0            everything on the caller's stream
- * Results are identical either way (own workspace regions, same kernels).
- * Not stream-ordered. */
-int acmi_set_backward_streams(int on);
-int acmi_get_backward_streams(void);
 /* plan facts of the band reduction of conv2 (layer 1) or conv3 (layer 2) at
  * `rows` images: info[0] sub-tiles, [1] groups (blocks per chunk), [2] chunks,
  * [3] rows per chunk, [4] sum over groups of the busiest SIMD's sub-tiles */

@@ -129,52 +129,6 @@ def test_relu_masks_written_and_bit_identical(lib, cuda, use_prep):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize('B', [160, 640], ids=['configs1-32x5', 'configs2-32x20'])
-def test_backward_streams_bit_identical(lib, cuda, B):
-    """acmi_set_backward_streams: at small batches acmi_backward runs the conv1
-    A factor and band conv3 on two library streams beside the heads / fc4
-    reductions and band conv2 (own workspace regions, joined before the
-    finalize that reads conv1's partials).  Gradients and A factors equal the
-    one-stream run bit for bit, run twice (the join is what orders them)."""
-    A, C3 = 4, 32
-    params = rand_params(A, C3, cuda, seed=51)
-    g = torch.Generator().manual_seed(52)
-    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
-    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
-    net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr())
-    _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), _lib.stream_handle())
-    ldh = 8
-    dhead = torch.zeros(B, ldh)
-    dhead[:, :A + 1] = torch.randn(B, A + 1, generator=g) / B
-    dhead = dhead.to(cuda)
-    z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=cuda)
-    so = (ctypes.c_int64 * 11)()
-    tot = ctypes.c_int64()
-    _lib.call('acmi_kfac_layout', A, C3, None, None, so, ctypes.byref(tot))
-    ws = z(lib.acmi_backward_ws_floats(B, A, C3))
-    t, acts = alloc_acts(B, A, C3, cuda, masks=True)
-    _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
-              _lib.stream_handle())
-    prev = lib.acmi_get_backward_streams()
-    out = []
-    try:
-        for on in (0, 1, 1):
-            _lib.call('acmi_set_backward_streams', on)
-            d = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
-            bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
-            grads, astat = z(params.numel()), z(tot.value)
-            ws.fill_(float('nan'))  # stale partials must not leak into the result
-            _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
-                      ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), _lib.stream_handle())
-            torch.cuda.synchronize()
-            out.append((grads.cpu(), astat.cpu()))
-    finally:
-        _lib.call('acmi_set_backward_streams', prev)
-    assert torch.isfinite(out[0][0]).all() and torch.isfinite(out[0][1]).all()
-    for o in out[1:]:
-        assert torch.equal(o[0], out[0][0]) and torch.equal(o[1], out[0][1])
-
-
 @pytest.mark.parametrize('M,N,K', [(128, 128, 32), (300, 260, 200), (1, 4, 4), (1000, 64, 1568)])
 def test_gemm_f32(lib, cuda, M, N, K):
     g = torch.Generator().manual_seed(1)
