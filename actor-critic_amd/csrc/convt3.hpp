@@ -13,9 +13,10 @@
 //   * the K loop streams only the weights (split into f16 h/l by the scale of
 //     max |W| at the commit into gemm3's k-contiguous image layout, ds_read_b128
 //     fragments);
-//   * a lane's B fragment (8 consecutive k = 8 channels of one tap of its
-//     column) is two ds_read_b128 of its dY pixel, split into h/l on the fly by
-//     the scale of max |dY| (published by the dY producer's epilogue);
+//   * the dY image is split into f16 h / l (scale of max |dY|, published by the
+//     dY producer's epilogue) once, as it is staged; a lane's B fragment (8
+//     consecutive k = 8 channels of one tap of its column) is then two
+//     ds_read_b128 of its dY pixel (h chunk, l chunk), no per-read split;
 //   * three f16 MFMAs per 32x32x16 (bf16x3 took six: 183 us per launch at
 //     M = 10240), accumulators unscaled before the epilogue (EpiConvT through
 //     the LDS transpose; it publishes max |dX| in turn).
@@ -75,21 +76,60 @@ struct ConvTX3 {
   }
 };
 
+// conv3's input-gradient weights pre-split once per parameter version (acmi_conv_prepare):
+// the A fragments of v_mfma_f32_32x32x16_f16, [k16 step][row tile][part h, l][lane]
+// x 16 B, lane l of (ks, rt): W3[tap][ci = 32 rt + (l & 31)][co .. co + 7] with k0 =
+// 16 ks + 8 (l >> 5) = (tap, co), scaled by the power of two of max |W3| (the
+// tower's header) -- a k-step's 4 KB then stages as one 16-byte copy per thread
+template <int COUT>
+struct CT3Prep {
+  static constexpr int CIN = 64, KSTEPS = 9 * COUT / 16;
+  static constexpr int STEP_BYTES = 2 * 2 * 1024;  // 2 row tiles x 2 parts x 64 lanes x 16 B
+  static constexpr long long BYTES = (long long)KSTEPS * STEP_BYTES;
+};
+// (block b; 256 threads = four fragments (rt, part-pair lanes))
+template <int COUT>
+__device__ __forceinline__ void convt3_prep_body(const float* w3, char* out, const unsigned* w3max, int b) {
+  using P = CT3Prep<COUT>;
+  const int g = b * 256 + threadIdx.x;  // (ks, rt, lane)
+  if (g >= P::KSTEPS * 2 * 64) return;
+  const int lane = g & 63, rt = (g >> 6) & 1, ks = g >> 7;
+  const int ci = 32 * rt + (lane & 31), k0 = 16 * ks + 8 * (lane >> 5);
+  const int tap = k0 / COUT, co = k0 - tap * COUT;
+  const float* p = w3 + ((long long)tap * P::CIN + ci) * COUT + co;
+  const float sw = f16x2_scale_of_bits(w3max);
+  const float4 x0 = *reinterpret_cast<const float4*>(p), x1 = *reinterpret_cast<const float4*>(p + 4);
+  uint4 h, l;
+  split2(x0.x, x0.y, sw, h.x, l.x);
+  split2(x0.z, x0.w, sw, h.y, l.y);
+  split2(x1.x, x1.y, sw, h.z, l.z);
+  split2(x1.z, x1.w, sw, h.w, l.w);
+  uint4* d = reinterpret_cast<uint4*>(out + (long long)ks * P::STEP_BYTES + rt * 2 * 1024) + lane;
+  d[0] = h;
+  d[64] = l;
+}
+
 template <class CT>
 constexpr int convt_x3_blocks_per_cu() {
   return std::min(8, 160 * 1024 / CT::LDS_BYTES);
 }
 
-template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, int NWAVES, class Epi>
+// PA: the weights come pre-split from acmi_conv_prepare (CT3Prep, S = 1 only): a
+// k-step's A staging is a 16-byte copy per thread; else they are staged from the
+// f32 weights and split at the commit.
+template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, int NWAVES, class Epi, bool PA>
 __global__ __launch_bounds__(64 * NWAVES) __attribute__((amdgpu_waves_per_eu(
     convt_x3_blocks_per_cu<ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES>>() * NWAVES / 4)))
-void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi, const unsigned* wmax, const unsigned* dymax) {
+void convt_x3_kernel(const float* w, const char* wprep, const float* dy, int B, Epi epi, const unsigned* wmax,
+                     const unsigned* dymax) {
   using CT = ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES>;
   using IA = typename CT::IA;
   using W = ConvTWeights<KH, KW, S, CIN, COUT>;
   constexpr int NI = CT::NI, K = CT::K, L = CT::L, NTHR = CT::NTHR;
   constexpr int NA = NI * 16 / 4 / NTHR;  // weight float4 runs per thread per K-tile
   static_assert(NA >= 1 && NI * 16 / 4 == NA * NTHR, "weight staging map");
+  static_assert(!PA || (S == 1 && NI == 64 && NTHR == 256 && IA::BYTES == CT3Prep<COUT>::STEP_BYTES),
+                "prepared weights: conv3's shape");
   __shared__ __attribute__((aligned(16))) char lds[CT::LDS_BYTES];
   char* dimg = lds;
   char* abuf = lds + CT::DY_BYTES;
@@ -103,30 +143,46 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi, const unsi
   const int img_lo = j0 / L;
   const int img_hi = min(B - 1, (j0 + NJ - 1) / L);
 
-  // weights: gemm3's k-contiguous staging (one ConvTWeights run per thread)
+  // weights: prepared fragments (one 16-byte copy per thread and k-step), or
+  // gemm3's k-contiguous staging (one ConvTWeights run per thread)
   const W opA{w};
   typename W::R rowA[NA];
+  if constexpr (!PA) {
 #pragma unroll
-  for (int v = 0; v < NA; ++v) rowA[v] = opA.row((tid + NTHR * v) / 4);
+    for (int v = 0; v < NA; ++v) rowA[v] = opA.row((tid + NTHR * v) / 4);
+  }
   StF4 ra[NA];
-  auto fetch = [&](int k0) {
-    const int k = k0 + (tid % 4) * 4;
-    const auto c = opA.col(k);
+  uint4 rp;
+  auto fetch = [&](int ks) {
+    if constexpr (PA) {
+      rp = reinterpret_cast<const uint4*>(wprep + (long long)min(ks, K / 16 - 1) * IA::BYTES)[tid];
+    } else {
+      const int k = 16 * ks + (tid % 4) * 4;
+      const auto c = opA.col(k);
 #pragma unroll
-    for (int v = 0; v < NA; ++v) ra[v] = opA.stage(rowA[v], c, k < K);
+      for (int v = 0; v < NA; ++v) ra[v] = opA.stage(rowA[v], c, k < K);
+    }
   };
   auto commit = [&](int buf) {
     char* As = abuf + buf * IA::BYTES;
+    if constexpr (PA) {
+      reinterpret_cast<uint4*>(As)[tid] = rp;
+    } else {
 #pragma unroll
-    for (int v = 0; v < NA; ++v) {
-      const int idx = tid + NTHR * v;
-      const int i = idx / 4;
-      IA::write(As, (idx - i * 4) * 4, i, finish(ra[v]), sw);
+      for (int v = 0; v < NA; ++v) {
+        const int idx = tid + NTHR * v;
+        const int i = idx / 4;
+        IA::write(As, (idx - i * 4) * 4, i, finish(ra[v]), sw);
+      }
     }
   };
 
   fetch(0);
-  // dY of images img_lo..img_hi (contiguous [img][OH][OW][COUT]) + the zero pixel
+  // dY of images img_lo..img_hi (contiguous [img][OH][OW][COUT]) + the zero pixel,
+  // split ONCE into its f16 h / l parts (scale of max |dY|) as it is staged: a
+  // pixel's 16-byte chunks c < CH/2 hold h of channels 8c .. 8c+7, chunks CH/2 + c
+  // their l -- every B fragment is then two plain reads (each dY value feeds up to
+  // KHP x KWP taps: split per read it cost 12 VALU per fragment)
   {
     // all of a thread's loads issued before its stores (one latency, not one per load)
     const int n4 = (img_hi - img_lo + 1) * CT::OP * CT::CH;
@@ -142,8 +198,12 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi, const unsi
     for (int q = 0; q < NPT; ++q) {
       const int e = tid + NTHR * q;
       if (e >= n4) break;
-      const int p = e / CT::CH, c = e - p * CT::CH;
-      *reinterpret_cast<float4*>(dimg + CT::chunk_pos(p, c)) = v[q];
+      const int p = e / CT::CH, c = e - p * CT::CH;  // f32 chunk c: channels 4c .. 4c+3
+      uint2 h, l;
+      split2(v[q].x, v[q].y, sd, h.x, l.x);
+      split2(v[q].z, v[q].w, sd, h.y, l.y);
+      *reinterpret_cast<uint2*>(dimg + CT::chunk_pos(p, c >> 1) + 8 * (c & 1)) = h;
+      *reinterpret_cast<uint2*>(dimg + CT::chunk_pos(p, CT::CH / 2 + (c >> 1)) + 8 * (c & 1)) = l;
     }
     for (int c = tid; c < CT::CH; c += NTHR)
       *reinterpret_cast<float4*>(dimg + CT::ZP * COUT * 4 + 16 * c) = f4zero();
@@ -163,10 +223,12 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi, const unsi
     cih[t] = p / CT::PW;
     ciw[t] = p - cih[t] * CT::PW;
   }
-  const int kh8 = 8 * (lane >> 5);
+  const int hl = lane >> 5;
   int aoff[2];
 #pragma unroll
-  for (int tm = 0; tm < 2; ++tm) aoff[tm] = IA::frag_off(lane, 0, wm * 64 + 32 * tm);
+  for (int tm = 0; tm < 2; ++tm)
+    aoff[tm] = PA ? ((2 * (2 * wm + tm)) * 64 + lane) * 16 : IA::frag_off(lane, 0, wm * 64 + 32 * tm);
+  const int apart = PA ? 64 * 16 : IA::PART;  // bytes from a fragment's h part to its l part
 
   f32x16 acc[2][CT::TN];
 #pragma unroll
@@ -177,36 +239,47 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi, const unsi
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   __syncthreads();
 
-  constexpr int NK = K / 16;
-  for (int ks = 0; ks < NK; ++ks) {
-    const int cur = ks & 1;
-    fetch((ks + 1) * 16);
-    __builtin_amdgcn_sched_barrier(0);
-    const char* As = abuf + cur * IA::BYTES;
-    f16x8 a[2][2];
-#pragma unroll
-    for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm) a[tm][pt] = IA::frag(As + pt * IA::PART, aoff[tm]);
-    // this lane's 8 k: channels co..co+7 of tap (khp, kwp)
-    const int k0 = 16 * ks + kh8;
-    const int tap = k0 / COUT, co = k0 - tap * COUT;
+  // taps outer (the lane's dY pixel and its chunk swizzle computed once per tap),
+  // the tap's COUT/16 k-steps inner; k-step ks = tap * NCS + cs
+  constexpr int NCS = COUT / 16, NTAP = CT::KHP * CT::KWP;
+  static_assert(NCS % 2 == 0, "k-steps per tap even: the LDS buffer is cs's parity");
+  for (int tap = 0; tap < NTAP; ++tap) {
     const int khp = tap / CT::KWP, kwp = tap - khp * CT::KWP;
+    int pb[CT::TN], psw[CT::TN];
 #pragma unroll
     for (int tn = 0; tn < CT::TN; ++tn) {
       const int oh = cih[tn] - khp, ow = ciw[tn] - kwp;
       const bool ok = cok[tn] & (oh >= 0) & (ow >= 0) & (oh < CT::OH) & (ow < CT::OW);
       const int p = ok ? cimg[tn] * CT::OP + oh * CT::OW + ow : CT::ZP;
-      const float4 x0 = *reinterpret_cast<const float4*>(dimg + CT::chunk_pos(p, co / 4));
-      const float4 x1 = *reinterpret_cast<const float4*>(dimg + CT::chunk_pos(p, co / 4 + 1));
-      f16x8 b[2];
-      split2x8(x0, x1, sd, b[0], b[1]);
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm) acc[tm][tn] = mfma_x2(a[tm], b, acc[tm][tn]);
+      pb[tn] = p * (COUT * 4);
+      psw[tn] = (p / CT::PIXW) & (CT::CH - 1);
     }
-    __builtin_amdgcn_sched_barrier(0);
-    if (ks + 1 < NK) commit(cur ^ 1);
-    __syncthreads();
+#pragma unroll
+    for (int cs = 0; cs < NCS; ++cs) {
+      const int ks = tap * NCS + cs;
+      const int cur = cs & 1;
+      fetch(ks + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const char* As = abuf + cur * IA::BYTES;
+      f16x8 a[2][2];
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm) a[tm][pt] = IA::frag(As + pt * apart, aoff[tm]);
+      // this lane's 8 k: channels co .. co+7, co = 16 cs + 8 hl: h chunk co / 8
+      const int ch = 2 * cs + hl;
+#pragma unroll
+      for (int tn = 0; tn < CT::TN; ++tn) {
+        f16x8 b[2];
+        b[0] = as_f16x8(*reinterpret_cast<const uint4*>(dimg + pb[tn] + 16 * (ch ^ psw[tn])));
+        b[1] = as_f16x8(*reinterpret_cast<const uint4*>(dimg + pb[tn] + 16 * ((CT::CH / 2 + ch) ^ psw[tn])));
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm) acc[tm][tn] = mfma_x2(a[tm], b, acc[tm][tn]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks + 1 < K / 16) commit(cur ^ 1);
+      __syncthreads();
+    }
   }
   // epilogue through the LDS transpose (the dY image is free now)
 #pragma unroll
@@ -221,12 +294,16 @@ void convt_x3_kernel(const float* w, const float* dy, int B, Epi epi, const unsi
 
 template <int IH, int IW, int KH, int KW, int S, int CIN, int COUT, int NJ, int NWAVES = 4,
           class Epi>
-inline void launch_convt_x3(const float* w, const float* dy, int B, const Epi& e, const unsigned* wmax,
-                            const unsigned* dymax, hipStream_t s) {
+inline void launch_convt_x3(const float* w, const char* wprep, const float* dy, int B, const Epi& e,
+                            const unsigned* wmax, const unsigned* dymax, hipStream_t s) {
   using CT = ConvTX3<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES>;
   static_assert(CT::DY_BYTES >= NWAVES * 32 * 36 * 4, "epilogue transpose needs the dY region");
-  hipLaunchKernelGGL((convt_x3_kernel<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES, Epi>),
-                     dim3(cdiv(B * CT::L, NJ)), dim3(CT::NTHR), 0, s, w, dy, B, e, wmax, dymax);
+  if (wprep)
+    hipLaunchKernelGGL((convt_x3_kernel<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES, Epi, true>),
+                       dim3(cdiv(B * CT::L, NJ)), dim3(CT::NTHR), 0, s, w, wprep, dy, B, e, wmax, dymax);
+  else
+    hipLaunchKernelGGL((convt_x3_kernel<IH, IW, KH, KW, S, CIN, COUT, NJ, NWAVES, Epi, false>),
+                       dim3(cdiv(B * CT::L, NJ)), dim3(CT::NTHR), 0, s, w, wprep, dy, B, e, wmax, dymax);
 }
 
 }  // namespace acmi

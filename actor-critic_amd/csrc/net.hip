@@ -1276,6 +1276,8 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
   // conv input gradients as transposed products: rows = (phase, channel) of
   // the weights, columns = (super-)pixels gathering dY (EpiConvT, float4 rows)
   {  // conv3 -> d2 (stride 1: one phase)
+    // its weights pre-split in the prepared buffer (after fc4's, acmi_conv_prep_bytes)
+    const char* ct3p = prep ? prep + TowerPrep<C3>::BYTES + CT2::BYTES + fc4_prep_bytes(49 * C3) : nullptr;
     using Src = ConvTRows<9, 9, 3, 3, 1, C3>;
     using W = ConvTWeights<3, 3, 1, 64, C3>;
     W opA{P + L.off[4]};
@@ -1283,7 +1285,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     auto run = [&](auto epi) {
       if (g_gemm_mode == ACMI_GEMM_X3)
         // f16x2 operands: the scales of max |W3| and of max |d3| (the fc4 dX epilogue's)
-        launch_convt_x3<9, 9, 3, 3, 1, 64, C3, 256>(P + L.off[4], bw->d3, B, epi, w3max, dxs + kBsMaxD3, s);
+        launch_convt_x3<9, 9, 3, 3, 1, 64, C3, 256>(P + L.off[4], ct3p, bw->d3, B, epi, w3max, dxs + kBsMaxD3, s);
       else
         launch_mm<64, 128, 16, 1, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
     };
@@ -1675,8 +1677,9 @@ static int forward_dispatch(const acmi_net_t* net, const uint8_t* obs, int64_t i
 int64_t acmi_conv_prep_bytes(int C3) {
   // the tower's conv weights, then conv2's input-gradient weights (convt2.hpp)
   // and fc4's weights (fc4roll.hpp)
-  return C3 == 32   ? TowerPrep<32>::BYTES + CT2::BYTES + fc4_prep_bytes(49 * 32)
-         : C3 == 64 ? TowerPrep<64>::BYTES + CT2::BYTES + fc4_prep_bytes(49 * 64)
+  // and conv3's input-gradient weights (convt3.hpp)
+  return C3 == 32   ? TowerPrep<32>::BYTES + CT2::BYTES + fc4_prep_bytes(49 * 32) + CT3Prep<32>::BYTES
+         : C3 == 64 ? TowerPrep<64>::BYTES + CT2::BYTES + fc4_prep_bytes(49 * 64) + CT3Prep<64>::BYTES
                     : -1;
 }
 
@@ -1704,7 +1707,9 @@ struct PrepArgs {
   unsigned* hdr;     // its bounds header
   char* ct2;         // CT2 block
   char* fc4;         // fc4 fragments
-  int nb3, nbt, nbc;  // split-pass block counts: stats3, tower, convt2 (fc4 after)
+  int nb3, nbt, nbc;  // split-pass block counts: stats3, tower, convt2 (fc4, then convt3 after)
+  int nbf;            // fc4's
+  char* ct3;          // conv3 input-gradient fragments (CT3Prep)
 };
 __global__ __launch_bounds__(256) void conv_prep_bounds_kernel(PrepArgs a) {
   const int b = blockIdx.x;
@@ -1720,8 +1725,12 @@ __global__ __launch_bounds__(256) void conv_prep_split_kernel(PrepArgs a) {
     tower_prep_body(a.w1, a.w2, a.w3, a.C3, a.tower, a.hdr, b);
   } else if ((b -= a.nbt) < a.nbc) {
     convt2_prep_body(a.w2, a.ct2, b);
+  } else if ((b -= a.nbc) < a.nbf) {
+    fc4_prep_body(a.w4, a.K4, a.fc4, a.hdr, b);
   } else {
-    fc4_prep_body(a.w4, a.K4, a.fc4, a.hdr, b - a.nbc);
+    b -= a.nbf;
+    if (a.C3 == 32) convt3_prep_body<32>(a.w3, a.ct3, a.hdr + kTowMaxW3, b);
+    else convt3_prep_body<64>(a.w3, a.ct3, a.hdr + kTowMaxW3, b);
   }
 }
 
@@ -1743,13 +1752,16 @@ int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
                      (CT2::BYTES - CT2::FRAG_BYTES) / 16);
   const float* P = net->params;
   char* base = static_cast<char*>(prep);
+  const int K4 = 49 * L.C3;
+  const int nbf = K4 / 16 * 16 * 64 / 256;
+  const int nb3p = (L.C3 == 32 ? CT3Prep<32>::KSTEPS : CT3Prep<64>::KSTEPS) * 2 * 64 / 256;
   PrepArgs a{P + L.off[0], P + L.off[1], P + L.off[2], P + L.off[3], P + L.off[4], P + L.off[5], P + L.off[6],
-             L.C3, 49 * L.C3, base, reinterpret_cast<unsigned*>(base + oh), base + o2, base + o2 + CT2::BYTES,
-             L.C3 / 4, (16 + 64 + 36 * (L.C3 / 32)) * 64 / 256 + 1, CT2::NKS * 4 * 64 / 256};
-  const int nbf = a.K4 / 16 * 16 * 64 / 256;
+             L.C3, K4, base, reinterpret_cast<unsigned*>(base + oh), base + o2, base + o2 + CT2::BYTES,
+             L.C3 / 4, (16 + 64 + 36 * (L.C3 / 32)) * 64 / 256 + 1, CT2::NKS * 4 * 64 / 256, nbf,
+             base + o2 + CT2::BYTES + fc4_prep_bytes(K4)};
   hipLaunchKernelGGL(conv_prep_bounds_kernel, dim3(64 + kPrepWmaxBlocks), dim3(256), 0, (hipStream_t)stream, a);
-  hipLaunchKernelGGL(conv_prep_split_kernel, dim3(a.nb3 + a.nbt + a.nbc + nbf), dim3(256), 0, (hipStream_t)stream,
-                     a);
+  hipLaunchKernelGGL(conv_prep_split_kernel, dim3(a.nb3 + a.nbt + a.nbc + nbf + nb3p), dim3(256), 0,
+                     (hipStream_t)stream, a);
   ACMI_LAUNCH_CHECK("acmi_conv_prepare");
   return ACMI_OK;
 }

@@ -129,6 +129,44 @@ def test_relu_masks_written_and_bit_identical(lib, cuda, use_prep):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize('C3', [32, 64])
+def test_conv3_dx_prepared_weights_bit_identical(lib, cuda, C3):
+    """conv3's input gradient (convt3.hpp) on W3 fragments pre-split by
+    acmi_conv_prepare equals the variant that stages and splits the f32 weights
+    per block, bit for bit (same scale of max |W3|, same fragments, same MFMA
+    order): d3 and d2 of one backward with and without net->conv_prep, on the
+    same forward activations and head gradients."""
+    A, B = 4, 300
+    params = rand_params(A, C3, cuda, seed=61)
+    g = torch.Generator().manual_seed(62)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
+    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
+    net_p = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr())
+    net_n = _lib.Net(A, C3, params.data_ptr(), None)
+    _lib.call('acmi_conv_prepare', ctypes.byref(net_p), _lib.ptr(prep), _lib.stream_handle())
+    ldh = 8
+    dhead = torch.zeros(B, ldh)
+    dhead[:, :A + 1] = torch.randn(B, A + 1, generator=g) / B
+    dhead = dhead.to(cuda)
+    z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=cuda)
+    ws = z(lib.acmi_backward_ws_floats(B, A, C3))
+    t, acts = alloc_acts(B, A, C3, cuda, masks=True)
+    _lib.call('acmi_forward', ctypes.byref(net_p), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+              _lib.stream_handle())
+    out = []
+    for net in (net_p, net_n):
+        d = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
+        bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
+        grads = z(params.numel())
+        _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
+                  ctypes.byref(bwd), _lib.ptr(grads), None, _lib.ptr(ws), _lib.stream_handle())
+        torch.cuda.synchronize()
+        out.append((d[2].cpu(), d[1].cpu()))
+    assert out[0][1].abs().max() > 0
+    assert torch.equal(out[0][0], out[1][0]), 'd3'
+    assert torch.equal(out[0][1], out[1][1]), 'd2'
+
+
 @pytest.mark.parametrize('M,N,K', [(128, 128, 32), (300, 260, 200), (1, 4, 4), (1000, 64, 1568)])
 def test_gemm_f32(lib, cuda, M, N, K):
     g = torch.Generator().manual_seed(1)
