@@ -94,6 +94,7 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
   const float sd = f16x2_scale_of_bits(d2max);
   const float inv = 1.f / (f16x2_scale_of_bits(reinterpret_cast<const unsigned*>(prep + CT2::FRAG_BYTES)) * sd);
 
+  float d1am = 0.f;  // !GRAM: max |d1| over the lane's stores, published once at the end
   f32x16 gacc;  // GRAM: this wave's D D^T over its tiles
 #pragma unroll
   for (int r = 0; r < 16; ++r) gacc[r] = 0.f;
@@ -205,10 +206,67 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
     // epilogue: rows (phase p, ci) x this wave's 32 super-pixel columns
     float* scr = reinterpret_cast<float*>(lds) + wave * 32 * 36;  // [32][36] per wave
     if constexpr (!GRAM) {
-      // ReLU'-masked d1 through the LDS transpose: each store instruction writes
-      // 8 whole 128-byte pixel rows (gemm.hpp store_tile_lds, EpiConvT addressing)
-      store_tile_lds<4, 1>(EpiConvT<20, 20, 2, 32, MASK>{d1, a1, d1max}, reinterpret_cast<const f32x16(&)[4][1]>(acc), 0,
-                           tile * CT2::TILE + 32 * wave, lane, scr, 4 * CT2::CIN, J);
+      // ReLU'-masked d1 through the LDS transpose (each store instruction writes 8
+      // whole 128-byte pixel rows): after it, lane (ri = 4 (lane & 7), cj = lane >> 3)
+      // holds channels ri .. ri+3 of super-pixel columns cj + 8 q (q < 4) of each
+      // phase.  Its four super-pixels are decoded once per tile (not per phase and
+      // element, as EpiConvT's generic offset() does), a phase adds (py, px) to the
+      // pixel, and the ReLU' bits come from one mask word per pixel.
+      const int ri = 4 * (lane & 7), cj = lane >> 3;
+      int pix[4];
+      bool jok[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = tile * CT2::TILE + 32 * wave + cj + 8 * q;
+        jok[q] = j < J;
+        const int jj = jok[q] ? j : 0;
+        const int nn = jj / CT2::L, sp = jj - nn * CT2::L;
+        const int yy = sp / CT2::PW, xx = sp - yy * CT2::PW;
+        pix[q] = (nn * 20 + 2 * yy) * 20 + 2 * xx;
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(scr + (lane & 31) * 36 + 8 * g + 4 * hl) =
+              make_float4(acc[p][4 * g], acc[p][4 * g + 1], acc[p][4 * g + 2], acc[p][4 * g + 3]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int dp = (p >> 1) * 20 + (p & 1);
+        float4 v[4];
+        uint32_t bits[4];
+        float4 xa[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[q] = *reinterpret_cast<const float4*>(scr + (cj + 8 * q) * 36 + ri);
+          const int px = pix[q] + dp;
+          if constexpr (MASK) bits[q] = reinterpret_cast<const uint32_t*>(jok[q] ? a1 + px : zero)[0] >> ri;
+          else xa[q] = *reinterpret_cast<const float4*>(jok[q] ? a1 + px * CT2::CIN + ri : zero);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float4 o;
+          if constexpr (MASK) {
+            o.x = (bits[q] & 1u) ? v[q].x : 0.f;
+            o.y = (bits[q] & 2u) ? v[q].y : 0.f;
+            o.z = (bits[q] & 4u) ? v[q].z : 0.f;
+            o.w = (bits[q] & 8u) ? v[q].w : 0.f;
+          } else {
+            o.x = xa[q].x > 0.f ? v[q].x : 0.f;
+            o.y = xa[q].y > 0.f ? v[q].y : 0.f;
+            o.z = xa[q].z > 0.f ? v[q].z : 0.f;
+            o.w = xa[q].w > 0.f ? v[q].w : 0.f;
+          }
+          if (jok[q]) {
+            *reinterpret_cast<float4*>(d1 + (long long)(pix[q] + dp) * CT2::CIN + ri) = o;
+            d1am = absmax4(d1am, o);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
     } else {
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
@@ -255,6 +313,7 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
     __syncthreads();  // the ring / scratch is reused by the next tile
   }
 
+  if constexpr (!GRAM) amax_publish(d1max, d1am, lane);
   if constexpr (GRAM) {
     // the 4 waves' Grams summed in wave order through LDS, then part[block][33][32]
     float* red = reinterpret_cast<float*>(lds);  // [32][32]

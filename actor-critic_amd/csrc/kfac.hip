@@ -327,12 +327,16 @@ __device__ void gj_next_pivot(const MatSet& s, double* ws, int step, int mi, dou
 
 // grid: the active matrices' pivot blocks, then every matrix's upper-triangle
 // 64x64 tiles (tile0 prefix sums)
+#ifndef ACMI_GJ_PROBE  // timing probes (wrong results): 1 no tile updates, 2 no next-pivot blocks
+#define ACMI_GJ_PROBE 0
+#endif
 __global__ __launch_bounds__(256) void gj_step_kernel(MatSet s, double* ws, int step) {
   __shared__ double lds[kGjLds];
   if ((int)blockIdx.x < s.count) {
-    gj_next_pivot(s, ws, step, blockIdx.x, lds);
+    if constexpr (!(ACMI_GJ_PROBE & 2)) gj_next_pivot(s, ws, step, blockIdx.x, lds);
     return;
   }
+  if constexpr (ACMI_GJ_PROBE & 1) return;
   const int b = blockIdx.x - s.count;
   int mi = 0;
   while (mi + 1 < s.count && b >= s.tile0[mi + 1]) ++mi;
