@@ -12,11 +12,11 @@ for cfg in "acktr32x20:--envs-per-gpu 32" "a2c32x5:--algo a2c --envs-per-gpu 32"
   tag=${cfg%%:*}; args=${cfg#*:}
   out="$root/gpurun_out/$name/$tag"; mkdir -p "$out"
   echo "=== $tag bench"
-  timeout -k 10 200 python3 bench.py $args --steps 50 --warmup 10 --no-cpu-baseline > "$out/bench.json" 2> "$out/bench.err" || exit $?
+  timeout -k 10 200 python3 bench.py $args --steps 50 --warmup 10 --no-cpu-baseline --no-configs2 > "$out/bench.json" 2> "$out/bench.err" || exit $?
   tail -1 "$out/bench.json" | cut -c1-300
   echo "=== $tag rocprofv3"
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$out/prof" -o prof \
-    --output-format csv -- python3 "$root/bench.py" $args --steps 30 --warmup 5 --no-cpu-baseline \
+    --output-format csv -- python3 "$root/bench.py" $args --steps 30 --warmup 5 --no-cpu-baseline --no-configs2 \
     > "$out/prof_bench.json" 2> "$out/prof.err") || exit $?
   cp "$(find "$out/prof" -name '*kernel_stats.csv' | head -1)" "$out/kernel_stats.csv"
   cp "$(find "$out/prof" -name '*kernel_trace.csv' | head -1)" "$out/kernel_trace.csv"
