@@ -19,6 +19,7 @@
 // the staged bf16x3 launch (test_fc4_rollout_matches_gemm3), not bit-identical.
 #pragma once
 
+#include "stepper.hpp"  // PendState, env_commit_pending
 #include "tower.hpp"
 
 namespace acmi {
@@ -52,9 +53,18 @@ inline long long fc4_prep_bytes(int K) { return (long long)(K / 16) * 16 * 2 * 1
 
 // block b: K chunk z = b % nz, then (row tile, column half); wave w: column
 // group 4 * half + w (64 columns).
+// commit: the split rollout step's pending env states (towersplit.hpp), written
+// into the env state by block 0 before this step's tail reads them (commitB = 0:
+// none).
+struct Fc4Commit {
+  PendState* pend;
+  acmi_env_state_t st;
+  int B;
+};
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
 void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w4p, int nz, int chunk_steps,
-                     float* part, const unsigned* hdr) {
+                     float* part, const unsigned* hdr, Fc4Commit cm) {
+  if (cm.B > 0 && blockIdx.x == 0) env_commit_pending(cm.st, cm.pend, cm.B);
   constexpr int D = kFc4Depth, NSLOT = D + 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int z = blockIdx.x % nz, rest = blockIdx.x / nz;
@@ -120,11 +130,11 @@ void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w
 // false when the shape is not one this kernel covers (the caller then uses gemm3)
 // hdr: the tower's bounds header (TowerPrep::HDR of the same prep)
 inline bool launch_fc4_roll(const float* a3, long long lda, int B, int K, const char* w4p, int nz, int chunk,
-                            float* part, const unsigned* hdr, hipStream_t s) {
+                            float* part, const unsigned* hdr, hipStream_t s, Fc4Commit cm = Fc4Commit{}) {
   if (chunk % 16 || K % 16 || (lda % 4) || ((uintptr_t)a3 % 16)) return false;
   const int cs = chunk / 16;
   const dim3 grid(nz * ((B + 31) / 32) * 2), blk(256);
-  hipLaunchKernelGGL(fc4_roll_kernel, grid, blk, 0, s, a3, lda, B, K, w4p, nz, cs, part, hdr);
+  hipLaunchKernelGGL(fc4_roll_kernel, grid, blk, 0, s, a3, lda, B, K, w4p, nz, cs, part, hdr, cm);
   return true;
 }
 

@@ -23,6 +23,7 @@
 #include "fc4roll.hpp"
 #include "convt2.hpp"
 #include "stepper.hpp"
+#include "towersplit.hpp"
 
 namespace acmi {
 
@@ -236,17 +237,22 @@ struct TailArgs {
 constexpr int kMaxHeads = 32;
 // sx [512], sl [kMaxHeads], s_action: the block's scratch in LDS; mirror
 // (nullable): the new stack also goes there (the fused next-step tower's image)
-template <int NZ>
+// SPLIT (towersplit.hpp): one of kSplitParts workgroups of env `row` (part `spart`):
+// the heads and the draw are computed by every part (the same arithmetic, so the
+// same action), only part 0 stores them; the env step builds the stack words the
+// part's tower needs (env_step_part) and the post-step state goes to pend.
+template <int NZ, bool SPLIT = false>
 __device__ __forceinline__ void rollout_tail_body(
     const float* part, int nz, const float* b4, float* a4, long long a4_stride, int B,
     const float* wpi, const float* bpi, const float* wv, const float* bv, int A, float* logits,
     long long l_stride, float* value, long long v_stride, const TailArgs& ta, float* sx, float* sl,
-    int& s_action, uint4* mirror) {
-  const int row = blockIdx.x;
+    int& s_action, uint4* mirror, int row = -1, int spart = 0, PendState* pend = nullptr) {
+  if (row < 0) row = blockIdx.x;
+  const bool writer = spart == 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   EnvPre pre;  // the env's state and current stack: in flight during the heads
-  env_prefetch(ta.io.state, row, ta.obs + (long long)row * ta.img_stride, pre);
-  if (ta.io.obs_copy) {  // the stacks this step read, filed where the batch keeps them
+  if constexpr (!SPLIT) env_prefetch(ta.io.state, row, ta.obs + (long long)row * ta.img_stride, pre);
+  if (!SPLIT && ta.io.obs_copy) {  // the stacks this step read, filed where the batch keeps them
     uint4* cp = reinterpret_cast<uint4*>(ta.io.obs_copy + (long long)row * ta.io.out_stride);
 #pragma unroll
     for (int i = 0; i < kEnvWords; ++i) {
@@ -281,7 +287,7 @@ __device__ __forceinline__ void rollout_tail_body(
 #pragma unroll
       for (int z = 0; z < NZ; ++z) acc += pv[h][z];
       const float v = fmaxf(acc + b4[j], 0.f);
-      x[j] = v;
+      if (writer) x[j] = v;
       sx[j] = v;
     }
   } else {
@@ -309,20 +315,32 @@ __device__ __forceinline__ void rollout_tail_body(
   __syncthreads();
   const acmi_rollout_io_t& io = ta.io;
   if (threadIdx.x == 0) {
-    for (int a = 0; a < A; ++a) logits[(long long)row * l_stride + a] = sl[a];
-    if (value) value[(long long)row * v_stride] = sl[A];
+    if (writer) {
+      for (int a = 0; a < A; ++a) logits[(long long)row * l_stride + a] = sl[a];
+      if (value) value[(long long)row * v_stride] = sl[A];
+    }
     const uint32_t ctr = io.counter + (io.counter_dev ? *io.counter_dev : 0u);
     bool bad;
     const int y = sample_row(sl, A, io.seed, io.stream_id, ctr, (uint32_t)(row + io.row_offset),
                              nullptr, 0, &bad);
-    if (bad) atomicAdd(io.bad_rows, 1);
-    io.actions[(long long)row * io.ld] = y;
+    if (writer) {
+      if (bad) atomicAdd(io.bad_rows, 1);
+      io.actions[(long long)row * io.ld] = y;
+    }
     s_action = y;
   }
   __syncthreads();
-  env_step_block_pre(io.state, row, (uint32_t)(io.env_offset + row), io.env_seed, (uint32_t)s_action, pre,
-                     io.obs_out + (long long)row * io.out_stride, io.rewards, io.terminals,
-                     io.episode_rewards, io.ld, mirror);
+  if constexpr (SPLIT) {
+    env_step_part(io.state, row, (uint32_t)(io.env_offset + row), io.env_seed, (uint32_t)s_action,
+                  ta.obs + (long long)row * ta.img_stride, split_word_lo(spart), split_word_hi(spart),
+                  split_own_lo(spart), split_own_hi(spart), io.obs_out + (long long)row * io.out_stride,
+                  io.obs_copy ? io.obs_copy + (long long)row * io.out_stride : nullptr, mirror, writer, io.rewards,
+                  io.terminals, io.episode_rewards, io.ld, pend);
+  } else {
+    env_step_block_pre(io.state, row, (uint32_t)(io.env_offset + row), io.env_seed, (uint32_t)s_action, pre,
+                       io.obs_out + (long long)row * io.out_stride, io.rewards, io.terminals,
+                       io.episode_rewards, io.ld, mirror);
+  }
 }
 
 template <int NZ>
@@ -363,6 +381,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void r
   __syncthreads();  // the image in LDS; the tail's scratch free again
   tower_body<C3, H16, true>(nullptr, 0, nt.b1, nt.b2, nt.b3, nt.a1, nt.a2, nt.a3, nt.st, nt.prep, nt.m1, nt.m2,
                             nt.m3, lds, blockIdx.x);
+}
+
+// The split rollout step (small batches, towersplit.hpp): kSplitParts workgroups
+// per env -- the tail (redundant heads / draw, the env step's words each part's
+// tower needs, the post-step state into pend) and then part j of the next
+// step's conv tower.  The pending states are committed by the next step's fc4
+// launch (fc4_roll_kernel: env_commit_pending), the first launch after this one.
+template <int NZ, int C3, bool H16>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void rollout_tail_split_kernel(
+    const float* part, int nz, const float* b4, float* a4, long long a4_stride, int B,
+    const float* wpi, const float* bpi, const float* wv, const float* bv, int A, float* logits,
+    long long l_stride, float* value, long long v_stride, TailArgs ta, NextTower nt, PendState* pend) {
+  __shared__ __attribute__((aligned(16))) char lds[kSpLds];
+  const int n = blockIdx.x / kSplitParts, j = blockIdx.x - n * kSplitParts;
+  float* sx = reinterpret_cast<float*>(lds + kSpImg);  // the tail's scratch in the a1 image
+  int* s_action = reinterpret_cast<int*>(sx + 512 + kMaxHeads);
+  rollout_tail_body<NZ, true>(part, nz, b4, a4, a4_stride, B, wpi, bpi, wv, bv, A, logits, l_stride, value, v_stride,
+                              ta, sx, sx + 512, *s_action, reinterpret_cast<uint4*>(lds), n, j, pend);
+  __syncthreads();  // the image rows in LDS; the tail's scratch free again
+  tower_part_body<C3, H16>(j, nt.b1, nt.b2, nt.b3, nt.a1, nt.a2, nt.a3, nt.st, nt.prep, nt.m1, nt.m2, nt.m3, lds, n);
+}
+// the split tower alone (small batches without a fused tail: step 0, the bootstrap
+// forward): part j loads the input rows 8j .. 8j+35 of image n
+template <int C3, bool H16>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void tower_split_kernel(
+    const uint8_t* obs, long long img_stride, NextTower nt) {
+  __shared__ __attribute__((aligned(16))) char lds[kSpLds];
+  const int n = blockIdx.x / kSplitParts, j = blockIdx.x - n * kSplitParts;
+  const uint4* src = reinterpret_cast<const uint4*>(obs + n * img_stride);
+  uint4* dst = reinterpret_cast<uint4*>(lds);
+  const int g0 = split_word_lo(j), g1 = split_word_hi(j);
+  constexpr int NW = (36 * 21 + 255) / 256;
+  uint4 v[NW];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int g = g0 + (int)threadIdx.x + 256 * i;
+    v[i] = src[g < g1 ? g : g0];
+  }
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int g = g0 + (int)threadIdx.x + 256 * i;
+    if (g < g1) dst[g] = v[i];
+  }
+  __syncthreads();
+  tower_part_body<C3, H16>(j, nt.b1, nt.b2, nt.b3, nt.a1, nt.a2, nt.a3, nt.st, nt.prep, nt.m1, nt.m2, nt.m3, lds, n);
 }
 
 inline int roundup4(int x) { return (x + 3) & ~3; }
@@ -476,12 +539,26 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   ACMI_REQUIRE(!nxt || (nxt->a1 && nxt->a2 && nxt->a3 && masks_ok(nxt) && tail->io.next_act_stride >= 1 &&
                         (uintptr_t)tail->io.obs_out % 16 == 0 && tail->io.out_stride % 16 == 0),
                ACMI_ERR_ARG, "acmi_rollout_step: bad next_acts / next_act_stride / obs_out alignment");
+  // small batches: each image's tower over kSplitParts workgroups (towersplit.hpp)
+  auto tower_any = [&](const uint8_t* o, long long ostride, float* a1, float* a2, float* a3, long long ast,
+                       uint32_t* m1, uint32_t* m2, uint32_t* m3) {
+    const bool h16 = g_forward_mode == ACMI_FWD_BF16;
+    if (B <= kSplitMaxB) {
+      const NextTower nt{P + L.off[1], P + L.off[3], P + L.off[5], a1, a2, a3, ast,
+                         static_cast<const char*>(prep), m1, m2, m3};
+      if (h16)
+        hipLaunchKernelGGL((tower_split_kernel<C3, true>), dim3(B * kSplitParts), dim3(256), 0, s, o, ostride, nt);
+      else
+        hipLaunchKernelGGL((tower_split_kernel<C3, false>), dim3(B * kSplitParts), dim3(256), 0, s, o, ostride, nt);
+    } else {
+      launch_tower<C3>(o, ostride, B, P, L.off, a1, a2, a3, ast, prep, s, h16, m1, m2, m3);
+    }
+  };
   if (tower) {
     // the three convs fused per image (16-byte image loads)
     if (!tower_done) {
       prof_begin(ACMI_PROF_CONV1_FWD, s);
-      launch_tower<C3>(obs, img_stride, B, P, L.off, a->a1, a->a2, a->a3, st, prep, s,
-                       g_forward_mode == ACMI_FWD_BF16, a->m1, a->m2, a->m3);
+      tower_any(obs, img_stride, a->a1, a->a2, a->a3, st, a->m1, a->m2, a->m3);
       prof_end(ACMI_PROF_CONV1_FWD, s);
     }
   } else {
@@ -532,14 +609,23 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   int nz, chunk;
   fc4_plan(B, K4, &nz, &chunk);
   const bool split = nz > 1 && a->ws && a->ws_floats >= (long long)nz * (B + 1) * 512;
+  // the split rollout step's pending env states, after fc4's slabs in the forward
+  // workspace (acmi_forward_ws_floats reserves them at B <= kSplitMaxB)
+  PendState* pend = split && tail && B <= kSplitMaxB &&
+                            a->ws_floats >= (long long)nz * (B + 1) * 512 + (long long)B * (sizeof(PendState) / 4)
+                        ? reinterpret_cast<PendState*>(a->ws + (long long)nz * (B + 1) * 512)
+                        : nullptr;
   if (split) {
     // small (rollout) batches: split K over chunks; the heads kernel reduces
     // the slabs in fixed order and applies bias + relu
     const char* w4p = prep ? static_cast<const char*>(prep) + TowerPrep<C3>::BYTES + CT2::BYTES : nullptr;
+    // (only a step whose tower ran in the previous step's tail can have states pending)
+    const Fc4Commit cm{pend, tail ? tail->io.state : acmi_env_state_t{}, pend && tower_done ? B : 0};
     if (!(g_gemm_mode == ACMI_GEMM_X3 && w4p &&
           launch_fc4_roll(a->a3, st * K4, B, K4, w4p, nz, chunk, a->ws,
                           reinterpret_cast<const unsigned*>(static_cast<const char*>(prep) + TowerPrep<C3>::HDR),
-                          s))) {
+                          s, cm))) {
+      // (no fused tower without the rollout fc4: no split step, nothing pending)
       EpiPartial epi{a->ws, B, 512};
       launch_mm<64, 128, 32, 1, 2, true, false, 16>(opA4, opB4, epi, B, 512, K4, nz, chunk, s);
     }
@@ -562,7 +648,18 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // below 128 images -- K = 1568 / 3136 in chunks of 7 / 13 k16-steps)
   const bool fuse_next = nxt && split && (nz == 8 || nz == 14 || nz == 16);
 #define ACMI_HEADS(NZ)                                                                          \
-  if (tail && fuse_next && (NZ == 8 || NZ == 14 || NZ == 16)) {                                 \
+  if (tail && fuse_next && pend && (NZ == 14 || NZ == 16)) {                                    \
+    if (h16)                                                                                    \
+      hipLaunchKernelGGL((rollout_tail_split_kernel<NZ == 16 ? 16 : 14, C3, true>), dim3(B * kSplitParts), hb, 0, s, \
+                         hp, nz, P + L.off[7], a->a4, st * 512, B, P + L.off[8], P + L.off[9],  \
+                         P + L.off[10], P + L.off[11], L.A, a->logits, st * a->ld_logits, hv, st, \
+                         *tail, ntw, pend);                                                     \
+    else                                                                                        \
+      hipLaunchKernelGGL((rollout_tail_split_kernel<NZ == 16 ? 16 : 14, C3, false>), dim3(B * kSplitParts), hb, 0, s, \
+                         hp, nz, P + L.off[7], a->a4, st * 512, B, P + L.off[8], P + L.off[9],  \
+                         P + L.off[10], P + L.off[11], L.A, a->logits, st * a->ld_logits, hv, st, \
+                         *tail, ntw, pend);                                                     \
+  } else if (tail && fuse_next && (NZ == 8 || NZ == 14 || NZ == 16)) {                          \
     if (h16)                                                                                    \
       hipLaunchKernelGGL((rollout_tail_tower_kernel<NZ == 16 ? 16 : NZ == 14 ? 14 : 8, C3, true>), dim3(B), hb, 0, s, hp, nz, \
                          P + L.off[7], a->a4, st * 512, B, P + L.off[8], P + L.off[9],          \
@@ -602,8 +699,8 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   }
 #undef ACMI_HEADS
   if (nxt && !fuse_next)  // the next step's tower on the stacks the tail just wrote
-    launch_tower<C3>(tail->io.obs_out, tail->io.out_stride, B, P, L.off, nxt->a1, nxt->a2, nxt->a3,
-                     tail->io.next_act_stride, prep, s, h16, nxt->m1, nxt->m2, nxt->m3);
+    tower_any(tail->io.obs_out, tail->io.out_stride, nxt->a1, nxt->a2, nxt->a3, tail->io.next_act_stride, nxt->m1,
+              nxt->m2, nxt->m3);
   ACMI_LAUNCH_CHECK("acmi_forward");
   return ACMI_OK;
 }
@@ -1797,7 +1894,9 @@ int64_t acmi_forward_ws_floats(int B) {
   fc4_plan(B, 49 * 64, &nz, &chunk);
   int nz2, chunk2;
   fc4_plan(B, 49 * 32, &nz2, &chunk2);
-  return (long long)std::max(nz, nz2) * (B + 1) * 512;
+  // + the split rollout step's pending env states (forward_impl)
+  return (long long)std::max(nz, nz2) * (B + 1) * 512 +
+         (B <= kSplitMaxB ? (long long)B * (long long)(sizeof(PendState) / 4) : 0);
 }
 
 int64_t acmi_backward_ws_floats(int B, int A, int C3) {

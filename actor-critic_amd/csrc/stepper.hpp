@@ -161,6 +161,104 @@ __device__ __forceinline__ void env_step_block_pre(acmi_env_state_t st, int n, u
   }
 }
 
+// The env step of one of several workgroups sharing env n (the split rollout
+// step, towersplit.hpp): every one reads the pre-step state (nobody writes it
+// during the launch), builds the new stack's 16-byte words [g0, g1) into `mirror`
+// (its LDS image, word g at mirror[g]) and files words [o0, o1) into obs_out
+// (the owners partition the stack); the writer also stores the reward, terminal
+// and episode total and the post-step state into pend[0..5] with pend[5] = 1
+// (committed into st by the next step's fc4 launch, env_commit_pending: a part
+// that started late could otherwise read a state another part already advanced).
+// The arithmetic is env_step_block_pre's, word for word.
+struct PendState {  // pend[8] per env: episode, step, length, total (bits), done, flag
+  int32_t k, t, L, total_bits, done, flag, pad0, pad1;
+};
+__device__ __forceinline__ void env_step_part(acmi_env_state_t st, int n, uint32_t e, uint32_t seed, uint32_t action,
+                                              const uint8_t* obs_in, int g0, int g1, int o0, int o1,
+                                              uint8_t* obs_out, uint8_t* obs_copy, uint4* mirror, bool writer,
+                                              float* rewards, uint8_t* terminals, float* ep_rewards, long long ld,
+                                              PendState* pend) {
+  const bool was_done = st.done[n] != 0;
+  int32_t k = st.episode[n];
+  int32_t t = st.step[n];
+  int32_t L = st.length[n];
+  float total = st.total[n];
+  const GameParams gp = game_params(env_game(st, n));
+  if (was_done) {
+    k += 1;
+    t = 0;
+    L = episode_length(seed, e, (uint32_t)k, gp);
+    total = 0.f;
+  }
+  t += 1;
+  const uint32_t a = (action & 255u) < gp.n_legal ? (action & 255u) : 0u;
+  const uint32_t gseed = seed ^ gp.salt;
+  const uint32_t base = key4(gseed, e, (uint32_t)k, (uint32_t)t * 256u + a);
+  const uint32_t rh = mix32(base ^ REW_SALT) >> 8;
+  const float rew = rh < gp.rew_lo ? -1.f : (rh >= gp.rew_hi ? 1.f : 0.f);
+  const bool term = t >= L;
+  const uint32_t rbase = key4(gseed, e, (uint32_t)k, RESET_TAG);
+  const uint4* in = reinterpret_cast<const uint4*>(obs_in);
+  uint4* out = reinterpret_cast<uint4*>(obs_out);
+  constexpr int NW = (36 * 21 + kEnvThreads - 1) / kEnvThreads;  // a part's range: <= 36 rows of 21 words
+  uint4 old[NW];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int g = g0 + (int)threadIdx.x + kEnvThreads * i;
+    old[i] = in[g < g1 ? g : g0];
+  }
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int g = g0 + (int)threadIdx.x + kEnvThreads * i;
+    if (g >= g1) break;
+    uint4 ow = old[i];
+    if (obs_copy && g >= o0 && g < o1) reinterpret_cast<uint4*>(obs_copy)[g] = ow;
+    if (was_done) {
+      const uint32_t w = word_hash(rbase, (uint32_t)g);
+      ow.x = (w & 255u) * 0x01010101u;
+      ow.y = ((w >> 8) & 255u) * 0x01010101u;
+      ow.z = ((w >> 16) & 255u) * 0x01010101u;
+      ow.w = (w >> 24) * 0x01010101u;
+    }
+    const uint32_t f = word_hash(base, (uint32_t)g);
+    uint4 o;
+    o.x = (term ? 0u : (ow.x >> 8)) | ((f & 255u) << 24);
+    o.y = (term ? 0u : (ow.y >> 8)) | (((f >> 8) & 255u) << 24);
+    o.z = (term ? 0u : (ow.z >> 8)) | (((f >> 16) & 255u) << 24);
+    o.w = (term ? 0u : (ow.w >> 8)) | ((f >> 24) << 24);
+    mirror[g] = o;
+    if (g >= o0 && g < o1) out[g] = o;
+  }
+  if (writer && threadIdx.x == 0) {
+    total += rew;
+    rewards[n * ld] = rew;
+    terminals[n * ld] = term ? 1 : 0;
+    ep_rewards[n * ld] = term ? total : __int_as_float(0x7fc00000);
+    PendState ps;
+    ps.k = k;
+    ps.t = t;
+    ps.L = L;
+    ps.total_bits = __float_as_int(term ? 0.f : total);
+    ps.done = term ? 1 : 0;
+    ps.flag = 1;
+    ps.pad0 = ps.pad1 = 0;
+    pend[n] = ps;
+  }
+}
+// the pending post-step states of envs 0 .. B-1 into st (one thread per env)
+__device__ __forceinline__ void env_commit_pending(acmi_env_state_t st, PendState* pend, int B) {
+  for (int n = threadIdx.x; n < B; n += blockDim.x) {
+    const PendState ps = pend[n];
+    if (!ps.flag) continue;
+    st.episode[n] = ps.k;
+    st.step[n] = ps.t;
+    st.length[n] = ps.L;
+    st.total[n] = __int_as_float(ps.total_bits);
+    st.done[n] = ps.done;
+    pend[n].flag = 0;
+  }
+}
+
 __device__ __forceinline__ void env_step_block(acmi_env_state_t st, int n, uint32_t e, uint32_t seed,
                                                uint32_t action, const uint8_t* obs_in,
                                                uint8_t* obs_out, float* rewards,

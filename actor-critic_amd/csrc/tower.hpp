@@ -27,6 +27,11 @@
 // waves (roles rotated by block parity: equal per-SIMD load); conv2 the 3x2
 // tiles as one full tile + half the K of row tile 2 per wave (the halves summed
 // in wave order through LDS); conv3 (C3 = 32) two row tiles x two K halves.
+// Every output pixel of every layer is the sum of two K halves, (first) +
+// (second), each an MFMA chain from zero: a wave running a tile's whole K keeps
+// the first half's accumulator and restarts at the midpoint.  That is the
+// partition towersplit.hpp (one image over 7 workgroups, small batches) can run
+// in parallel, so the two towers agree bit for bit.
 // Activations are also written to global memory (strided rows, like EpiAct) for
 // the update's backward and K-FAC statistics.
 #pragma once
@@ -231,15 +236,19 @@ __device__ __forceinline__ void tower_prep_body(const float* w1, const float* w2
 
 // row of the 32x32 C/D fragment element r of `lane`
 __device__ __forceinline__ int tow_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+// llvm.amdgcn.writelane (no clang builtin in this toolchain): v_writelane that
+// hipcc schedules and pads -- a VALU-written SGPR (the ballot, often vcc) needs 2
+// wait states before a writelane reads it, which hipcc inserts (s_nop 1) or fills
+__device__ int acmi_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 // the ReLU' words of element R's two rows (ballot halves: rows tow_row(R, 0) and
 // tow_row(R, 32)) written into the lanes of the same index of mw
 template <int R>
 __device__ __forceinline__ uint32_t tow_mword(uint32_t mw, unsigned long long bal) {
   constexpr int rr = (R & 3) + 8 * (R >> 2);
   const uint32_t lo = (uint32_t)bal, hi = (uint32_t)(bal >> 32);
-  asm volatile("v_writelane_b32 %0, %1, %2\n\tv_writelane_b32 %0, %3, %4"
-               : "+v"(mw)
-               : "s"(lo), "n"(rr), "s"(hi), "n"(rr + 4));
+  // (an unpadded asm-string writelane straight after the v_cmp read a stale vcc_lo)
+  mw = (uint32_t)acmi_writelane((int)lo, rr, (int)mw);
+  mw = (uint32_t)acmi_writelane((int)hi, rr + 4, (int)mw);
   return mw;
 }
 // f(std::integral_constant<int, I>) for I = B .. E-1
@@ -324,7 +333,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       const int oh = p / 20, ow = p - oh * 20;
       abase[u] = (4 * oh * 84 + 4 * ow) * 4 + 8 * kh8;
     }
-    f32x16 acc[4];
+    f32x16 acc[4], h0[3];  // h0: tiles u < 3, K half 0 (k-steps 0-7)
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -347,6 +356,14 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
         b[1] = b[0];
       }
       const int koff = (s >> 1) * 336 + 16 * (s & 1);  // kernel row kh = s/2, kw half
+      if (s == 8) {  // every pixel sums its K halves (k-steps 0-7) + (8-15): the split tower's partition
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          h0[u] = acc[u];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
+        }
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (u == 3 && (w < 2 || (s >> 3) != w - 2)) continue;
@@ -383,7 +400,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       uint32_t mw = 0;
       tow_static_for<0, 16>([&](auto R) {  // rows < 384
         constexpr int r = decltype(R)::value;
-        mw = tow_mword<r>(mw, emit1(32 * tile_of(u) + tow_row(r, lane), acc[u][r]));
+        mw = tow_mword<r>(mw, emit1(32 * tile_of(u) + tow_row(r, lane), h0[u][r] + acc[u][r]));
       });
       if (!(ACMI_TOW_PROBE & 4) && mg && lane < 32) mg[32 * tile_of(u) + lane] = mw;
     }
@@ -421,7 +438,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       pin[u] = 2 * oh * 20 + 2 * ow;
       px[u] = 2 * ow;
     }
-    f32x16 accF, accH;
+    f32x16 accF, accH, hF;  // hF: row tile rtf, K half 0 (k-steps 0-15)
 #pragma unroll
     for (int r = 0; r < 16; ++r) accF[r] = accH[r] = 0.f;
     TowB<64, H16> bw{prep + P::O2};
@@ -434,6 +451,11 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       bw.get(s % kTowSlots, b);
       const int tap = s >> 1, kh = tap >> 2, kw = tap & 3;
       const int c8 = 2 * (s & 1) + kh8;  // the 8 channels of this k-step and lane half
+      if (s == 16) {  // every pixel sums its K halves (0-15) + (16-31)
+        hF = accF;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accF[r] = 0.f;
+      }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         if (u == 1 && (s < hk0 || s >= hk0 + 16)) continue;
@@ -477,7 +499,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       uint32_t mw = 0;
       tow_static_for<0, 16>([&](auto R) {  // rows 0..63 are all valid
         constexpr int r = decltype(R)::value;
-        mw = tow_mword<r>(mw, emit(32 * rtf + tow_row(r, lane), accF[r], true));
+        mw = tow_mword<r>(mw, emit(32 * rtf + tow_row(r, lane), hF[r] + accF[r], true));
       });
       if (!(ACMI_TOW_PROBE & 4) && mg && lane < 32) mg[2 * (32 * rtf + lane) + ct] = mw;
     }
@@ -507,7 +529,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     const int p0 = min(32 * rt + col, 48);
     const int oh = p0 / 7, ow = p0 - oh * 7;
     const int pin = oh * 9 + ow;
-    f32x16 acc;
+    f32x16 acc, h3;  // h3 (C3 = 64): K half 0 (k-steps 0-17)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     TowB<C3, H16> bw{prep + P::O3};
@@ -517,6 +539,11 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
 #pragma unroll
     for (int i = 0; i < NK; ++i) {
       const int ss = s0 + i;
+      if (C3 == 64 && i == NS / 2) {  // every pixel sums its K halves (0-17) + (18-35)
+        h3 = acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      }
       if (i + kTowDepth < NK) bw.fetch(ss + kTowDepth, ct, lane, (i + kTowDepth) % kTowSlots);
       f16x8 b[2];
       bw.get(i % kTowSlots, b);
@@ -571,7 +598,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       __syncthreads();
       if (wave < 2) emit_tile([&](int r) { return acc[r] + scr[(rt * 32 + tow_row(r, lane)) * 32 + col]; });
     } else {
-      emit_tile([&](int r) { return acc[r]; });
+      emit_tile([&](int r) { return h3[r] + acc[r]; });
     }
   }
 }

@@ -84,13 +84,16 @@ def _relu_bits(a, words):
     return torch.where(v >= 2 ** 31, v - 2 ** 32, v).int()
 
 
-@pytest.mark.parametrize('use_prep', [True, False], ids=['tower', 'per-layer'])
-def test_relu_masks_written_and_bit_identical(lib, cuda, use_prep):
+@pytest.mark.parametrize('use_prep,B', [(True, 300), (True, 5), (False, 300)],
+                         ids=['tower', 'split-tower', 'per-layer'])
+def test_relu_masks_written_and_bit_identical(lib, cuda, use_prep, B):
     """The ReLU' bit masks (acmi_acts_t m1..m3) written by the forward -- the fused
-    tower's ballots or the per-layer path's act_mask_kernel -- equal (a > 0) bit for
-    bit, and the backward and output statistics that mask their input gradients
-    from them instead of re-reading a1..a3 are bit-identical to the mask-free run."""
-    A, C3, B = 4, 32, 300
+    tower's ballots (B = 300), the split tower's (B = 5 <= kSplitMaxB: each image
+    over 7 workgroups, every mask word written by the part that owns its row) or
+    the per-layer path's act_mask_kernel -- equal (a > 0) bit for bit, and the
+    backward and output statistics that mask their input gradients from them
+    instead of re-reading a1..a3 are bit-identical to the mask-free run."""
+    A, C3 = 4, 32
     params = rand_params(A, C3, cuda, seed=41)
     g = torch.Generator().manual_seed(42)
     obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
@@ -127,6 +130,41 @@ def test_relu_masks_written_and_bit_identical(lib, cuda, use_prep):
         out[masks] = (grads.cpu(), astat.cpu(), gstat.cpu(), d1.cpu())
     for a, b in zip(out[False], out[True]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('C3', [32, 64])
+@pytest.mark.parametrize('fwd', ['f32', 'bf16'])
+def test_split_tower_bit_identical_to_one_block_tower(lib, cuda, C3, fwd):
+    """The small-batch split tower (towersplit.hpp: B <= kSplitMaxB = 64, each image
+    over 7 workgroups) equals the one-block tower (tower.hpp) bit for bit -- a1..a3
+    and the ReLU' words m1..m3 of the same images, once as a 5-image batch and once
+    inside a 70-image batch -- in both forward modes and at both conv3 widths: every
+    output pixel runs the same MFMA chain over the same K partition (conv1 pixels
+    384..399, conv2 pixels 64..80 and conv3 at C3 = 32 as two K halves)."""
+    A, B = 4, 5
+    prev = lib.acmi_get_forward_mode()
+    _lib.call('acmi_set_forward_mode', _lib.FWD_BF16 if fwd == 'bf16' else _lib.FWD_F32)
+    try:
+        params = rand_params(A, C3, cuda, seed=71)
+        g = torch.Generator().manual_seed(72)
+        big = torch.randint(0, 256, (70, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
+        prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
+        net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr())
+        _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), _lib.stream_handle())
+        out = []
+        for obs in (big[17:17 + B].contiguous(), big):
+            t, acts = alloc_acts(obs.shape[0], A, C3, cuda, masks=True)
+            ws = torch.zeros(int(lib.acmi_forward_ws_floats(obs.shape[0])), device=cuda)
+            acts.ws, acts.ws_floats = ws.data_ptr(), ws.numel()
+            _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, obs.shape[0],
+                      ctypes.byref(acts), 1, _lib.stream_handle())
+            torch.cuda.synchronize()
+            out.append(t)
+        for k in ('a1', 'a2', 'a3', 'm1', 'm2', 'm3'):
+            assert torch.equal(out[0][k], out[1][k][17:17 + B]), k
+        assert torch.equal(out[1]['m2'], _relu_bits(out[1]['a2'], 162))
+    finally:
+        _lib.call('acmi_set_forward_mode', prev)
 
 
 @pytest.mark.parametrize('C3', [32, 64])

@@ -349,6 +349,16 @@ def test_rollout_matches_oracle_env_and_tower(lib, cuda):
         r = ref[name].reshape(got.shape)
         rel = np.abs(got.cpu().double().numpy() - r).max() / np.abs(r).max()
         assert rel < 1e-5, (name, rel)
+    # at N = 3 the rollout's towers ran split (step 0: tower_split_kernel, steps 1..:
+    # rollout_tail_split_kernel, each image over 7 workgroups; towersplit.hpp): bit
+    # for bit the one-block tower's activations and ReLU' words on the same
+    # observations inside a 72-image batch (B > kSplitMaxB)
+    M = N * T
+    rep = torch.from_numpy(np.concatenate([o.reshape(M, 84, 84, 4)] * 4)).to(cuda)
+    one, _ = model.engine.forward_obs(rep, key='one-block')
+    torch.cuda.synchronize()
+    for k in ('a1', 'a2', 'a3', 'm1', 'm2', 'm3'):
+        assert torch.equal(getattr(fwd.acts, k)[:M], getattr(one, k)[:M]), k
     # the actions are the oracle's inverse-CDF draws of the rollout's counters
     lg = fwd.flat_logits.cpu().numpy().reshape(N, T, A)
     for t in range(T):
