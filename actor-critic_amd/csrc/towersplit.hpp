@@ -26,6 +26,10 @@
 namespace acmi {
 
 constexpr int kSplitParts = 7;   // = conv3's output rows
+#ifndef ACMI_SPLIT_DEPTH  // k-steps of B fragments in flight per wave (tower.hpp TowB)
+#define ACMI_SPLIT_DEPTH 2
+#endif
+constexpr int kSpDepth = ACMI_SPLIT_DEPTH, kSpSlots = kSpDepth + 1;
 constexpr int kSplitMaxB = 64;   // images per launch the split path takes (7 x 64 = 448 workgroups)
 constexpr int kSpA1Rows = 8;     // a1 rows per part
 constexpr int kSpA1Px = kSpA1Rows * 20;  // 160 = 5 tiles of 32
@@ -87,14 +91,14 @@ __device__ __forceinline__ void tower_part_body(int j, const float* b1, const fl
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
-    TowB<32, H16> bw{prep + P::O1};
+    TowB<32, H16, kSpDepth> bw{prep + P::O1};
 #pragma unroll
-    for (int i = 0; i < kTowDepth; ++i) bw.fetch(i, 0, lane, i);
+    for (int i = 0; i < kSpDepth; ++i) bw.fetch(i, 0, lane, i);
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      if (s + kTowDepth < 16) bw.fetch(s + kTowDepth, 0, lane, (s + kTowDepth) % kTowSlots);
+      if (s + kSpDepth < 16) bw.fetch(s + kSpDepth, 0, lane, (s + kSpDepth) % kSpSlots);
       f16x8 b[2];
-      bw.get(s % kTowSlots, b);
+      bw.get(s % kSpSlots, b);
       const int koff = (s >> 1) * 336 + 16 * (s & 1);
       if (s == 8) {
         h0 = acc[0];
@@ -138,6 +142,9 @@ __device__ __forceinline__ void tower_part_body(int j, const float* b1, const fl
     if (wave == 0) tile_out(4, [&](int r) { return acc[1][r] + scr[tow_row(r, lane) * 32 + col]; });
   }
   __syncthreads();
+#ifdef ACMI_SPLIT_STOP  // timing probe (wrong results): 1 stop after conv1, 2 after conv2
+  if constexpr (ACMI_SPLIT_STOP == 1) return;
+#endif
 
   // ---- conv2: a2 rows j .. j+2 (local pixel q2 = global - 9 j) -----------------
   {
@@ -147,15 +154,15 @@ __device__ __forceinline__ void tower_part_body(int j, const float* b1, const fl
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    TowB<64, H16> bw{prep + P::O2};
+    TowB<64, H16, kSpDepth> bw{prep + P::O2};
 #pragma unroll
-    for (int i = 0; i < kTowDepth; ++i) bw.fetch(16 * kq + i, ct, lane, i);
+    for (int i = 0; i < kSpDepth; ++i) bw.fetch(16 * kq + i, ct, lane, i);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int s = 16 * kq + i;
-      if (i + kTowDepth < 16) bw.fetch(s + kTowDepth, ct, lane, (i + kTowDepth) % kTowSlots);
+      if (i + kSpDepth < 16) bw.fetch(s + kSpDepth, ct, lane, (i + kSpDepth) % kSpSlots);
       f16x8 b[2];
-      bw.get(i % kTowSlots, b);
+      bw.get(i % kSpSlots, b);
       const int tap = s >> 1, kh = tap >> 2, kw = tap & 3;
       const int c8 = 2 * (s & 1) + kh8;
       const int p = pin + kh * 20 + kw, x = 2 * (q2 % 9) + kw;
@@ -194,6 +201,9 @@ __device__ __forceinline__ void tower_part_body(int j, const float* b1, const fl
     }
   }
   __syncthreads();
+#ifdef ACMI_SPLIT_STOP
+  if constexpr (ACMI_SPLIT_STOP == 2) return;
+#endif
 
   // ---- conv3: a3 row j (7 pixels) ------------------------------------------------
   {
@@ -206,16 +216,16 @@ __device__ __forceinline__ void tower_part_body(int j, const float* b1, const fl
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      TowB<C3, H16> bw{prep + P::O3};
+      TowB<C3, H16, kSpDepth> bw{prep + P::O3};
       const int s0 = 18 * kh;
 #pragma unroll
-      for (int i = 0; i < kTowDepth; ++i) bw.fetch(s0 + i, ct, lane, i);
+      for (int i = 0; i < kSpDepth; ++i) bw.fetch(s0 + i, ct, lane, i);
 #pragma unroll
       for (int i = 0; i < 18; ++i) {
         const int ss = s0 + i;
-        if (i + kTowDepth < 18) bw.fetch(ss + kTowDepth, ct, lane, (i + kTowDepth) % kTowSlots);
+        if (i + kSpDepth < 18) bw.fetch(ss + kSpDepth, ct, lane, (i + kSpDepth) % kSpSlots);
         f16x8 b[2];
-        bw.get(i % kTowSlots, b);
+        bw.get(i % kSpSlots, b);
         const int tap = ss >> 2, kr = tap / 3, kc = tap - kr * 3;
         const int c8 = 2 * (ss & 3) + kh8;
         const int p = kr * 9 + q3 + kc, x = q3 + kc;
