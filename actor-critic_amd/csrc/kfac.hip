@@ -177,23 +177,33 @@ __device__ void pivot_inverse(double (*P)[GJB + 1], double (*Q)[GJB + 1]) {
       double (*src)[GJB + 1] = h ? Q : P;
       double (*dst)[GJB + 1] = h ? P : Q;
       const int k0 = t + 2 * h;
+      // every LDS read of the sweep first (the writes go to the other image, but
+      // interleaved with them the reads could not be hoisted: one LDS round trip
+      // per row), then the arithmetic, then the four writes
       const double a = src[k0][k0], b = src[k0][k0 + 1], e = src[k0 + 1][k0], d = src[k0 + 1][k0 + 1];
+      const double s0 = src[k0][c], s1 = src[k0 + 1][c];
+      double m0[4], m1[4], mc[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = r0 + 8 * q;
+        m0[q] = src[r][k0];
+        m1[q] = src[r][k0 + 1];
+        mc[q] = src[r][c];
+      }
       const double idet = recip_f64(fma(a, d, -(b * e)));
       const double D00 = d * idet, D01 = -b * idet, D10 = -e * idet, D11 = a * idet;
-      const double s0 = src[k0][c], s1 = src[k0 + 1][c];
       const double u0 = fma(D00, s0, D01 * s1), u1 = fma(D10, s0, D11 * s1);  // (D M_Kc)
       const int ck = c - k0;
       const double dc0 = ck == 0 ? D00 : D01, dc1 = ck == 0 ? D10 : D11;  // column c of D (c in K)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int r = r0 + 8 * q;
-        const double m0 = src[r][k0], m1 = src[r][k0 + 1];
         double v;
         if (r == k0 || r == k0 + 1) {
           const double w = r == k0 ? u0 : u1;
           v = (ck == 0 || ck == 1) ? (r == k0 ? dc0 : dc1) : w;
         } else {
-          v = (ck == 0 || ck == 1) ? -fma(m0, dc0, m1 * dc1) : src[r][c] - fma(m0, u0, m1 * u1);
+          v = (ck == 0 || ck == 1) ? -fma(m0[q], dc0, m1[q] * dc1) : mc[q] - fma(m0[q], u0, m1[q] * u1);
         }
         dst[r][c] = v;
       }
@@ -277,6 +287,9 @@ __global__ __launch_bounds__(256) void gj_first_kernel(MatSet s, double* ws) {
 constexpr int kGjLds = GJB * (GJB + 1) + 64 * (GJB + 1) + GJB * (64 + 1);
 typedef double GjRow[GJB + 1];
 
+#ifndef ACMI_GJ_PROBE  // timing probes (wrong results): 1 no tile updates, 2 no next-pivot blocks,
+#define ACMI_GJ_PROBE 0  // 4 no pivot inverse (sweeps), 8 next-pivot blocks stop after their loads
+#endif
 // block (m, 0): Pinv_{k+1} from M_k and Pinv_k
 __device__ void gj_next_pivot(const MatSet& s, double* ws, int step, int mi, double* lds) {
   const int np = s.np[mi];
@@ -302,34 +315,41 @@ __device__ void gj_next_pivot(const MatSet& s, double* ws, int step, int mi, dou
     oldv[u] = M[(long long)(nb + r) * np + nb + c];
   }
   __syncthreads();
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {  // the tile blocks' Rrow' sums (q order)
-    const int t = r0 + 8 * u;
-    double acc = 0.0;
+  if constexpr (ACMI_GJ_PROBE & 8) {
+    if (Pv[0][0] == 12345.0) PIn[0] = Mr[1][1] + Cn[2][2] + oldv[0];
+    return;
+  }
+  {  // the tile blocks' Rrow' sums (q order), four independent chains
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 8
-    for (int q = 0; q < GJB; ++q) acc += Pv[t][q] * Mr[q][c];
-    Rn[t][c] = acc;
+    for (int q = 0; q < GJB; ++q) {
+      const double m = Mr[q][c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += Pv[r0 + 8 * u][q] * m;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) Rn[r0 + 8 * u][c] = acc[u];
   }
   __syncthreads();
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {  // the tile blocks' update sums (t order)
-    const int r = r0 + 8 * u;
-    double acc = 0.0;
+  {  // the tile blocks' update sums (t order)
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 8
-    for (int t = 0; t < GJB; ++t) acc += Cn[r][t] * Rn[t][c];
-    P[r][c] = oldv[u] - acc;
+    for (int t = 0; t < GJB; ++t) {
+      const double rn = Rn[t][c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += Cn[r0 + 8 * u][t] * rn;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) P[r0 + 8 * u][c] = oldv[u] - acc[u];
   }
   __syncthreads();
-  pivot_inverse(P, Q);
+  if constexpr (!(ACMI_GJ_PROBE & 4)) pivot_inverse(P, Q);
 #pragma unroll
   for (int u = 0; u < 4; ++u) PIn[(r0 + 8 * u) * GJB + c] = P[r0 + 8 * u][c];
 }
 
 // grid: the active matrices' pivot blocks, then every matrix's upper-triangle
 // 64x64 tiles (tile0 prefix sums)
-#ifndef ACMI_GJ_PROBE  // timing probes (wrong results): 1 no tile updates, 2 no next-pivot blocks
-#define ACMI_GJ_PROBE 0
-#endif
 __global__ __launch_bounds__(256) void gj_step_kernel(MatSet s, double* ws, int step) {
   __shared__ double lds[kGjLds];
   if ((int)blockIdx.x < s.count) {
@@ -351,33 +371,57 @@ __global__ __launch_bounds__(256) void gj_step_kernel(MatSet s, double* ws, int 
   double* Mo = gj_out(s, mi, step, ws);
   const double* PIk = ws + s.pi_off[mi] + (step & 1) * GJB * GJB;
   const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
-  // every load issued up front: the old values of the non-pivot outputs, Pinv_k,
-  // this thread's column of the pivot rows, the old pivot columns of the rows
+  // every load issued up front, then the LDS stores: the old values of the
+  // non-pivot outputs, Pinv_k, the old pivot columns of the rows (Cs) and the
+  // pivot rows over the tile's columns (Rs) -- 36 independent loads per thread in
+  // one round trip (loads behind conditions or interleaved with their LDS stores
+  // each waited for the whole queue: ~20 round trips per step)
+  // (the upper-triangle element of (row, pivot column) / (pivot row, column) is a
+  // row segment of M on one side of the pivot and a column segment on the other:
+  // consecutive threads walk whichever index is contiguous in memory)
+  auto sym_idx = [&](int r, int c) -> long long {  // gj_sym's element, clamped into the matrix
+    const int a = min(min(r, c), np - 1), b = min(max(r, c), np - 1);
+    return (long long)a * np + b;
+  };
+  // (no selects on the loaded values: a value of a padding row / column or of the
+  // pivot block is loaded from a clamped address and never used -- the outputs
+  // out of range are not stored, the pivot rows / columns take Rrow' / Pinv, and
+  // the Rrow' sums of the pivot and padding columns are not formed -- so the
+  // compiler cannot turn a select into a branch that waits for its load)
   double old[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
-    const int i = i0 + ty + 16 * a;
-    const bool ipiv = i >= kb && i < kb + GJB;
+    const int i = min(i0 + ty + 16 * a, np - 1);
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int j = j0 + tx + 16 * b;
-      const bool jpiv = j >= kb && j < kb + GJB;
-      old[a][b] = (i >= np || j >= np || ipiv || jpiv) ? 0.0 : M[(long long)i * np + j];
-    }
+    for (int b = 0; b < 4; ++b) old[a][b] = M[(long long)i * np + min(j0 + tx + 16 * b, np - 1)];
+  }
+  const bool rows_below = i0 >= kb + GJB, cols_left = j0 + 64 <= kb;
+  double pv[GJB * GJB / 256], cv[64 * GJB / 256], rv[64 * GJB / 256];
+#pragma unroll
+  for (int u = 0; u < GJB * GJB / 256; ++u) pv[u] = PIk[threadIdx.x + 256 * u];
+#pragma unroll
+  for (int u = 0; u < 64 * GJB / 256; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    const int r = rows_below ? e % 64 : e / GJB, t = rows_below ? e / 64 : e % GJB;
+    cv[u] = M[sym_idx(i0 + r, kb + t)];
+    const int q = cols_left ? e % GJB : e / 64, c = cols_left ? e / GJB : e % 64;
+    rv[u] = M[sym_idx(kb + q, j0 + c)];  // pivot rows
   }
   GjRow* Pv = reinterpret_cast<GjRow*>(lds);
   GjRow* Cs = Pv + GJB;                                         // [64]
   double (*Rs)[64 + 1] = reinterpret_cast<double (*)[64 + 1]>(Cs + 64);  // [GJB]
-  for (int e = threadIdx.x; e < GJB * GJB; e += 256) Pv[e / GJB][e % GJB] = PIk[e];
-  // (the upper-triangle element of (row, pivot column) / (pivot row, column) is a
-  // row segment of M on one side of the pivot and a column segment on the other:
-  // consecutive threads walk whichever index is contiguous in memory)
-  const bool rows_below = i0 >= kb + GJB, cols_left = j0 + 64 <= kb;
-  for (int e = threadIdx.x; e < 64 * GJB; e += 256) {
+#pragma unroll
+  for (int u = 0; u < GJB * GJB / 256; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    Pv[e / GJB][e % GJB] = pv[u];
+  }
+#pragma unroll
+  for (int u = 0; u < 64 * GJB / 256; ++u) {
+    const int e = threadIdx.x + 256 * u;
     const int r = rows_below ? e % 64 : e / GJB, t = rows_below ? e / 64 : e % GJB;
-    Cs[r][t] = (i0 + r < np) ? gj_sym(M, np, i0 + r, kb + t) : 0.0;
-    const int q = cols_left ? e % GJB : e / 64, c = cols_left ? e / GJB : e % 64, jq = j0 + c;
-    Rs[q][c] = (jq < np && !(jq >= kb && jq < kb + GJB)) ? gj_sym(M, np, kb + q, jq) : 0.0;  // pivot rows
+    Cs[r][t] = cv[u];
+    const int q = cols_left ? e % GJB : e / 64, c = cols_left ? e / GJB : e % 64;
+    Rs[q][c] = rv[u];
   }
   __syncthreads();
   {  // Rrow' in place of the pivot rows: thread (column cj, pivot rows t0 .. t0 + 7)
