@@ -287,6 +287,28 @@ __global__ __launch_bounds__(256) void gj_first_kernel(MatSet s, double* ws) {
 constexpr int kGjLds = GJB * (GJB + 1) + 64 * (GJB + 1) + GJB * (64 + 1);
 typedef double GjRow[GJB + 1];
 
+// The step's products on the fp64 matrix cores (v_mfma_f64_16x16x4f64): a 16 x 16
+// block of A[.][0..31] B[0..31][.] as eight k-steps of 4 in k order.  Lane l feeds
+// A[l & 15][4s + (l >> 4)] and B[4s + (l >> 4)][l & 15]; result reg r is element
+// (row (l >> 4) + 4r, column l & 15).  The tile blocks and the next-pivot block
+// form every element of Rrow' and of the update with this same chain, so the
+// pivot block's copy of M_{k+1}'s next pivot block is bit-identical to the one
+// the tile block stores.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int gj_lrow(int r) { return ((threadIdx.x & 63) >> 4) + 4 * r; }  // result row
+__device__ __forceinline__ int gj_lcol() { return threadIdx.x & 15; }                          // result column
+template <int NB, class FA, class FB>
+__device__ __forceinline__ void gj_mfma32(f64x4 (&acc)[NB], FA a, FB b) {
+  const int l = threadIdx.x & 63, ar = l & 15, ak = l >> 4;
+#pragma unroll
+  for (int u = 0; u < NB; ++u) acc[u] = f64x4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < GJB / 4; ++s)
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a(u, ar, 4 * s + ak), b(u, 4 * s + ak, ar), acc[u], 0, 0, 0);
+}
+
 #ifndef ACMI_GJ_PROBE  // timing probes (wrong results): 1 no tile updates, 2 no next-pivot blocks,
 #define ACMI_GJ_PROBE 0  // 4 no pivot inverse (sweeps), 8 next-pivot blocks stop after their loads
 #endif
@@ -305,6 +327,8 @@ __device__ void gj_next_pivot(const MatSet& s, double* ws, int step, int mi, dou
   GjRow* P = Mr;
   GjRow* Q = Pv;
   const int c = threadIdx.x & (GJB - 1), r0 = threadIdx.x >> 5;
+  // wave w: the 16 x 16 block (rows 16 (w >> 1), columns 16 (w & 1)) of Rn and P
+  const int w = threadIdx.x >> 6, br = 16 * (w >> 1), bc = 16 * (w & 1);
   double oldv[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -312,35 +336,25 @@ __device__ void gj_next_pivot(const MatSet& s, double* ws, int step, int mi, dou
     Pv[r][c] = PIk[r * GJB + c];
     Mr[r][c] = gj_sym(M, np, kb + r, nb + c);
     Cn[c][r] = M[(long long)(kb + r) * np + nb + c];  // (the upper element of (nb + c, kb + r))
-    oldv[u] = M[(long long)(nb + r) * np + nb + c];
+    oldv[u] = M[(long long)(nb + br + gj_lrow(u)) * np + nb + bc + gj_lcol()];
   }
   __syncthreads();
   if constexpr (ACMI_GJ_PROBE & 8) {
     if (Pv[0][0] == 12345.0) PIn[0] = Mr[1][1] + Cn[2][2] + oldv[0];
     return;
   }
-  {  // the tile blocks' Rrow' sums (q order), four independent chains
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 8
-    for (int q = 0; q < GJB; ++q) {
-      const double m = Mr[q][c];
+  {  // the tile blocks' Rrow' = Pinv_k M_k[kb.., nb..]
+    f64x4 acc[1];
+    gj_mfma32(acc, [&](int, int i, int k) { return Pv[br + i][k]; }, [&](int, int k, int j) { return Mr[k][bc + j]; });
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] += Pv[r0 + 8 * u][q] * m;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) Rn[r0 + 8 * u][c] = acc[u];
+    for (int r = 0; r < 4; ++r) Rn[br + gj_lrow(r)][bc + gj_lcol()] = acc[0][r];
   }
   __syncthreads();
-  {  // the tile blocks' update sums (t order)
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 8
-    for (int t = 0; t < GJB; ++t) {
-      const double rn = Rn[t][c];
+  {  // the tile blocks' update: P = M_k[nb.., nb..] - Ccol Rrow'
+    f64x4 acc[1];
+    gj_mfma32(acc, [&](int, int i, int k) { return Cn[br + i][k]; }, [&](int, int k, int j) { return Rn[k][bc + j]; });
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] += Cn[r0 + 8 * u][t] * rn;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) P[r0 + 8 * u][c] = oldv[u] - acc[u];
+    for (int r = 0; r < 4; ++r) P[br + gj_lrow(r)][bc + gj_lcol()] = oldv[r] - acc[0][r];
   }
   __syncthreads();
   if constexpr (!(ACMI_GJ_PROBE & 4)) pivot_inverse(P, Q);
@@ -370,7 +384,6 @@ __global__ __launch_bounds__(256) void gj_step_kernel(MatSet s, double* ws, int 
   const double* M = gj_in(s, mi, step, ws);
   double* Mo = gj_out(s, mi, step, ws);
   const double* PIk = ws + s.pi_off[mi] + (step & 1) * GJB * GJB;
-  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
   // every load issued up front, then the LDS stores: the old values of the
   // non-pivot outputs, Pinv_k, the old pivot columns of the rows (Cs) and the
   // pivot rows over the tile's columns (Rs) -- 36 independent loads per thread in
@@ -388,13 +401,17 @@ __global__ __launch_bounds__(256) void gj_step_kernel(MatSet s, double* ws, int 
   // out of range are not stored, the pivot rows / columns take Rrow' / Pinv, and
   // the Rrow' sums of the pivot and padding columns are not formed -- so the
   // compiler cannot turn a select into a branch that waits for its load)
+  // wave w: output quadrant (rows 32 (w >> 1), columns 32 (w & 1)) as 2 x 2
+  // blocks of 16 x 16 (block u: rows + 16 (u >> 1), columns + 16 (u & 1))
+  const int w = threadIdx.x >> 6, qr = 32 * (w >> 1), qc = 32 * (w & 1);
+  auto out_i = [&](int u, int r) { return i0 + qr + 16 * (u >> 1) + gj_lrow(r); };
+  auto out_j = [&](int u) { return j0 + qc + 16 * (u & 1) + gj_lcol(); };
   double old[4][4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int i = min(i0 + ty + 16 * a, np - 1);
+  for (int u = 0; u < 4; ++u)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) old[a][b] = M[(long long)i * np + min(j0 + tx + 16 * b, np - 1)];
-  }
+    for (int r = 0; r < 4; ++r)
+      old[u][r] = M[(long long)min(out_i(u, r), np - 1) * np + min(out_j(u), np - 1)];
   const bool rows_below = i0 >= kb + GJB, cols_left = j0 + 64 <= kb;
   double pv[GJB * GJB / 256], cv[64 * GJB / 256], rv[64 * GJB / 256];
 #pragma unroll
@@ -424,64 +441,55 @@ __global__ __launch_bounds__(256) void gj_step_kernel(MatSet s, double* ws, int 
     Rs[q][c] = rv[u];
   }
   __syncthreads();
-  {  // Rrow' in place of the pivot rows: thread (column cj, pivot rows t0 .. t0 + 7)
-    const int cj = threadIdx.x & 63, j = j0 + cj;
-    const int t0 = (threadIdx.x >> 6) * 8;
+  if constexpr (ACMI_GJ_PROBE & 16) {  // tiles stop after their staging
+    if (Pv[1][1] == 12345.0) Mo[0] = Cs[2][2] + Rs[3][3] + old[0][0];
+    return;
+  }
+  {  // Rrow' = Pinv_k M_k[kb.., j] in place of the pivot rows: wave w, columns 16 w ..
+    f64x4 acc[2];  // row blocks 0, 16
+    gj_mfma32(acc, [&](int u, int i, int k) { return Pv[16 * u + i][k]; },
+              [&](int, int k, int j) { return Rs[k][16 * w + j]; });
+    const int cj = 16 * w + gj_lcol(), j = j0 + cj;
     const bool jcol = j < np && !(j >= kb && j < kb + GJB);
-    double acc[8];
+    double v[2][4];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) acc[t] = 0.0;
-    if (jcol) {
-#pragma unroll 8
-      for (int q = 0; q < GJB; ++q) {
-        const double cq = Rs[q][cj];
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int t = 0; t < 8; ++t) acc[t] += Pv[t0 + t][q] * cq;
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * u + gj_lrow(r);
+        // pivot columns: Rrow' = Pinv; padding columns: never used
+        v[u][r] = jcol ? acc[u][r] : (j < np ? Pv[t][j - kb] : 0.0);
       }
-    } else if (j < np) {  // pivot columns: Rrow' = Pinv
-#pragma unroll
-      for (int t = 0; t < 8; ++t) acc[t] = Pv[t0 + t][j - kb];
-    }
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < 8; ++t) Rs[t0 + t][cj] = acc[t];
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Rs[16 * u + gj_lrow(r)][cj] = v[u][r];
   }
   __syncthreads();
-  // 4x4 outputs per thread, register-blocked: per pivot column t, 4 values of
-  // Ccol and 4 of Rrow' feed 16 FMAs
-  double acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
-#pragma unroll 8
-  for (int t = 0; t < GJB; ++t) {
-    double cv[4], rv[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) cv[a] = Cs[ty + 16 * a][t];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) rv[b] = Rs[t][tx + 16 * b];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] += cv[a] * rv[b];
+  if constexpr (ACMI_GJ_PROBE & 32) {  // tiles stop after Rrow'
+    if (Pv[1][1] == 12345.0) Mo[0] = Cs[2][2] + Rs[3][3] + old[0][0];
+    return;
   }
+  f64x4 acc[4];  // Ccol Rrow' over the wave's quadrant
+  gj_mfma32(acc, [&](int u, int i, int k) { return Cs[qr + 16 * (u >> 1) + i][k]; },
+            [&](int u, int k, int j) { return Rs[k][qc + 16 * (u & 1) + j]; });
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int i = i0 + ty + 16 * a;
-    if (i >= np) continue;
-    const bool ipiv = i >= kb && i < kb + GJB;
+  for (int u = 0; u < 4; ++u) {
+    const int jj = out_j(u);
+    if (jj >= np) continue;
+    const bool jpiv = jj >= kb && jj < kb + GJB;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int jj = j0 + tx + 16 * b;
-      if (jj >= np) continue;
-      const bool jpiv = jj >= kb && jj < kb + GJB;
+    for (int r = 0; r < 4; ++r) {
+      const int i = out_i(u, r);
+      if (i >= np) continue;
+      const bool ipiv = i >= kb && i < kb + GJB;
       double v;
       if (ipiv) {  // pivot rows: Pinv M_kj; the pivot block -Pinv
-        const double r = Rs[i - kb][tx + 16 * b];
-        v = jpiv ? -r : r;
+        const double rr = Rs[i - kb][jj - j0];
+        v = jpiv ? -rr : rr;
       } else {     // pivot columns: M_ik Pinv; the rest M_ij - M_ik Pinv M_kj
-        v = jpiv ? acc[a][b] : old[a][b] - acc[a][b];
+        v = jpiv ? acc[u][r] : old[u][r] - acc[u][r];
       }
       Mo[(long long)i * np + jj] = v;
     }
