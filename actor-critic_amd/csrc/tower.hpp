@@ -84,6 +84,72 @@ __device__ __forceinline__ void tow_put(char* img, int p, int x, int ch, float v
   *reinterpret_cast<_Float16*>(img + (eh ^ (2 * C))) = l;
 }
 
+// conv1's epilogue addressing (C = 32, S = 2, swizzle by pixel index): for the
+// row p = 32 T + tow_row(R, lane) of row tile T, the h element of channel col
+// lies at T * 4096 + 128 (R & 3) + 1024 (R >> 2) + lv[k(R)] with the lane part
+// lv[k] = 512 hl + 2 (col & 7) + (16 ((col >> 3) ^ 2 hl) ^ 16 kb(k)), because
+// (p / 2) & 7 = ((R >> 1) & 1) | hl << 1 | ((R >> 2) & 1) << 2 for every T; the
+// l element XOR 64.  So a row costs no address arithmetic: the four XOR variants
+// are formed once, the row's constant lands in the ds_write offset field (and in
+// the buffer store's for the global copy: 128 (R & 3) + 1024 (R >> 2) < 4096).
+static_assert(ACMI_TOW_PSWZ == 1, "Tow1Addr assumes the pixel-index swizzle");
+struct Tow1Addr {
+  int lh[4], ll[4];  // h / l lane parts of the 4 XOR variants
+  int go;            // lane part of the global byte offset: 512 hl + 4 col
+  __device__ explicit Tow1Addr(int lane) {
+    const int col = lane & 31, hl = lane >> 5;
+    const int x = 512 * hl + 2 * (col & 7) + 16 * ((col >> 3) ^ (hl << 1));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      lh[k] = x ^ (16 * ((k & 1) | ((k >> 1) << 2)));
+      ll[k] = lh[k] ^ 64;
+    }
+    go = 512 * hl + 4 * col;
+  }
+};
+template <int R>
+constexpr int tow1_roff() { return 128 * (R & 3) + 1024 * (R >> 2); }  // bytes, the lane-independent row part
+template <int R>
+constexpr int tow1_k() { return ((R >> 1) & 1) | (((R >> 2) & 1) << 1); }
+// tow_put<32, 2> of row tile T's element R (img: the a1 image)
+template <int R>
+__device__ __forceinline__ void tow1_put(char* img, int T, const Tow1Addr& ad, float v, float s) {
+  const _Float16 h = (_Float16)(v * s);
+  const _Float16 l = (_Float16)fmaf(v, s, -(float)h);
+  char* base = img + T * 4096;
+  *reinterpret_cast<_Float16*>(base + ad.lh[tow1_k<R>()] + tow1_roff<R>()) = h;
+  *reinterpret_cast<_Float16*>(base + ad.ll[tow1_k<R>()] + tow1_roff<R>()) = l;
+}
+
+// conv2's epilogue addressing (C = 64, S = 1): row p = 32 T + tow_row(R, lane),
+// column c: (p & 15) = (R & 3) | hl << 2 | ((R >> 2) & 1) << 3, so the h element
+// lies at T * 8192 + 256 (R & 3) + 2048 (R >> 2) + lh[k(R)] with lh[k] =
+// 1024 hl + 2 (c & 7) + (16 ((c >> 3) ^ 4 hl) ^ 16 kr(k)); the l element (XOR
+// 128) is the variant with kr's bit 3 flipped, lh[k ^ 4].
+struct Tow2Addr {
+  int lh[8];
+  int go;  // lane part of the global byte offset: 1024 hl + 4 c
+  __device__ Tow2Addr(int lane, int c) {
+    const int hl = lane >> 5;
+    const int x = 1024 * hl + 2 * (c & 7) + 16 * ((c >> 3) ^ (hl << 2));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) lh[k] = x ^ (16 * ((k & 3) | ((k >> 2) << 3)));
+    go = 1024 * hl + 4 * c;
+  }
+};
+template <int R>
+constexpr int tow2_roff() { return 256 * (R & 3) + 2048 * (R >> 2); }
+template <int R>
+constexpr int tow2_k() { return (R & 3) | (((R >> 2) & 1) << 2); }
+template <int R>
+__device__ __forceinline__ void tow2_put(char* img, int T, const Tow2Addr& ad, float v, float s) {
+  const _Float16 h = (_Float16)(v * s);
+  const _Float16 l = (_Float16)fmaf(v, s, -(float)h);
+  char* base = img + T * 8192;
+  *reinterpret_cast<_Float16*>(base + ad.lh[tow2_k<R>()] + tow2_roff<R>()) = h;
+  *reinterpret_cast<_Float16*>(base + ad.lh[tow2_k<R>() ^ 4] + tow2_roff<R>()) = l;
+}
+
 // a1 / a2 to global memory: read again only by the update, after the rollout
 #ifndef ACMI_TOW_NT
 #define ACMI_TOW_NT 1
@@ -94,6 +160,15 @@ struct TowOut {  // one image's a1 / a2 in global memory as a buffer (SGPR base,
       : rs(__builtin_amdgcn_make_buffer_rsrc(base, (short)0, nfloats * 4, 0x00020000)) {}
   __device__ __forceinline__ void store(int i, float v) const {
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, 4 * i, 0, ACMI_TOW_NT ? 2 : 0);  // aux 2: nt
+  }
+  // at byte offset vo (lane part) + IMM (compile time: the instruction's offset
+  // field below 4096, else the scalar offset)
+  template <int IMM>
+  __device__ __forceinline__ void store_imm(int vo, float v) const {
+    if constexpr (IMM < 4096)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, vo + IMM, 0, ACMI_TOW_NT ? 2 : 0);
+    else
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, vo, IMM, ACMI_TOW_NT ? 2 : 0);
   }
 };
 // Prepared weights (acmi_conv_prepare): conv1/conv2/conv3 weights split once
@@ -383,14 +458,17 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     uint32_t* mg = m1g ? m1g + img * st * 400 : nullptr;
     // one row of the tile: returns the ReLU' ballot (bit = lane: the low word row
     // p of the lower half's pixel, the high word the upper half's)
-    auto emit1 = [&](int p, float v) -> unsigned long long {
+    const Tow1Addr ad(lane);
+    // row R of row tile T (pixel 32 T + tow_row(R, lane))
+    auto emit1 = [&](auto RC, int T, float v) -> unsigned long long {
+      constexpr int R = decltype(RC)::value;
       if constexpr (ACMI_TOW_PROBE & 16) {  // probe: no conv1 epilogue (one store keeps acc live)
-        if (v == 12345.f) g.store(p, v);
+        if (v == 12345.f) g.store(T, v);
         return 0;
       }
       v = fmaxf(__builtin_fmaf(v, inv1, bias), 0.f);
-      tow_put<32, 2>(a1L, p, ACMI_TOW_PSWZ ? 0 : p % 20, col, v, sa1);
-      if constexpr (!(ACMI_TOW_PROBE & 4)) g.store(p * 32 + col, v);
+      tow1_put<R>(a1L, T, ad, v, sa1);
+      if constexpr (!(ACMI_TOW_PROBE & 4)) g.store_imm<tow1_roff<R>()>(T * 4096 + ad.go, v);
       return __ballot(v > 0.f);
     };
     // the tile's ReLU' words gathered by v_writelane (lane j: the tile's row j) and
@@ -400,7 +478,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       uint32_t mw = 0;
       tow_static_for<0, 16>([&](auto R) {  // rows < 384
         constexpr int r = decltype(R)::value;
-        mw = tow_mword<r>(mw, emit1(32 * tile_of(u) + tow_row(r, lane), h0[u][r] + acc[u][r]));
+        mw = tow_mword<r>(mw, emit1(R, tile_of(u), h0[u][r] + acc[u][r]));
       });
       if (!(ACMI_TOW_PROBE & 4) && mg && lane < 32) mg[32 * tile_of(u) + lane] = mw;
     }
@@ -416,7 +494,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       tow_static_for<0, 8>([&](auto R) {
         constexpr int r = decltype(R)::value;
         const int m = tow_row(r, lane);
-        mw = tow_mword<r>(mw, emit1(384 + m, acc[3][r] + scr12[m * 32 + col]));
+        mw = tow_mword<r>(mw, emit1(R, 12, acc[3][r] + scr12[m * 32 + col]));
       });
       if (!(ACMI_TOW_PROBE & 4) && mg && lane < 16) mg[384 + lane] = mw;
     }
@@ -487,11 +565,14 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     const TowOut g(a2g + img * st * 5184, 5184);
     uint32_t* mg = m2g ? m2g + img * st * 162 : nullptr;
     // (act: the lane's row exists; the ballot runs on every lane)
-    auto emit = [&](int p, float v, bool act) -> unsigned long long {
+    const Tow2Addr ad(lane, c);
+    // row R of row tile T (pixel 32 T + tow_row(R, lane))
+    auto emit = [&](auto RC, int T, float v, bool act) -> unsigned long long {
+      constexpr int R = decltype(RC)::value;
       v = fmaxf(__builtin_fmaf(v, inv2, bias), 0.f);
       if (act) {
-        tow_put<64, 1>(imgL, p, ACMI_TOW_PSWZ ? 0 : p % 9, c, v, sa2);
-        if constexpr (!(ACMI_TOW_PROBE & 4)) g.store(p * 64 + c, v);
+        tow2_put<R>(imgL, T, ad, v, sa2);
+        if constexpr (!(ACMI_TOW_PROBE & 4)) g.store_imm<tow2_roff<R>()>(T * 8192 + ad.go, v);
       }
       return __ballot(act && v > 0.f);
     };
@@ -499,7 +580,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       uint32_t mw = 0;
       tow_static_for<0, 16>([&](auto R) {  // rows 0..63 are all valid
         constexpr int r = decltype(R)::value;
-        mw = tow_mword<r>(mw, emit(32 * rtf + tow_row(r, lane), hF[r] + accF[r], true));
+        mw = tow_mword<r>(mw, emit(R, rtf, hF[r] + accF[r], true));
       });
       if (!(ACMI_TOW_PROBE & 4) && mg && lane < 32) mg[2 * (32 * rtf + lane) + ct] = mw;
     }
@@ -509,7 +590,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
         constexpr int r = decltype(R)::value;
         const int m = tow_row(r, lane);
         const bool act = m < 17;
-        mw = tow_mword<r>(mw, emit(64 + m, act ? accH[r] + scr[(ct * 17 + m) * 32 + col] : 0.f, act));
+        mw = tow_mword<r>(mw, emit(R, 2, act ? accH[r] + scr[(ct * 17 + m) * 32 + col] : 0.f, act));
       });
       if (!(ACMI_TOW_PROBE & 4) && mg && lane < 17) mg[2 * (64 + lane) + ct] = mw;
     }

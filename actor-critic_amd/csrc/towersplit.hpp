@@ -117,17 +117,22 @@ __device__ __forceinline__ void tower_part_body(int j, const float* b1, const fl
     const TowOut g(a1g + img * st * 12800, 12800);
     uint32_t* mg = m1g ? m1g + img * st * 400 : nullptr;
     const int own_lo = 20 * split_a1_lo(j) - 40 * j, own_hi = 20 * (split_a1_hi(j) + 1) - 40 * j;  // local [lo, hi)
-    auto emit1 = [&](int q, float v) -> unsigned long long {
+    const Tow1Addr ad(lane);
+    // row R of local row tile u (local pixel q = 32 u + tow_row(R, lane))
+    auto emit1 = [&](auto RC, int u, float v) -> unsigned long long {
+      constexpr int R = decltype(RC)::value;
+      const int q = 32 * u + tow_row(R, lane);
       v = fmaxf(__builtin_fmaf(v, inv1, bias), 0.f);
-      tow_put<32, 2>(a1L, q, ACMI_TOW_PSWZ ? 0 : q % 20, col, v, sa1);
-      if (q >= own_lo && q < own_hi) g.store((40 * j + q) * 32 + col, v);
+      tow1_put<R>(a1L, u, ad, v, sa1);
+      if ((unsigned)(q - own_lo) < (unsigned)(own_hi - own_lo))
+        g.store_imm<tow1_roff<R>()>((40 * j + 32 * u) * 128 + ad.go, v);
       return __ballot(v > 0.f);
     };
     auto tile_out = [&](int u, auto get) {
       uint32_t mw = 0;
       tow_static_for<0, 16>([&](auto R) {
         constexpr int r = decltype(R)::value;
-        mw = tow_mword<r>(mw, emit1(32 * u + tow_row(r, lane), get(r)));
+        mw = tow_mword<r>(mw, emit1(R, u, get(r)));
       });
       const int q = 32 * u + lane;
       if (mg && lane < 32 && q >= own_lo && q < own_hi) mg[40 * j + q] = mw;
@@ -184,6 +189,7 @@ __device__ __forceinline__ void tower_part_body(int j, const float* b1, const fl
       const TowOut g(a2g + img * st * 5184, 5184);
       uint32_t* mg = m2g ? m2g + img * st * 162 : nullptr;
       const int own_lo = 9 * split_a2_lo(j) - 9 * j, own_hi = 9 * (split_a2_hi(j) + 1) - 9 * j;
+      const Tow2Addr ad(lane, c);
       uint32_t mw = 0;
       tow_static_for<0, 16>([&](auto R) {
         constexpr int r = decltype(R)::value;
@@ -192,8 +198,9 @@ __device__ __forceinline__ void tower_part_body(int j, const float* b1, const fl
         float v = acc[r] + scr[(ct * 32 + m) * 32 + col];
         v = fmaxf(__builtin_fmaf(v, inv2, bias), 0.f);
         if (act) {
-          tow_put<64, 1>(a2L, m, ACMI_TOW_PSWZ ? 0 : m % 9, c, v, sa2);
-          if (m >= own_lo && m < own_hi) g.store((9 * j + m) * 64 + c, v);
+          tow2_put<r>(a2L, 0, ad, v, sa2);
+          if ((unsigned)(m - own_lo) < (unsigned)(own_hi - own_lo))
+            g.store_imm<tow2_roff<r>()>(9 * j * 256 + ad.go, v);
         }
         mw = tow_mword<r>(mw, __ballot(act && v > 0.f));
       });

@@ -13,7 +13,7 @@ tail -1 "$out/bench_default.json" | cut -c1-400
 cd /tmp && export TMPDIR=/tmp
 echo "=== rocprofv3 stats"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof" -o prof --output-format csv \
-  -- python3 "$root/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$out/prof_bench.json" 2> "$out/prof.err" || exit $?
+  -- python3 "$root/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-configs2 > "$out/prof_bench.json" 2> "$out/prof.err" || exit $?
 f=$(find "$out/prof" -name '*kernel_stats.csv' | head -1)
 cp "$f" "$out/kernel_stats.csv"
 python3 "$root/scripts/prof_summary.py" "$out/kernel_stats.csv" "rocprofv3 --kernel-trace --stats, bench.py --steps 10 --warmup 2 --no-cpu-baseline (12 iterations), ACKTR 512x20, 1x MI355X" 12 > "$out/summary.md"
@@ -22,6 +22,6 @@ cp "$trace" "$out/kernel_trace.csv"
 echo "=== pmc"
 for pmc in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $pmc -d "$out/pmc/$pmc" -o "$pmc" --output-format csv \
-    -- python3 "$root/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$out/pmc_$pmc.log" 2>&1 || exit $?
+    -- python3 "$root/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-configs2 > "$out/pmc_$pmc.log" 2>&1 || exit $?
 done
 exit 0
