@@ -794,9 +794,38 @@ __device__ __forceinline__ void finalize_wgrad_body(const WgradDesc& d, int bx, 
   }
 }
 
+// Gradient outputs (d.astat == nullptr) of a partial with few chunks (<= 8): one
+// thread per output instead of 32 outputs x 8 chunk groups per block (7 of the 8
+// groups idle at one chunk: the fc4 gradient's 803 K outputs were 25 K blocks).
+// The same sums in the same order: group g holds chunk g alone (0 + p[g]), the
+// groups added in order from 0.
+__device__ __forceinline__ void finalize_grad_thread_body(const WgradDesc& d, int bx) {
+  const int K = d.I;
+  const long long idx = (long long)bx * 256 + threadIdx.x;
+  if (idx >= (long long)(K + 1) * d.cout) return;
+  const int a = (int)(idx / d.cout), n = (int)(idx - (long long)a * d.cout);
+  const float* p = d.part + (long long)(a < K ? a : d.I) * d.J + d.kp + n;
+  const long long cs = (long long)(d.I + 1) * d.J;
+  float v[kFinGroups];
+#pragma unroll
+  for (int g = 0; g < kFinGroups; ++g) v[g] = p[(long long)(g < d.nchunk ? g : 0) * cs];
+  float s = 0.f;
+#pragma unroll
+  for (int g = 0; g < kFinGroups; ++g) s += g < d.nchunk ? 0.f + v[g] : 0.f;
+  if (a < K) s *= d.wscale;
+  if (n < d.nsplit) d.gradA[(long long)a * d.nsplit + n] = s;
+  else d.gradB[(long long)a * (d.cout - d.nsplit) + (n - d.nsplit)] = s;
+}
+__device__ __forceinline__ bool fin_thread_ok(const WgradDesc& d) { return !d.astat && d.nchunk <= kFinGroups; }
+inline int fin_blocks(const WgradDesc& d) {
+  const long long total = (long long)(d.I + 1) * d.cout + (d.astat ? (long long)(d.I + 1) * (d.I + 1) : 0);
+  return (int)(!d.astat && d.nchunk <= kFinGroups ? cdiv(total, 256) : cdiv(total, 32));
+}
+
 __global__ __launch_bounds__(256) void finalize_wgrad_kernel(WgradDesc d) {
   __shared__ float red[kFinGroups][32];
-  finalize_wgrad_body(d, blockIdx.x, red);
+  if (fin_thread_ok(d)) finalize_grad_thread_body(d, blockIdx.x);
+  else finalize_wgrad_body(d, blockIdx.x, red);
 }
 
 // The A factor of a split-K wgrad partial ((K+1)^2, symmetric): one block per
@@ -874,8 +903,12 @@ __global__ __launch_bounds__(256) void finalize_wgrad_multi_kernel(WgradSet S) {
   while (k + 1 < S.n && (int)blockIdx.x >= S.t[k + 1].blk0) ++k;
   const WgradTask& T = S.t[k];
   const int b = blockIdx.x - T.blk0;
-  if (T.kind == 0) finalize_wgrad_body(T.d, b, red);
-  else finalize_afactor_body(T.d, T.ntile, b, tr);
+  if (T.kind == 0) {
+    if (fin_thread_ok(T.d)) finalize_grad_thread_body(T.d, b);
+    else finalize_wgrad_body(T.d, b, red);
+  } else {
+    finalize_afactor_body(T.d, T.ntile, b, tr);
+  }
 }
 
 // G factor: part [nchunk][I+1][J] (I == J == n, no colsum row used); one
@@ -941,7 +974,8 @@ struct CovSet {
   int blocks = 0;
   CovTask t[kCovTasks];
   void add(const float* part, int nchunk, int n_, int sub, float* out, int rows, int kind, int a = 0) {
-    const int nb = kind == 0 ? cdiv(sub * sub, 256) : kind == 1 ? cdiv(sub * sub, 4) : 1;
+    const int nt = cdiv(sub, 32);
+    const int nb = kind == 0 ? cdiv(sub * sub, 256) : kind == 1 ? cdiv(sub * sub, 4) : kind == 3 ? nt * (nt + 1) / 2 : 1;
     t[n++] = CovTask{part, out, nchunk, n_, sub, rows, kind, a, blocks};
     blocks += nb;
   }
@@ -952,6 +986,36 @@ __global__ __launch_bounds__(256) void finalize_cov_multi_kernel(CovSet S) {
   const CovTask& T = S.t[k];
   const int b = blockIdx.x - T.blk0;
   const long long cs = (long long)(T.n + 1) * T.n;
+  if (T.kind == 3) {
+    // kind 0's sums on 32 x 32 upper-triangle tiles, both halves written by
+    // coalesced rows through an LDS transpose (kind 0's mirror store is a 4-byte
+    // scatter with stride sub: the 512-wide G factor's half)
+    __shared__ float tr[32][33];
+    const int ntile = (T.sub + 31) / 32;
+    int t = b, ta = 0;
+    while (t >= ntile - ta) t -= ntile - ta, ++ta;
+    const int tb = ta + t;
+    const int c = threadIdx.x & 31, r0 = threadIdx.x >> 5;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int r = r0 + 8 * it;
+      const int a = 32 * ta + r, cc = 32 * tb + c;
+      float v = 0.f;
+      if (a < T.sub && cc < T.sub && a <= cc) {
+        v = chunk_sum(T.part + (long long)a * T.n + cc, T.nchunk, cs) * (1.0f / (float)T.rows);
+        T.out[a * T.sub + cc] = v;
+      }
+      tr[r][c] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int r = r0 + 8 * it;
+      const int bb = 32 * tb + r, a = 32 * ta + c;
+      if (a < T.sub && bb < T.sub && a < bb) T.out[bb * T.sub + a] = tr[c][r];
+    }
+    return;
+  }
   if (T.kind == 0) {
     const int idx = b * 256 + threadIdx.x;
     if (idx >= T.sub * T.sub) return;
@@ -1208,10 +1272,9 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
   // many (the heads' 80): one output per 8 threads, chunk groups in parallel
   const bool tiles = astat && nc <= kFinGroups;
   WgradDesc d{part, nc, I, J, kp, cout, gradA, nsplit, gradB, tiles ? nullptr : astat, (int)rows, wscale};
-  const long long total = (long long)(K + 1) * cout + (d.astat ? (long long)(K + 1) * (K + 1) : 0);
   if (used) *used = pl.floats;
   if (defer) {
-    defer->add(d, 0, 0, (int)cdiv(total, 32));
+    defer->add(d, 0, 0, fin_blocks(d));
     if (tiles) {
       d.astat = astat;
       const int nt = cdiv(K + 1, 32);
@@ -1220,7 +1283,7 @@ static int wgrad_layer(const Src& src, int K, long long rows, const float* dy,
     ACMI_LAUNCH_CHECK("wgrad_layer");
     return ACMI_OK;
   }
-  hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(cdiv(total, 32)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(finalize_wgrad_kernel, dim3(fin_blocks(d)), dim3(256), 0, s, d);
   if (tiles) {
     d.astat = astat;
     const int nt = cdiv(K + 1, 32);
@@ -1265,7 +1328,7 @@ static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
   }
   if (used) *used = (long long)nc * (np + 1) * np;
   if (defer) {
-    defer->add(part, nc, np, sub, out, (int)rows, nc <= 64 ? 0 : 1);
+    defer->add(part, nc, np, sub, out, (int)rows, nc <= 64 ? (sub >= 64 ? 3 : 0) : 1);
     if (out_v) defer->add(part, nc, np, 1, out_v, (int)rows, 2, v_index);
     ACMI_LAUNCH_CHECK("gcov_layer");
     return ACMI_OK;
@@ -1488,7 +1551,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
     const long long rows = 400LL * B;
     WgradDesc d{wpart_c1, conv1_afactor_fused_chunks(rows), 256, 32, 0, 32, grads + L.off[0], 32,
                 nullptr, nullptr, (int)rows, 1.0f / 255.0f};
-    fin.add(d, 0, 0, (int)cdiv(257 * 32, 32));
+    fin.add(d, 0, 0, fin_blocks(d));
   }
   float* part = ws;
   // need: the layer's partial floats (its plan), checked here so that a layer

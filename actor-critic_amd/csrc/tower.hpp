@@ -161,14 +161,11 @@ struct TowOut {  // one image's a1 / a2 in global memory as a buffer (SGPR base,
   __device__ __forceinline__ void store(int i, float v) const {
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, 4 * i, 0, ACMI_TOW_NT ? 2 : 0);  // aux 2: nt
   }
-  // at byte offset vo (lane part) + IMM (compile time: the instruction's offset
-  // field below 4096, else the scalar offset)
+  // at byte offset vo (lane part) + IMM (compile time, as the scalar offset: a
+  // vo + IMM sum was formed by VALU ORs per row instead of the offset field)
   template <int IMM>
   __device__ __forceinline__ void store_imm(int vo, float v) const {
-    if constexpr (IMM < 4096)
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, vo + IMM, 0, ACMI_TOW_NT ? 2 : 0);
-    else
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, vo, IMM, ACMI_TOW_NT ? 2 : 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, vo, IMM, ACMI_TOW_NT ? 2 : 0);
   }
 };
 // Prepared weights (acmi_conv_prepare): conv1/conv2/conv3 weights split once
