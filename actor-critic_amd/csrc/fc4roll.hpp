@@ -61,26 +61,30 @@ struct Fc4Commit {
   acmi_env_state_t st;
   int B;
 };
+// CT: 32-column tiles per wave (2; 1 at small batches: twice the blocks, half
+// the MFMA chain per wave)
+template <int CT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
 void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w4p, int nz, int chunk_steps,
                      float* part, const unsigned* hdr, Fc4Commit cm) {
   if (cm.B > 0 && blockIdx.x == 0) env_commit_pending(cm.st, cm.pend, cm.B);
   constexpr int D = kFc4Depth, NSLOT = D + 1;
+  constexpr int NG = 512 / (128 * CT);  // column groups of 4 waves
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int z = blockIdx.x % nz, rest = blockIdx.x / nz;
-  const int rt = rest >> 1, cg = 4 * (rest & 1) + wave;
+  const int rt = rest / NG, cg = 4 * (rest % NG) + wave;  // the wave's columns 32 CT cg ..
   const int s0 = z * chunk_steps;
   const int ns = min(K / 16, s0 + chunk_steps) - s0;
   const int col = lane & 31;
   const int row = min(32 * rt + col, B - 1);
   const float* ap = a3 + (long long)row * lda + 16 * s0 + 8 * (lane >> 5);
   // fragment (step s, col tile ct, part pt): uint4 index (s * 16 + ct) * 128 + 64 pt + lane
-  const uint4* bp = reinterpret_cast<const uint4*>(w4p) + ((long long)s0 * 16 + 2 * cg) * 128 + lane;
+  const uint4* bp = reinterpret_cast<const uint4*>(w4p) + ((long long)s0 * 16 + CT * cg) * 128 + lane;
   const float sa = f16x2_scale_of_bits(hdr + kTowMaxA3);
   const float inv = 1.0f / (sa * f16x2_scale_of_bits(hdr + kTowMaxW4));  // exact
 
   float4 av[NSLOT][2];
-  uint4 bv[NSLOT][2][2];
+  uint4 bv[NSLOT][CT][2];
 #ifndef ACMI_FC4_PROBE  // timing probes (wrong results): 1 no a3 loads, 2 no W4 loads, 4 no MFMAs
 #define ACMI_FC4_PROBE 0
 #endif
@@ -95,16 +99,16 @@ void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w
     }
     const uint4* b = bp + (long long)i * 16 * 128;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < CT; ++t)
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt) {
         if constexpr (ACMI_FC4_PROBE & 2) bv[slot][t][pt] = make_uint4(i, t, pt, lane);
         else bv[slot][t][pt] = b[t * 128 + 64 * pt];
       }
   };
-  f32x16 acc[2];
+  f32x16 acc[CT];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < CT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 #pragma unroll
@@ -121,7 +125,7 @@ void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w
         f16x8 a[2];
         split2x8(av[sl][0], av[sl][1], sa, a[0], a[1]);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < CT; ++t) {
           const f16x8 b[2] = {as_f16x8(bv[sl][t][0]), as_f16x8(bv[sl][t][1])};
           if constexpr (ACMI_FC4_PROBE & 4) acc[t][0] += (float)a[0][0] * (float)b[1][1] + (float)a[1][2];
           else acc[t] = mfma_x2(a, b, acc[t]);
@@ -129,9 +133,9 @@ void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w
       }
     }
   }
-  float* out = part + (long long)z * (B + 1) * 512 + 64 * cg + col;
+  float* out = part + (long long)z * (B + 1) * 512 + 32 * CT * cg + col;
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < CT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rr = 32 * rt + tow_row(r, lane);
@@ -145,8 +149,16 @@ inline bool launch_fc4_roll(const float* a3, long long lda, int B, int K, const 
                             float* part, const unsigned* hdr, hipStream_t s, Fc4Commit cm = Fc4Commit{}) {
   if (chunk % 16 || K % 16 || (lda % 4) || ((uintptr_t)a3 % 16)) return false;
   const int cs = chunk / 16;
-  const dim3 grid(nz * ((B + 31) / 32) * 2), blk(256);
-  hipLaunchKernelGGL(fc4_roll_kernel, grid, blk, 0, s, a3, lda, B, K, w4p, nz, cs, part, hdr, cm);
+#ifndef ACMI_FC4_SMALL_CT  // column tiles per wave at batches <= 64
+#define ACMI_FC4_SMALL_CT 1
+#endif
+  if (B <= 64 && ACMI_FC4_SMALL_CT == 1) {
+    const dim3 grid(nz * ((B + 31) / 32) * 4), blk(256);
+    hipLaunchKernelGGL(fc4_roll_kernel<1>, grid, blk, 0, s, a3, lda, B, K, w4p, nz, cs, part, hdr, cm);
+  } else {
+    const dim3 grid(nz * ((B + 31) / 32) * 2), blk(256);
+    hipLaunchKernelGGL(fc4_roll_kernel<2>, grid, blk, 0, s, a3, lda, B, K, w4p, nz, cs, part, hdr, cm);
+  }
   return true;
 }
 
