@@ -516,7 +516,14 @@ typedef struct acmi_rollout_io {
    * a1..a3 / m1..m3 rows (image stride next_act_stride) -- the tower launch
    * of the next step is then skipped by passing tower_done = 1 with it.
    * Needs the fused tower (x3 gemm mode, prepared weights, 16-byte aligned
-   * obs_out / out_stride).  Bit-identical to the unfused steps. */
+   * obs_out / out_stride).  Bit-identical to the unfused steps.
+   * At B <= 64 the fused step splits each image's tower over 7 workgroups;
+   * their env step then leaves the post-step env states pending in acts->ws
+   * (after the fc4 slabs; acmi_forward_ws_floats(B) reserves them) and the
+   * NEXT step's fc4 launch commits them into `state`: consecutive fused steps
+   * of a rollout must pass the same acts->ws, and a rollout must end with an
+   * unfused step (next_acts = NULL, tower_done = 1), whose launch commits the
+   * last pending states before its own env step. */
   int tower_done;
   const struct acmi_acts* next_acts;
   int64_t next_act_stride;
