@@ -152,7 +152,10 @@ inline bool launch_fc4_roll(const float* a3, long long lda, int B, int K, const 
 #ifndef ACMI_FC4_SMALL_CT  // column tiles per wave at batches <= 64
 #define ACMI_FC4_SMALL_CT 1
 #endif
-  if (B <= 64 && ACMI_FC4_SMALL_CT == 1) {
+#ifndef ACMI_FC4_CT1_MAXB  // largest batch with one column tile per wave
+#define ACMI_FC4_CT1_MAXB 64
+#endif
+  if (B <= ACMI_FC4_CT1_MAXB && ACMI_FC4_SMALL_CT == 1) {
     const dim3 grid(nz * ((B + 31) / 32) * 4), blk(256);
     hipLaunchKernelGGL(fc4_roll_kernel<1>, grid, blk, 0, s, a3, lda, B, K, w4p, nz, cs, part, hdr, cm);
   } else {
