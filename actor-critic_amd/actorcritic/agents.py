@@ -21,6 +21,7 @@ kept for hosts where launch overhead is not hidden.
 
 import ctypes
 import os
+import time
 
 from abc import ABCMeta, abstractmethod
 
@@ -200,7 +201,9 @@ class MultiEnvAgent(Agent):
             self._bufs = _RolloutBuffers(eng, N, T)
         rb = self._bufs
         if rb.bad_event is not None:  # deferred NaN-logit check of the previous rollout
+            t_wait = time.perf_counter()
             rb.bad_event.synchronize()
+            self.last_sync_wait = time.perf_counter() - t_wait  # (bench.py's host-time split)
             if int(rb.bad_host[0]) > 0:
                 eng.check_bad_rows()
         if self._observations is None:

@@ -223,8 +223,12 @@ def _measure(args, N, T, A, algo, games, steps, warmup, prof_site=None):
         gc.collect()
         gc.disable()
         t0 = time.perf_counter()
+        host = []  # host time per iteration minus its wait on the previous rollout's event
         for k in range(steps):
+            th = time.perf_counter()
+            agent.last_sync_wait = 0.0
             iteration(s, marks[k])
+            host.append(time.perf_counter() - th - getattr(agent, 'last_sync_wait', 0.0))
             inv_flags.append(bool(getattr(optimizer, 'last_flags', (0, 0, 0))[2]) if acktr else False)
         torch.cuda.synchronize()
         parallel.barrier()
@@ -244,7 +248,8 @@ def _measure(args, N, T, A, algo, games, steps, warmup, prof_site=None):
     return dict(value=N * T * steps * world / elapsed, ms_per_step=1e3 * elapsed / steps, elapsed=elapsed,
                 update_ms=mean(upd_ms), update_ms_inverse_iters=mean([u for u, f in zip(upd_ms, inv_flags) if f]),
                 update_ms_plain_iters=mean([u for u, f in zip(upd_ms, inv_flags) if not f]),
-                rollout_ms=mean(roll_ms), comm_ms=comm_ms_max, comm_bytes=comm_bytes, comm_n=comm_n,
+                rollout_ms=mean(roll_ms), host_ms=1e3 * mean(host[1:] or host), comm_ms=comm_ms_max,
+                comm_bytes=comm_bytes, comm_n=comm_n,
                 prof_ms=tot_ms.value, prof_n=cnt.value)
 
 
@@ -298,7 +303,8 @@ def run(args):
               'num_actions': 4, 'forward': 'f32', 'steps': args.configs2_steps, 'warmup': max(5, args.warmup),
               'value': c2r['value'], 'unit': 'env-steps/s', 'ms_per_step': c2r['ms_per_step'],
               'update_ms': c2r['update_ms'], 'update_ms_inverse_iters': c2r['update_ms_inverse_iters'],
-              'update_ms_plain_iters': c2r['update_ms_plain_iters'], 'rollout_ms': c2r['rollout_ms']}
+              'update_ms_plain_iters': c2r['update_ms_plain_iters'], 'rollout_ms': c2r['rollout_ms'],
+              'host_ms_per_step': c2r['host_ms']}
 
     # dominant kernel: conv2 weight gradient fused with the K-FAC A factor,
     # [P;1]^T [P | dY] over the M*81 conv2 output pixels, P = 4x4x32 patches.
@@ -382,6 +388,9 @@ def run(args):
                 'parallelism': 'dp{}'.format(world)},
             'update_ms': r['update_ms'], 'update_ms_inverse_iters': r['update_ms_inverse_iters'],
             'update_ms_plain_iters': r['update_ms_plain_iters'], 'rollout_ms': r['rollout_ms'],
+            # host time per iteration of the Python loop (ctypes launches, graph
+            # evaluation): below ms_per_step the GPU, not the host, sets the pace
+            'host_ms_per_step': r['host_ms'],
             # communication: compute-stream stall on the per-update all-reduce
             # (NetEngine.comm_timing; max over ranks), bytes summed per update
             'allreduce_ms': r['comm_ms'] if world > 1 else 0.0, 'allreduce_bytes': r['comm_bytes'],
