@@ -132,61 +132,6 @@ def test_relu_masks_written_and_bit_identical(lib, cuda, use_prep, B):
         assert torch.equal(a, b)
 
 
-def test_backward_and_stats_in_reduced_workspaces_bit_identical(lib, cuda):
-    """acmi_backward / acmi_kfac_output_stats with less workspace than their
-    *_ws_floats ask for: the split-K partials of the layers are then finalized in
-    several ranges (the one-launch finalize set flushed whenever the next layer's
-    plan does not fit after the others) instead of one -- the same sums, so the
-    gradients and both factor statistics are bit-identical to the full-workspace
-    run; a workspace too small for the largest single layer raises ACMI_ERR_WS."""
-    A, C3, B = 4, 32, 300
-    params = rand_params(A, C3, cuda, seed=81)
-    g = torch.Generator().manual_seed(82)
-    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
-    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
-    net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr())
-    _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), _lib.stream_handle())
-    ldh = 8
-    dhead = torch.zeros(B, ldh)
-    dhead[:, :A + 1] = torch.randn(B, A + 1, generator=g) / B
-    dhead = dhead.to(cuda)
-    z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=cuda)
-    so = (ctypes.c_int64 * 11)()
-    tot = ctypes.c_int64()
-    _lib.call('acmi_kfac_layout', A, C3, None, None, so, ctypes.byref(tot))
-    t, acts = alloc_acts(B, A, C3, cuda, masks=True)
-    _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
-              _lib.stream_handle())
-    full = int(lib.acmi_backward_ws_floats(B, A, C3))
-
-    def run(nws):
-        ws = z(nws)
-        d = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
-        bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
-        grads, astat, gstat = z(params.numel()), z(tot.value), z(tot.value)
-        _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
-                  ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), ctypes.c_void_p(ws.data_ptr()),
-                  _lib.stream_handle())
-        _lib.call('acmi_kfac_output_stats', ctypes.byref(net), B, ctypes.byref(acts), ctypes.byref(bwd),
-                  7, 0, 3, _lib.ptr(gstat), ctypes.c_void_p(ws.data_ptr()), _lib.stream_handle())
-        torch.cuda.synchronize()
-        return grads.cpu(), astat.cpu(), gstat.cpu()
-
-    ref = run(full)
-    ran = []
-    for frac in (0.7, 0.5, 0.35, 0.25):
-        try:
-            out = run(int(full * frac))
-        except _lib.AcmiError:
-            continue
-        ran.append(frac)
-        for a, b in zip(ref, out):
-            assert torch.equal(a, b), frac
-    assert ran and min(ran) < 0.7, ran
-    with pytest.raises(_lib.AcmiError):
-        run(1024)
-
-
 @pytest.mark.parametrize('C3', [32, 64])
 @pytest.mark.parametrize('fwd', ['f32', 'bf16'])
 def test_split_tower_bit_identical_to_one_block_tower(lib, cuda, C3, fwd):
