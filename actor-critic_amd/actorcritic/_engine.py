@@ -187,6 +187,11 @@ class NetEngine(object):
         from actorcritic import parallel
         self.rank = parallel.rank()
         self.world_size = parallel.world_size()
+        # the per-update exchange runs when there are ranks to exchange with -- or,
+        # test-only (ACMI_FORCE_COLLECTIVE=1 with a process group of one rank), through
+        # the same RCCL calls at world size 1, where the sum must leave every bit as is
+        self.collective = self.world_size > 1 or (
+            os.environ.get('ACMI_FORCE_COLLECTIVE') == '1' and parallel.is_initialized())
         if self.world_size > 1:  # identical initial parameters on every rank
             parallel.broadcast_(self.params)
         self.version = 0  # bumped by every parameter update (activation-cache key)
@@ -235,7 +240,7 @@ class NetEngine(object):
         net = self.net()
         _lib.call('acmi_backward', ctypes.byref(net), ctypes.c_void_p(fwd.obs.data_ptr()), OBS_BYTES, fwd.M,
                   ctypes.byref(fwd.acts.struct), ctypes.byref(st.bwd), _lib.ptr(st.grads),
-                  _lib.ptr(st.astat) if with_stats else None, _lib.ptr(st.bwd_ws), self.stream())
+                  _lib.ptr(st.astat) if with_stats else None, _lib.ptr(st.bwd_ws), st.bwd_ws.numel(), self.stream())
 
     def output_stats(self, fwd, st, seed, counter, side=None):
         """side: run on UpdateState.side()'s stream and workspace (see there)."""
@@ -243,7 +248,7 @@ class NetEngine(object):
         bwd, ws = (side.bwd, side.ws) if side is not None else (st.bwd, st.bwd_ws)
         _lib.call('acmi_kfac_output_stats', ctypes.byref(net), fwd.M, ctypes.byref(fwd.acts.struct),
                   ctypes.byref(bwd), seed, self.rank * fwd.M, counter, _lib.ptr(st.gstat), _lib.ptr(ws),
-                  self.stream())
+                  ws.numel(), self.stream())
 
     # the G chain on a side stream: '1' always, '0' never, unset: at small batches
     # (M <= CONCURRENT_STATS_ROWS), where each of its launches fills a fraction of
@@ -287,10 +292,10 @@ class NetEngine(object):
     def allreduce(self, st, with_stats):
         """Sums [grads | losses (| factor stats)] over ranks (RCCL); the 1/world scale is
         folded into the loss gradient and the factor EMA."""
-        if self.world_size > 1:
+        if self.collective:
             from actorcritic import parallel
             k = st.red.numel() if with_stats else st.n_grad_red
-            parallel.allreduce_sum_(st.red[:k])
+            parallel.allreduce_sum_(st.red[:k], force=True)
             st.loss_reduced = True
 
     def _packed(self, st):
@@ -311,7 +316,7 @@ class NetEngine(object):
         G part) computes on this one.  Returns the pending handle (None on one rank);
         allreduce_end completes ``red``."""
         st.pk_active = False
-        if self.world_size <= 1:
+        if not self.collective:
             return None
         from actorcritic import parallel
         st.loss_reduced = True
@@ -330,7 +335,7 @@ class NetEngine(object):
         """Sums the G factor stats (packed, if the prefix carried the A stats) and makes
         this stream wait for the pending prefix sum, then unpacks: ``red`` is fully
         reduced for the kernels enqueued next."""
-        if self.world_size <= 1:
+        if not self.collective:
             return
         from actorcritic import parallel
         marks = self._comm_mark() if self._comm is not None else None
@@ -340,7 +345,7 @@ class NetEngine(object):
             pk, ng, L = st.pk, st.n_grad_red, self.layout
             _lib.call('acmi_kfac_pack', L.A, L.C3, 2, ctypes.c_void_p(st.stats.data_ptr()),
                       ctypes.c_void_p(pk[ng + st.pk_na:].data_ptr()), self.stream())
-            parallel.allreduce_sum_(pk[ng + st.pk_na:])
+            parallel.allreduce_sum_(pk[ng + st.pk_na:], force=True)
             pending.wait()
             st.red[:ng].copy_(pk[:ng])
             _lib.call('acmi_kfac_unpack', L.A, L.C3, 3, ctypes.c_void_p(pk[ng:].data_ptr()),

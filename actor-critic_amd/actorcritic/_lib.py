@@ -97,9 +97,10 @@ _SIGS = {
                               c_vp, c_int, c_vp, c_vp, c_vp]),
     'acmi_backward_ws_floats': (c_i64, [c_int, c_int, c_int]),
     'acmi_backward': (c_int, [ctypes.POINTER(Net), c_vp, c_i64, c_int, ctypes.POINTER(Acts),
-                              ctypes.POINTER(Bwd), c_vp, c_vp, c_vp, c_vp]),
+                              ctypes.POINTER(Bwd), c_vp, c_vp, c_vp, c_i64, c_vp]),
     'acmi_kfac_output_stats': (c_int, [ctypes.POINTER(Net), c_int, ctypes.POINTER(Acts), ctypes.POINTER(Bwd),
-                                       c_u32, c_u32, c_u32, c_vp, c_vp, c_vp]),
+                                       c_u32, c_u32, c_u32, c_vp, c_vp, c_i64, c_vp]),
+    'acmi_debug_ws_flushes': (c_int, []),
     'acmi_kfac_ema': (c_int, [c_vp, c_vp, c_vp, c_i64, c_float, c_float, c_float, c_vp]),
     'acmi_kfac_inverse_layout': (c_int, [c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     'acmi_kfac_inverse_floats': (c_i64, [c_int, c_int]),
@@ -160,7 +161,7 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.acmi_abi_version() != 3:
+        if lib.acmi_abi_version() != 4:
             raise ImportError('libacmi ABI mismatch')
         _lib = lib
     return _lib

@@ -52,8 +52,10 @@ def init_from_env(backend=None):
     return world_size(), rank()
 
 
-def allreduce_sum_(t):
-    if world_size() > 1:
+def allreduce_sum_(t, force=False):
+    """In-place SUM over ranks; force: also with a process group of one rank (the
+    engine's ACMI_FORCE_COLLECTIVE test switch)."""
+    if world_size() > 1 or (force and is_initialized()):
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t
 

@@ -118,6 +118,87 @@ inline std::vector<char> band_needed(const BandGeom& g) {
   return need;
 }
 
+// A group from its tiles: the staged slabs are the ones the tiles use, in column
+// order; tile m goes to wave m % 8, slot m / 8 (waves w and w + 4 share a SIMD,
+// so 13..16 tiles give every SIMD 3..4 sub-tiles)
+inline BandGroup band_group_of(const BandGeom& g, const std::vector<std::pair<int, int>>& tiles) {
+  std::vector<int> used;
+  for (const auto& t : tiles) used.push_back(t.first), used.push_back(t.second);
+  std::sort(used.begin(), used.end());
+  used.erase(std::unique(used.begin(), used.end()), used.end());
+  BandGroup G;
+  G.nslab = (unsigned char)used.size();
+  G.xmask = 0;
+  for (int i = 0; i < kBandSlabs; ++i) {
+    G.base[i] = i < (int)used.size() ? 64 * used[i] : -1;
+    if (i < (int)used.size() && used[i] < g.nxs) G.xmask |= (unsigned char)(1u << i);
+  }
+  for (int w = 0; w < 8; ++w)
+    for (int t = 0; t < 2; ++t) G.ra[w][t] = G.cb[w][t] = -1, G.tile[w][t] = -1;
+  G.csown = 0;
+  G.pad = 0;
+  auto idx = [&](int slab) { return (int)(std::lower_bound(used.begin(), used.end(), slab) - used.begin()); };
+  for (int m = 0; m < (int)tiles.size(); ++m) {
+    G.ra[m % 8][m / 8] = (signed char)idx(tiles[m].first);
+    G.cb[m % 8][m / 8] = (signed char)idx(tiles[m].second);
+  }
+  return G;
+}
+
+// Repair pass over a covering (off by default: modelled by scripts/band_l2sim.cpp,
+// conv2's fabric bytes 2.44 -> 2.36 GB only): the greedy leaves a tail of small groups (conv2:
+// 19 one-tile groups), whose blocks stream the image rows at a different pace
+// from the full groups beside them, so the rows one block pulls into its XCD's
+// L2 are gone when the others reach them.  Move every tile of the smallest
+// groups into the fullest group that has a free slot and holds its slabs (or can
+// stage the missing ones within NS); a group emptied this way is dropped.
+inline void band_plan_repair(std::vector<std::vector<std::pair<int, int>>>& groups, int NS, int cap) {
+  auto slabs_of = [](const std::vector<std::pair<int, int>>& gt) {
+    std::vector<int> u;
+    for (const auto& t : gt) u.push_back(t.first), u.push_back(t.second);
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    return u;
+  };
+  for (int pass = 0; pass < 4; ++pass) {
+    std::vector<int> ord(groups.size());
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return groups[x].size() < groups[y].size(); });
+    bool moved_any = false;
+    for (int si : ord) {
+      auto& src = groups[si];
+      if (src.empty() || (int)src.size() >= 13) continue;
+      // try to empty this group entirely: plan all moves first
+      std::vector<std::vector<std::pair<int, int>>> trial = groups;
+      bool ok = true;
+      for (const auto& t : src) {
+        int best = -1;
+        for (size_t gi = 0; gi < trial.size(); ++gi) {
+          if ((int)gi == si || trial[gi].empty() || (int)trial[gi].size() >= cap) continue;
+          std::vector<int> u = slabs_of(trial[gi]);
+          u.push_back(t.first), u.push_back(t.second);
+          std::sort(u.begin(), u.end());
+          u.erase(std::unique(u.begin(), u.end()), u.end());
+          if ((int)u.size() > NS) continue;
+          if (best < 0 || trial[gi].size() > trial[best].size()) best = (int)gi;
+        }
+        if (best < 0) {
+          ok = false;
+          break;
+        }
+        trial[best].push_back(t);
+      }
+      if (!ok) continue;
+      trial[si].clear();
+      groups.swap(trial);
+      moved_any = true;
+    }
+    groups.erase(std::remove_if(groups.begin(), groups.end(), [](const auto& gt) { return gt.empty(); }),
+                 groups.end());
+    if (!moved_any) break;
+  }
+}
+
 // Greedy covering of the needed sub-tiles by groups of <= kBandSlabs slabs and
 // <= 16 tiles (two per wave): each of the 32 slabs with the most uncovered tiles
 // seeds a candidate set grown by the neighbour adding the most uncovered tiles;
@@ -127,7 +208,7 @@ inline std::vector<char> band_needed(const BandGeom& g) {
 // small).  Seeded restarts, the fewest groups kept.  Conv2 (M = 10240): 190
 // groups, 117 of them full, against 243 six-slab groups of 9.5 tiles -- 8 slabs
 // double the pairs a staged set can hold (28 + 8 against 15 + 6).
-inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 3) {
+inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 3, bool repair = false) {
   constexpr int NS = kBandSlabs;
   constexpr int cap = 16;
   const int ns = g.ns;
@@ -149,7 +230,7 @@ inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 3) 
           ++deg[a];
           if (b != a) ++deg[b], nbr[a].push_back(b), nbr[b].push_back(a);
         }
-    std::vector<BandGroup> groups;
+    std::vector<std::vector<std::pair<int, int>>> groups;  // each group's tiles (a <= b slabs)
     std::vector<int> order(ns);
     for (int i = 0; i < ns; ++i) order[i] = i;
     std::vector<int> cand;
@@ -215,37 +296,21 @@ inline bool band_plan_build(const BandGeom& g, BandPlan* out, int restarts = 3) 
         }
       std::stable_sort(tiles.begin(), tiles.end(), [](const T& x, const T& y) { return x.key < y.key; });
       if ((int)tiles.size() > cap) tiles.resize(cap);
-      // the staged slabs: the ones the chosen tiles use, in column order
-      std::vector<int> used;
-      for (const T& t : tiles) used.push_back(t.a), used.push_back(t.b);
-      std::sort(used.begin(), used.end());
-      used.erase(std::unique(used.begin(), used.end()), used.end());
-      BandGroup G;
-      G.nslab = (unsigned char)used.size();
-      G.xmask = 0;
-      for (int i = 0; i < NS; ++i) {
-        G.base[i] = i < (int)used.size() ? 64 * used[i] : -1;
-        if (i < (int)used.size() && used[i] < g.nxs) G.xmask |= (unsigned char)(1u << i);
-      }
-      for (int w = 0; w < 8; ++w)
-        for (int t = 0; t < 2; ++t) G.ra[w][t] = G.cb[w][t] = -1, G.tile[w][t] = -1;
-      G.csown = 0;
-      G.pad = 0;
-      auto idx = [&](int slab) { return (int)(std::lower_bound(used.begin(), used.end(), slab) - used.begin()); };
-      for (int m = 0; m < (int)tiles.size(); ++m) {
-        const int a = tiles[m].a, b = tiles[m].b;
-        need[(size_t)a * ns + b] = 0;
+      std::vector<std::pair<int, int>> gt;
+      for (const T& t : tiles) {
+        need[(size_t)t.a * ns + t.b] = 0;
         --remaining;
-        --deg[a];
-        if (b != a) --deg[b];
-        G.ra[m % 8][m / 8] = (signed char)idx(a);
-        G.cb[m % 8][m / 8] = (signed char)idx(b);
+        --deg[t.a];
+        if (t.b != t.a) --deg[t.b];
+        gt.push_back({t.a, t.b});
       }
-      groups.push_back(G);
+      groups.push_back(gt);
     }
+    if (repair) band_plan_repair(groups, NS, cap);
     if (found && groups.size() >= out->groups.size()) continue;
     out->geom = g;
-    out->groups = groups;
+    out->groups.clear();
+    for (const auto& gt : groups) out->groups.push_back(band_group_of(g, gt));
     found = true;
   }
   if (!found) return false;

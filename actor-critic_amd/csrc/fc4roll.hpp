@@ -145,9 +145,13 @@ void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w
 
 // false when the shape is not one this kernel covers (the caller then uses gemm3)
 // hdr: the tower's bounds header (TowerPrep::HDR of the same prep)
+// the shapes fc4_roll_kernel takes (launch_fc4_roll returns false otherwise)
+inline bool fc4_roll_ok(const float* a3, long long lda, int K, int chunk) {
+  return !(chunk % 16 || K % 16 || (lda % 4) || ((uintptr_t)a3 % 16));
+}
 inline bool launch_fc4_roll(const float* a3, long long lda, int B, int K, const char* w4p, int nz, int chunk,
                             float* part, const unsigned* hdr, hipStream_t s, Fc4Commit cm = Fc4Commit{}) {
-  if (chunk % 16 || K % 16 || (lda % 4) || ((uintptr_t)a3 % 16)) return false;
+  if (!fc4_roll_ok(a3, lda, K, chunk)) return false;
   const int cs = chunk / 16;
 #ifndef ACMI_FC4_SMALL_CT  // column tiles per wave at batches <= 64
 #define ACMI_FC4_SMALL_CT 1

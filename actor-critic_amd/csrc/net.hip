@@ -615,19 +615,23 @@ static int forward_impl(const Layout& L, const float* P, const uint8_t* obs,
   int nz, chunk;
   fc4_plan(B, K4, &nz, &chunk);
   const bool split = nz > 1 && a->ws && a->ws_floats >= (long long)nz * (B + 1) * 512;
+  const char* w4p = prep ? static_cast<const char*>(prep) + TowerPrep<C3>::BYTES + CT2::BYTES : nullptr;
   // the split rollout step's pending env states, after fc4's slabs in the forward
-  // workspace (acmi_forward_ws_floats reserves them at B <= kSplitMaxB)
-  PendState* pend = split && tail && B <= kSplitMaxB &&
+  // workspace (acmi_forward_ws_floats reserves them at B <= kSplitMaxB); only with
+  // the rollout fc4 kernel, the one launch that commits them
+  const bool fc4_roll = split && g_gemm_mode == ACMI_GEMM_X3 && w4p && fc4_roll_ok(a->a3, st * K4, K4, chunk);
+  PendState* pend = fc4_roll && tail && B <= kSplitMaxB &&
                             a->ws_floats >= (long long)nz * (B + 1) * 512 + (long long)B * (sizeof(PendState) / 4)
                         ? reinterpret_cast<PendState*>(a->ws + (long long)nz * (B + 1) * 512)
                         : nullptr;
   if (split) {
     // small (rollout) batches: split K over chunks; the heads kernel reduces
     // the slabs in fixed order and applies bias + relu
-    const char* w4p = prep ? static_cast<const char*>(prep) + TowerPrep<C3>::BYTES + CT2::BYTES : nullptr;
-    // (only a step whose tower ran in the previous step's tail can have states pending)
-    const Fc4Commit cm{pend, tail ? tail->io.state : acmi_env_state_t{}, pend && tower_done ? B : 0};
-    if (!(g_gemm_mode == ACMI_GEMM_X3 && w4p &&
+    // every rollout step with a pending area commits the entries flagged there
+    // (the previous fused step's; also, at step 0, those a rollout abandoned
+    // between fused steps left behind -- the flag is cleared on commit)
+    const Fc4Commit cm{pend, tail ? tail->io.state : acmi_env_state_t{}, pend ? B : 0};
+    if (!(fc4_roll &&
           launch_fc4_roll(a->a3, st * K4, B, K4, w4p, nz, chunk, a->ws,
                           reinterpret_cast<const unsigned*>(static_cast<const char*>(prep) + TowerPrep<C3>::HDR),
                           s, cm))) {
@@ -1346,8 +1350,9 @@ static int gcov_layer(const float* g, int ld, int n, long long rows, int sub,
   return ACMI_OK;
 }
 
-static long long bwd_partial_cap(int B, int A, int C3) {
-  // the largest split-K partial over all layers (with stats)
+// the split-K partial region's minimum: the largest partial over all layers (with
+// stats, both gemm modes, both Gram paths, the band reductions)
+static long long bwd_partial_floats(int B, int A, int C3) {
   long long m = 0;
   const long long rowsL[5] = {400LL * B, 81LL * B, 49LL * B, B, B};
   const int Ks[5] = {256, 512, 576, 49 * C3, 512};
@@ -1370,11 +1375,20 @@ static long long bwd_partial_cap(int B, int A, int C3) {
   // band reductions of conv2 / conv3 (rows = images)
   m = std::max(m, band_ws_floats(band_host_plan(20, 20, 32, 4, 4, 2, 64), B));
   m = std::max(m, band_ws_floats(band_host_plan(9, 9, 64, 3, 3, 1, C3), B));
-  // + the band reductions' scratch (operand-scale maxima, band.hpp) at the end
-  return (m + 3) / 4 * 4 + kBandScratch;
+  return (m + 63) / 64 * 64;
 }
 
 static long long afactor_ws_floats(int B) { return conv1_afactor_ws_ints(400LL * B); }
+
+// Workspace of acmi_backward / acmi_kfac_output_stats (one size for both):
+//   backward:      [scratch kBandScratch | conv1 A-factor ints | partials ...]
+//   output stats:  [scratch kBandScratch | sampled head gradients B x ldg | partials ...]
+// (prefixes rounded to 256 B); the partial region is the rest of the caller's
+// buffer, at least bwd_partial_floats
+static long long head_grad_ldg(int A) { return roundup4(A + 1) < 8 ? 8 : roundup4(A + 1); }
+static long long bwd_prefix_floats(int B) { return kBandScratch + (afactor_ws_floats(B) + 63) / 64 * 64; }
+static long long stats_prefix_floats(int B, int A) { return kBandScratch + ((long long)B * head_grad_ldg(A) + 63) / 64 * 64; }
+static int g_ws_flushes = 0;  // acmi_debug_ws_flushes
 
 // Recorded on the backward's stream right after its input-gradient chain (per
 // device): acmi_stream_wait_backward_dx lets the sampled-loss chain on another
@@ -1515,10 +1529,12 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // gather competes with the symmetric reductions for L2 and LDS; the A factor
   // before the dX chain.)
   const bool fuse_c1 = st && g_gemm_mode == ACMI_GEMM_X3;
-  // band reductions: operand-scale scratch (band.hpp) after the partial region;
-  // the dX epilogues publish max |d3|, |d2| into it
-  const long long pcap_all = bwd_partial_cap(B, L.A, L.C3);
-  unsigned* bscr = reinterpret_cast<unsigned*>(ws + pcap_all - kBandScratch);
+  // operand-scale scratch (band.hpp) first: the dX epilogues publish max |d3|,
+  // |d2| into it; then the conv1 A-factor integers; the partial region is the rest
+  unsigned* bscr = reinterpret_cast<unsigned*>(ws);
+  const long long prefix = bwd_prefix_floats(B);
+  float* part = ws + prefix;
+  const long long avail = ws_cap - prefix;
   const bool band = band_on(st);
   int rc = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s, prep, nullptr, nullptr, bscr);
   if (rc) return rc;
@@ -1528,20 +1544,19 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   }
   float* wpart_c1 = nullptr;  // conv1's fused weight-gradient partials (in the A-factor workspace)
   if (st) {
-    const long long pcap = bwd_partial_cap(B, L.A, L.C3);
     prof_begin(ACMI_PROF_CONV1_AFACTOR, s);
     const int rc0 = conv1_afactor_u8(obs, img_stride, B, astat + L.stat_off[0],
-                                     reinterpret_cast<int*>(ws + pcap), afactor_ws_floats(B), s,
+                                     reinterpret_cast<int*>(ws + kBandScratch), afactor_ws_floats(B), s,
                                      fuse_c1 ? bw->d1 : nullptr, &wpart_c1, bscr + kBsMaxD1);
     prof_end(ACMI_PROF_CONV1_AFACTOR, s);
     if (rc0) return rc0;
   }
   // the conv1, heads and fc4 finalizes deferred into one launch: each layer's
-  // partials in their own range of the partial region (below the band scratch;
-  // a layer that does not fit after the others finalizes the set so far first)
+  // partials in their own range of the partial region (a layer that does not fit
+  // after the others finalizes the set so far first -- at workspaces near the
+  // minimum, acmi_debug_ws_flushes counts it)
   WgradSet fin;
   long long off = 0;
-  const long long avail = pcap_all - kBandScratch;
   auto flush = [&]() {
     if (fin.n) hipLaunchKernelGGL(finalize_wgrad_multi_kernel, dim3(fin.blocks), dim3(256), 0, s, fin);
     fin = WgradSet();
@@ -1553,13 +1568,16 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
                 nullptr, nullptr, (int)rows, 1.0f / 255.0f};
     fin.add(d, 0, 0, fin_blocks(d));
   }
-  float* part = ws;
   // need: the layer's partial floats (its plan), checked here so that a layer
-  // that does not fit after the others starts a new range instead of failing
-  auto layer = [&](long long need, auto&& run) {
+  // that does not fit after the others starts a new range instead of failing;
+  // the layer then reports what it used, which must be that plan
+  auto layer = [&](long long need, auto&& run) -> int {
     long long used = 0;
-    if (fin.n + 2 > kWgradTasks || (off > 0 && need > avail - off)) flush();
+    if (off > 0 && need > avail - off) ++g_ws_flushes, flush();
+    else if (fin.n + 2 > kWgradTasks) flush();
     const int r = run(part + off, avail - off, &used);
+    ACMI_REQUIRE(r != ACMI_OK || used == need, ACMI_ERR_ARG,
+                 "internal: a layer used %lld partial floats against its planned %lld", used, need);
     off += (used + 3) / 4 * 4;
     return r;
   };
@@ -1583,7 +1601,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   flush();
   // conv3 / conv2: pixel-pair band reductions over the dense activation rows
   // (band.hpp), or the patches of a2 / a1
-  const long long band_cap = pcap_all - kBandScratch;
+  const long long band_cap = avail;
   // a1 / a2 bounds from the weights (max |d2|, |d3| came with the dX chain): the
   // prepared weights' header holds them (tower_stats_body, the same sums as
   // band_bounds_kernel), else computed here
@@ -1598,7 +1616,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
                     astat + L.stat_off[2], 1.f, a2b, bscr + kBsMaxD3, s);
   } else
     rc = wgrad_layer(ConvRows<float, 9, 9, 64, 3, 3, 1>{a->a2, 81 * 64, B * 49}, 576, 49LL * B,
-                     bw->d3, C3, C3, st, part, ws_cap, grads + L.off[4], C3, nullptr,
+                     bw->d3, C3, C3, st, part, avail, grads + L.off[4], C3, nullptr,
                      st ? astat + L.stat_off[2] : nullptr, s);
   if (rc) return rc;
   if (band)
@@ -1606,7 +1624,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
                     astat + L.stat_off[1], 1.f, a1b, bscr + kBsMaxD2, s, ACMI_PROF_CONV2_WGRAD);
   else
     rc = wgrad_layer(ConvRows<float, 20, 20, 32, 4, 4, 2>{a->a1, 400 * 32, B * 81}, 512,
-                     81LL * B, bw->d2, 64, 64, st, part, ws_cap, grads + L.off[2], 64, nullptr,
+                     81LL * B, bw->d2, 64, 64, st, part, avail, grads + L.off[2], 64, nullptr,
                      st ? astat + L.stat_off[1] : nullptr, s, ACMI_PROF_CONV2_WGRAD);
   if (rc) return rc;
   // conv1: patches of the u8 observations
@@ -1614,7 +1632,7 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   // the i8 matrix cores (exact integer sums, afactor_u8.hip)
   if (!fuse_c1)
     rc = wgrad_layer(ConvRows<uint8_t, 84, 84, 4, 8, 8, 4>{obs, (uint32_t)img_stride, B * 400}, 256,
-                     400LL * B, bw->d1, 32, 32, false, part, ws_cap, grads + L.off[0], 32, nullptr,
+                     400LL * B, bw->d1, 32, 32, false, part, avail, grads + L.off[0], 32, nullptr,
                      nullptr, s, ACMI_PROF_CONV1_WGRAD, 1.0f / 255.0f);  // raw u8 patches
   return rc;
 }
@@ -1658,14 +1676,13 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
                              uint32_t seed, uint32_t row0, uint32_t ctr,
                              float* gstat, float* ws, long long ws_cap,
                              hipStream_t s, const char* prep) {
-  const int ldg = roundup4(L.A + 1) < 8 ? 8 : roundup4(L.A + 1);
-  float* ghead = ws;  // [B][ldg]
-  float* part = ws + (long long)B * ldg;
-  // the dX chain's scratch (operand-scale maxima) in the workspace's last words,
-  // 16-byte aligned (an unaligned hipMemsetAsync runs as three fill kernels)
-  const long long dxo = (ws_cap - kBandScratch) & ~3LL;
-  const long long cap = dxo - (long long)B * ldg;
-  unsigned* dxs = reinterpret_cast<unsigned*>(ws + dxo);
+  const int ldg = (int)head_grad_ldg(L.A);
+  // [the dX chain's scratch (operand-scale maxima) | ghead [B][ldg] | partials]
+  unsigned* dxs = reinterpret_cast<unsigned*>(ws);
+  float* ghead = ws + kBandScratch;
+  const long long prefix = stats_prefix_floats(B, L.A);
+  float* part = ws + prefix;
+  const long long cap = ws_cap - prefix;
   hipLaunchKernelGGL(sampled_head_grad_kernel, dim3(cdiv(B, 128)), dim3(128), 0, s,
                      a->logits, a->ld_logits, B, L.A, seed, row0, ctr, ghead, ldg);
   bool g1_done = false;
@@ -1689,10 +1706,14 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
   // one Gram into the next free range, or -- when its plan's partials do not fit
   // after the others -- into a new range after the set so far is finalized
   auto gram = [&](const float* g, int ld, int n, long long rows, int sub, float* out, float* out_v, int vi,
-                  const unsigned* gmax) {
+                  const unsigned* gmax) -> int {
     long long used = 0;
-    if (fin.n + 2 > kCovTasks || (off > 0 && gcov_need(n, rows) > cap - off)) flush();
+    const long long need = gcov_need(n, rows);
+    if (off > 0 && need > cap - off) ++g_ws_flushes, flush();
+    else if (fin.n + 2 > kCovTasks) flush();
     const int r = gcov_layer(g, ld, n, rows, sub, part + off, cap - off, out, s, out_v, vi, gmax, &fin, &used);
+    ACMI_REQUIRE(r != ACMI_OK || used == need, ACMI_ERR_ARG,
+                 "internal: a Gram used %lld partial floats against its planned %lld", used, need);
     off += (used + 3) / 4 * 4;
     return r;
   };
@@ -1971,13 +1992,12 @@ int64_t acmi_forward_ws_floats(int B) {
 int64_t acmi_backward_ws_floats(int B, int A, int C3) {
   Layout L;
   if (!make_layout(A, C3, &L) || B < 0) return -1;
-  const int ldg = roundup4(A + 1) < 8 ? 8 : roundup4(A + 1);
-  return bwd_partial_cap(B, A, C3) + afactor_ws_floats(B) + (long long)B * ldg + 64;
+  return std::max(bwd_prefix_floats(B), stats_prefix_floats(B, A)) + bwd_partial_floats(B, A, C3);
 }
 
 int acmi_backward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,
                   const acmi_acts_t* acts, const acmi_bwd_t* bwd, float* grads,
-                  float* a_stats, float* ws, acmi_stream_t stream) {
+                  float* a_stats, float* ws, int64_t ws_floats, acmi_stream_t stream) {
   Layout L;
   ACMI_REQUIRE(net && acts && bwd && grads && ws && obs, ACMI_ERR_ARG,
                "acmi_backward: null argument");
@@ -1990,13 +2010,15 @@ int acmi_backward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride,
                "acmi_backward: ldh must be >= A+1 and a multiple of 4 (zero padded)");
   ACMI_REQUIRE(spans32(B, img_stride, 84 * 84 * 4) && spans32(B, 400 * 32, 400 * 32), ACMI_ERR_ARG,
                "acmi_backward: batch spans >= 2^31 elements (B=%d)", B);
-  const long long cap = acmi_backward_ws_floats(B, net->num_actions, net->conv3_filters);
+  const long long need = acmi_backward_ws_floats(B, net->num_actions, net->conv3_filters);
+  ACMI_REQUIRE(ws_floats >= need, ACMI_ERR_WS, "acmi_backward: workspace of %lld floats < %lld",
+               (long long)ws_floats, need);
   hipStream_t s = (hipStream_t)stream;
   if (L.C3 == 32)
     return backward_impl<32>(L, net->params, obs, img_stride, B, acts, bwd, grads, a_stats, ws,
-                             cap, s, static_cast<const char*>(net->conv_prep));
+                             ws_floats, s, static_cast<const char*>(net->conv_prep));
   return backward_impl<64>(L, net->params, obs, img_stride, B, acts, bwd, grads, a_stats, ws,
-                           cap, s, static_cast<const char*>(net->conv_prep));
+                           ws_floats, s, static_cast<const char*>(net->conv_prep));
 }
 
 int acmi_stream_wait_backward_dx(acmi_stream_t stream) {
@@ -2008,20 +2030,23 @@ int acmi_stream_wait_backward_dx(acmi_stream_t stream) {
 
 int acmi_kfac_output_stats(const acmi_net_t* net, int B, const acmi_acts_t* acts,
                            const acmi_bwd_t* bwd, uint32_t seed, uint32_t row_offset,
-                           uint32_t counter, float* g_stats, float* ws, acmi_stream_t stream) {
+                           uint32_t counter, float* g_stats, float* ws, int64_t ws_floats,
+                           acmi_stream_t stream) {
   Layout L;
   ACMI_REQUIRE(net && acts && bwd && g_stats && ws, ACMI_ERR_ARG,
                "acmi_kfac_output_stats: null argument");
   ACMI_REQUIRE(make_layout(net->num_actions, net->conv3_filters, &L), ACMI_ERR_ARG, "bad net");
   ACMI_REQUIRE(B > 0 && spans32(B, 400 * 32, 400 * 32), ACMI_ERR_ARG, "bad B");
   ACMI_REQUIRE(masks_ok(acts), ACMI_ERR_ARG, "acmi_kfac_output_stats: ReLU masks m1..m3 must be all set or all NULL");
-  const long long cap = acmi_backward_ws_floats(B, net->num_actions, net->conv3_filters);
+  const long long need = acmi_backward_ws_floats(B, net->num_actions, net->conv3_filters);
+  ACMI_REQUIRE(ws_floats >= need, ACMI_ERR_WS, "acmi_kfac_output_stats: workspace of %lld floats < %lld",
+               (long long)ws_floats, need);
   hipStream_t s = (hipStream_t)stream;
   if (L.C3 == 32)
     return output_stats_impl<32>(L, net->params, B, acts, bwd, seed, row_offset, counter,
-                                 g_stats, ws, cap, s, static_cast<const char*>(net->conv_prep));
+                                 g_stats, ws, ws_floats, s, static_cast<const char*>(net->conv_prep));
   return output_stats_impl<64>(L, net->params, B, acts, bwd, seed, row_offset, counter, g_stats,
-                               ws, cap, s, static_cast<const char*>(net->conv_prep));
+                               ws, ws_floats, s, static_cast<const char*>(net->conv_prep));
 }
 
 int acmi_prof_enable(int site, int capacity) {
@@ -2070,6 +2095,12 @@ int acmi_prof_collect(double* total_ms, int* count) {
 // upper triangle of P^T P and every (P, dY) sub-tile is produced by sym_plan's
 // groups, each column's sum by exactly one wave, for K = 64..max_k; and
 // plan_rounds' chunks cover the rows exactly.  0 = ok, else the failing K.
+int acmi_debug_ws_flushes(void) {
+  const int n = g_ws_flushes;
+  g_ws_flushes = 0;
+  return n;
+}
+
 int acmi_selftest_plans(int max_k) {
   for (int K = 64; K <= max_k; K += 32) {
     SymPlan p;

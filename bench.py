@@ -65,6 +65,56 @@ def measured_traffic(kernel, workload):
     return None
 
 
+INT8_MFMA_PEAK_TOPS = 2 * BF16_MFMA_PEAK_TFLOPS  # v_mfma_i32_32x32x32_i8: twice the bf16 rate
+U8F16X2_F32EQ_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 2  # u8 pixels exact: two f16 MFMAs per product
+FP64_MFMA_PEAK_TFLOPS = 78.6  # v_mfma_f64_16x16x4f64, dense
+
+
+def iteration_ceiling(N, T, A, C3, acktr, band_tiles=None):
+    """The build's algorithmic work per training iteration (DESIGN.md section 3,
+    per-kernel accounting), each kernel's work priced at the ceiling of the
+    arithmetic it runs: the time the iteration would take if every kernel ran at
+    its roofline.  band_tiles: (conv2, conv3) needed 64x64 sub-tiles of the band
+    reductions (acmi_band_info).  Returns {component: (work, unit, ceiling, ms)}."""
+    M = N * T
+    K3 = 49 * C3
+    imgs = M + N  # the rollout's towers (T steps) and the bootstrap forward
+    f2, x3 = F16X2_F32EQ_PEAK_TFLOPS, X3_F32EQ_PEAK_TFLOPS
+    c = {}
+
+    def add(name, work, ceil, unit='GFLOP'):
+        # work in G-units; ceil in T-units per second -> ms
+        c[name] = (work, unit, ceil, work / ceil)
+
+    # rollout: conv tower (conv1 u8 x f16x2 on two MFMAs; conv2 / conv3 f16x2), fc4 + heads
+    add('tower conv1', 2 * 400 * 256 * 32 * imgs / 1e9, U8F16X2_F32EQ_PEAK_TFLOPS)
+    add('tower conv2 + conv3', (2 * 81 * 512 * 64 + 2 * 49 * 576 * C3) * imgs / 1e9, f2)
+    add('rollout fc4 + heads', (2 * K3 * 512 + 2 * 512 * (A + 1)) * imgs / 1e9, f2)
+    # env stepping: the 4-frame stack read and written per env-step (HBM)
+    add('stepper', 2 * 84 * 84 * 4 * M / 1e9, HBM_PEAK_GBS / 1e3, 'GB')
+    chains = 2 if acktr else 1  # the loss backward, and the sampled-loss (G statistics) chain
+    add('dX fc4 / conv3 / conv2', chains * (2 * K3 * 512 + 2 * 49 * 576 * C3 + 2 * 81 * 512 * 64) * M / 1e9, f2)
+    if acktr:
+        t2, t3 = band_tiles
+        add('band conv2 (wgrad + A)', 2 * 64 * 64 * t2 * M / 1e9, f2)
+        add('band conv3 (wgrad + A)', 2 * 64 * 64 * t3 * M / 1e9, f2)
+        add('fc4 wgrad + A', 2 * ((K3 + 1) * (K3 + 2) / 2 + (K3 + 1) * 512) * M / 1e9, f2)
+        add('heads wgrad + A', 2 * (513 * 514 / 2 + 513 * (A + 1)) * M / 1e9, x3)
+        add('conv1 A factor (i8, unique)', 2 * 400 * 256 * 257 / 2 * M / 1e9, INT8_MFMA_PEAK_TOPS, 'Gop')
+        add('conv1 wgrad', 2 * 400 * 257 * 32 * M / 1e9, U8F16X2_F32EQ_PEAK_TFLOPS)
+        add('G factors (unique)', (512 * 513 + 81 * 64 * 65 + 49 * C3 * (C3 + 1) + 400 * 32 * 33) * M / 1e9, f2)
+        # the damped inverses (fp64 block sweep, ~2 n^3 per matrix) every 10th update
+        dims = [257, 513, 577, K3 + 1, 513, 513, 32, 64, C3, 512, A, 1]
+        add('K-FAC inverse (1/10)', sum(2.0 * n ** 3 for n in dims) / 10 / 1e9, FP64_MFMA_PEAK_TFLOPS)
+        # the preconditioned step: Ainv G Ginv per layer (f32 MFMA)
+        blocks = [(257, 32), (513, 64), (577, C3), (K3 + 1, 512), (513, A), (513, 1)]
+        add('K-FAC step', sum(2.0 * a * b * (a + b) for a, b in blocks) / 1e9, FP32_MFMA_PEAK_TFLOPS)
+    else:
+        add('wgrad conv1..heads', 2 * (400 * 257 * 32 + 81 * 513 * 64 + 49 * 577 * C3 + (K3 + 1) * 512
+                                       + 513 * (A + 1)) * M / 1e9, f2)
+    return c
+
+
 def workload_name(algo, N, T, A, forward, world, games=None):
     """The BASELINE.json config a line measures (configs[1]-[4]; others: as given)."""
     if games == 'atari57':
@@ -222,19 +272,21 @@ def _measure(args, N, T, A, algo, games, steps, warmup, prof_site=None):
         # regions of the host-launch-bound small config (rollout 0.52 -> 0.56-0.61 ms)
         gc.collect()
         gc.disable()
-        t0 = time.perf_counter()
-        host = []  # host time per iteration minus its wait on the previous rollout's event
-        for k in range(steps):
-            th = time.perf_counter()
-            agent.last_sync_wait = 0.0
-            iteration(s, marks[k])
-            host.append(time.perf_counter() - th - getattr(agent, 'last_sync_wait', 0.0))
-            inv_flags.append(bool(getattr(optimizer, 'last_flags', (0, 0, 0))[2]) if acktr else False)
-        torch.cuda.synchronize()
-        parallel.barrier()
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-        gc.enable()
+        try:
+            t0 = time.perf_counter()
+            host = []  # host time per iteration minus its wait on the previous rollout's event
+            for k in range(steps):
+                th = time.perf_counter()
+                agent.last_sync_wait = 0.0
+                iteration(s, marks[k])
+                host.append(time.perf_counter() - th - getattr(agent, 'last_sync_wait', 0.0))
+                inv_flags.append(bool(getattr(optimizer, 'last_flags', (0, 0, 0))[2]) if acktr else False)
+            torch.cuda.synchronize()
+            parallel.barrier()
+            torch.cuda.synchronize()
+            elapsed = time.perf_counter() - t0
+        finally:
+            gc.enable()
         if prof_site is not None:
             _lib.call('acmi_prof_collect', ctypes.byref(tot_ms), ctypes.byref(cnt))
             _lib.call('acmi_prof_enable', 0, 0)
@@ -356,6 +408,21 @@ def run(args):
         # the patch-row formulation's unique FLOPs over the same time: the rate
         # the replaced kernel would have needed to match
         roofline['patch_equivalent_tflops'] = patch_flops / (kern_ms * 1e-3) / 1e12
+    if x3:
+        # the whole iteration against its roofline: every kernel's algorithmic work
+        # at the ceiling of its arithmetic, summed, over the measured ms_per_step
+        bt = None
+        if acktr:
+            i2, i3 = (ctypes.c_int64 * 5)(), (ctypes.c_int64 * 5)()
+            _lib.call('acmi_band_info', 1, C3, M, i2)
+            _lib.call('acmi_band_info', 2, C3, M, i3)
+            bt = (int(i2[0]), int(i3[0]))
+        ceil = iteration_ceiling(N, T, A, C3, acktr, bt)
+        ceil_ms = sum(v[3] for v in ceil.values())
+        roofline['iteration_frac'] = ceil_ms / ms_per_step
+        roofline['iteration_ceiling_ms'] = ceil_ms
+        roofline['iteration_ceiling'] = {k: {'work': round(v[0], 4), 'unit': v[1], 'ceiling_per_s': round(v[2], 1),
+                                             'ms': round(v[3], 5)} for k, v in ceil.items()}
     if x3 and achieved:
         # peak = 16-bit dense peak / nmf (f32-equivalent); the same rate against
         # the f32-input MFMA peak and the bf16x3 ceiling, and the 16-bit MFMA work

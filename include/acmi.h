@@ -22,7 +22,8 @@
 extern "C" {
 #endif
 
-#define ACMI_ABI_VERSION 3  /* 3: acmi_env_state_t.game, acmi_rollout_io_t step fusion fields */
+#define ACMI_ABI_VERSION 4  /* 3: acmi_env_state_t.game, acmi_rollout_io_t step fusion fields;
+                               4: ws_floats on acmi_backward / acmi_kfac_output_stats */
 
 enum {
   ACMI_OK = 0,
@@ -292,7 +293,12 @@ int acmi_a2c_loss(const float* logits, int ld, const float* values,
  *           (conv: x = the (kh,kw,cin) input patch at every output location,
  *            rows = B*locations; fc: x = the input row; A_4 = fc4 output).
  * dhead: [B][ldh] from acmi_a2c_loss.  d1..d4 are [B]x(layer output) scratch.
- * ws: >= acmi_backward_ws_floats(B, A, C3) floats.
+ * ws: ws_floats >= acmi_backward_ws_floats(B, A, C3) floats; a smaller
+ * ws_floats fails with ACMI_ERR_WS before anything is enqueued (nothing is
+ * written).  Layout: [operand-scale scratch | conv1 A-factor integers |
+ * split-K partials]; the partial region is everything past the fixed prefix, so
+ * a larger workspace only lets more of the small layers' finalizes share one
+ * launch (results bit-identical for every legal size).
  * net->conv_prep (when non-null) must have been prepared (acmi_conv_prepare)
  * from the same parameters as net->params: its header supplies the a1 / a2 /
  * a3 bounds that scale the f16x2 operands of the conv2 / conv3 / fc4
@@ -313,7 +319,7 @@ int64_t acmi_backward_ws_floats(int B, int num_actions, int conv3_filters);
 int acmi_backward(const acmi_net_t* net, const uint8_t* obs,
                   int64_t img_stride, int B, const acmi_acts_t* acts,
                   const acmi_bwd_t* bwd, float* grads, float* a_stats,
-                  float* ws, acmi_stream_t stream);
+                  float* ws, int64_t ws_floats, acmi_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * K-FAC output-factor statistics (kfac "gradients" estimation mode over the
@@ -324,12 +330,15 @@ int acmi_backward(const acmi_net_t* net, const uint8_t* obs,
  * a data-parallel shard draws exactly the full batch's samples; the per-example
  * gradients of -log p(y) w.r.t. each registered layer output are
  * back-propagated (dX only) and G_l = mean over rows of g g^T is written to
- * g_stats (layout of acmi_kfac_layout, G part).  Reuses bwd->d1..d4 and ws.
+ * g_stats (layout of acmi_kfac_layout, G part).  Reuses bwd->d1..d4 and ws
+ * (ws_floats >= acmi_backward_ws_floats(B, A, C3), else ACMI_ERR_WS before
+ * anything is enqueued; layout [scratch | sampled head gradients | partials]).
  * ---------------------------------------------------------------------- */
 int acmi_kfac_output_stats(const acmi_net_t* net, int B,
                            const acmi_acts_t* acts, const acmi_bwd_t* bwd,
                            uint32_t seed, uint32_t row_offset, uint32_t counter,
-                           float* g_stats, float* ws, acmi_stream_t stream);
+                           float* g_stats, float* ws, int64_t ws_floats,
+                           acmi_stream_t stream);
 /* Makes `stream` wait (stream-ordered, no host sync) for the point right after
  * the input-gradient chain of the most recent acmi_backward on this device, so
  * a sampled-loss chain (acmi_kfac_output_stats on its own buffers) enqueued on
@@ -523,7 +532,11 @@ typedef struct acmi_rollout_io {
    * NEXT step's fc4 launch commits them into `state`: consecutive fused steps
    * of a rollout must pass the same acts->ws, and a rollout must end with an
    * unfused step (next_acts = NULL, tower_done = 1), whose launch commits the
-   * last pending states before its own env step. */
+   * last pending states before its own env step.  Every step at B <= 64 commits
+   * the entries still flagged there first, so a rollout abandoned between
+   * fused steps is committed by the next rollout's step 0 on the same
+   * acts->ws; the pending area must start zeroed (zero-fill the forward
+   * workspace once before its first rollout step). */
   int tower_done;
   const struct acmi_acts* next_acts;
   int64_t next_act_stride;
@@ -546,6 +559,11 @@ int acmi_rollout_step(const acmi_net_t* net, const uint8_t* obs,
  * sub-tile and column sum for K = 64..max_k, split-K chunks cover the rows.
  * Returns 0, or the first failing K (-1: chunk plan). */
 int acmi_selftest_plans(int max_k);
+/* Host-only diagnostic: the number of times acmi_backward / acmi_kfac_output_stats
+ * finalized their deferred small-layer set early because the next layer's
+ * split-K partials did not fit in the rest of the workspace (a legal size near
+ * the minimum), since the previous call of this function (which resets it). */
+int acmi_debug_ws_flushes(void);
 
 /* C[M][N] = A[M][K] @ B[K][N], row-major fp32, f32-input MFMA */
 int acmi_gemm_f32(const float* A, const float* B, float* C, int M, int N,

@@ -161,13 +161,13 @@ def _stats_vs_float64(lib, cuda, B, params, seed=2024):
     bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
     grads, astat, gstat = z(params.numel()), z(tot.value), z(tot.value)
     _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
-              ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), st)
+              ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), ws.numel(), st)
     ds = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
     dhead_s = z(B, ldh)  # the sampled chain writes its own head gradients here
     bwd_s = _lib.Bwd(*[x.data_ptr() for x in ds], dhead_s.data_ptr(), ldh)
     seed_s, counter = 0x4b464143, 41
     _lib.call('acmi_kfac_output_stats', ctypes.byref(net), B, ctypes.byref(acts), ctypes.byref(bwd_s), seed_s, 0,
-              counter, _lib.ptr(gstat), _lib.ptr(ws), st)
+              counter, _lib.ptr(gstat), _lib.ptr(ws), ws.numel(), st)
     torch.cuda.synchronize()
     assert torch.isfinite(grads).all() and torch.isfinite(astat).all() and torch.isfinite(gstat).all()
 

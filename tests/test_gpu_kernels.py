@@ -119,10 +119,10 @@ def test_relu_masks_written_and_bit_identical(lib, cuda, use_prep, B):
         bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
         grads, astat, gstat = z(params.numel()), z(tot.value), z(tot.value)
         _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
-                  ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), _lib.stream_handle())
+                  ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), ws.numel(), _lib.stream_handle())
         d1 = d[0].clone()
         _lib.call('acmi_kfac_output_stats', ctypes.byref(net), B, ctypes.byref(acts), ctypes.byref(bwd),
-                  7, 0, 3, _lib.ptr(gstat), _lib.ptr(ws), _lib.stream_handle())
+                  7, 0, 3, _lib.ptr(gstat), _lib.ptr(ws), ws.numel(), _lib.stream_handle())
         torch.cuda.synchronize()
         if masks:
             for k, words in (('1', 400), ('2', 162), ('3', 49 * C3 // 32)):
@@ -130,6 +130,84 @@ def test_relu_masks_written_and_bit_identical(lib, cuda, use_prep, B):
         out[masks] = (grads.cpu(), astat.cpu(), gstat.cpu(), d1.cpu())
     for a, b in zip(out[False], out[True]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('C3,B', [(32, 24), (64, 640)])
+def test_backward_workspace_contract(lib, cuda, C3, B):
+    """ws_floats in the ABI (v4): an undersized workspace fails with ACMI_ERR_WS
+    before anything is enqueued -- the workspace with a guard region past the
+    nominal end, the gradients, the factors and d1..d4 (all NaN-filled) stay
+    untouched -- and every legal size gives bit-identical results.  At C3 = 64,
+    B = 640 with K-FAC statistics the minimum workspace cannot hold the heads'
+    (5.3 M floats) and fc4's (22.9 M) split-K partials side by side (the minimum
+    partial region is the largest single plan, 26.6 M), so the backward
+    finalizes its deferred set early (acmi_debug_ws_flushes > 0); five times the
+    minimum never does.
+    Reference: SURVEY 8(b) "workspaces passed in"; the error mapping of
+    actorcritic/model.py:180-186."""
+    A = 4
+    g = torch.Generator().manual_seed(31)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
+    params = rand_params(A, C3, cuda, seed=5)
+    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
+    net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr())
+    _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), _lib.stream_handle())
+    ldh = 8
+    dhead = torch.zeros(B, ldh)
+    dhead[:, :A + 1] = torch.randn(B, A + 1, generator=g) / B
+    dhead = dhead.to(cuda)
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, None, None, so, ctypes.byref(tot))
+    t, acts = alloc_acts(B, A, C3, cuda, masks=True)
+    _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+              _lib.stream_handle())
+    need = int(lib.acmi_backward_ws_floats(B, A, C3))
+    nan = float('nan')
+    guard = 4096
+
+    def run(ws_floats, alloc):
+        ws = torch.full((alloc,), nan, dtype=torch.float32, device=cuda)
+        d = [torch.full(sh, nan, device=cuda) for sh in ((B, 20, 20, 32), (B, 9, 9, 64), (B, 7, 7, C3), (B, 512))]
+        bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
+        grads = torch.full((params.numel(),), nan, device=cuda)
+        astat = torch.full((tot.value,), nan, device=cuda)
+        gstat = torch.full((tot.value,), nan, device=cuda)
+        torch.cuda.synchronize()
+        lib.acmi_debug_ws_flushes()
+        rc_b = lib.acmi_backward(ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
+                                 ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), ws_floats,
+                                 _lib.stream_handle())
+        rc_s = lib.acmi_kfac_output_stats(ctypes.byref(net), B, ctypes.byref(acts), ctypes.byref(bwd), 7, 0, 3,
+                                          _lib.ptr(gstat), _lib.ptr(ws), ws_floats, _lib.stream_handle())
+        torch.cuda.synchronize()
+        return rc_b, rc_s, lib.acmi_debug_ws_flushes(), ws, [grads, astat, gstat] + d
+
+    # undersized by one float: both entry points refuse, nothing is written
+    rc_b, rc_s, fl, ws, outs = run(need - 1, need + guard)
+    assert rc_b == -3 and rc_s == -3, (rc_b, rc_s)
+    assert b'workspace' in lib.acmi_last_error()
+    assert fl == 0
+    assert torch.isnan(ws).all(), 'an undersized call wrote into its workspace or the guard region'
+    for x in outs:
+        assert torch.isnan(x).all(), 'an undersized call wrote an output'
+    # the minimum and a large workspace: identical bits; nothing past ws_floats
+    rc_b, rc_s, fl_min, ws_min, out_min = run(need, need + guard)
+    assert rc_b == 0 and rc_s == 0
+    assert torch.isnan(ws_min[need:]).all(), 'the backward wrote past ws_floats'
+    rc_b, rc_s, fl_big, _, out_big = run(5 * need, 5 * need)
+    assert rc_b == 0 and rc_s == 0
+    assert fl_big == 0
+    if C3 == 64:
+        assert fl_min > 0, 'the minimum workspace was expected to finalize the deferred set early'
+    # written: grads, the A part of a_stats, the G part of g_stats, d1..d4
+    ga = so[5]
+    written = [out_min[0], out_min[1][:ga], out_min[2][ga:]] + out_min[3:]
+    for a in written:
+        assert not torch.isnan(a).any()
+    for a, b in zip(out_min, out_big):
+        assert torch.equal(torch.isnan(a), torch.isnan(b))
+        assert torch.equal(torch.nan_to_num(a), torch.nan_to_num(b))
 
 
 @pytest.mark.parametrize('C3', [32, 64])
@@ -197,7 +275,7 @@ def test_conv3_dx_prepared_weights_bit_identical(lib, cuda, C3):
         bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
         grads = z(params.numel())
         _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
-                  ctypes.byref(bwd), _lib.ptr(grads), None, _lib.ptr(ws), _lib.stream_handle())
+                  ctypes.byref(bwd), _lib.ptr(grads), None, _lib.ptr(ws), ws.numel(), _lib.stream_handle())
         torch.cuda.synchronize()
         out.append((d[2].cpu(), d[1].cpu()))
     assert out[0][1].abs().max() > 0
@@ -270,7 +348,7 @@ def _backward_errors(lib, cuda, B=6, seed=3):
     astat = z(tot.value)
     ws = z(lib.acmi_backward_ws_floats(B, A, C3))
     _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs_d), 84 * 84 * 4, B, ctypes.byref(acts),
-              ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), _lib.stream_handle())
+              ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), ws.numel(), _lib.stream_handle())
     torch.cuda.synchronize()
     # reference gradients by autograd in float64
     p64 = params.cpu().double().requires_grad_(True)
@@ -385,7 +463,7 @@ def _band_backward(lib, cuda, B, mode, reps=1, seed=8):
         grads, astat = z(params.numel()), z(tot.value)
         _with_conv_stats(lib, mode, _lib.call, 'acmi_backward', ctypes.byref(net), _lib.ptr(obs),
                          84 * 84 * 4, B, ctypes.byref(acts), ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat),
-                         _lib.ptr(ws), _lib.stream_handle())
+                         _lib.ptr(ws), ws.numel(), _lib.stream_handle())
         torch.cuda.synchronize()
         outs.append((grads.cpu(), astat.cpu()))
     return outs, list(din), list(so), _layout(A, C3)[0]
@@ -651,14 +729,14 @@ def test_convt2_matches_gemm3_path(lib, cuda, B):
         bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
         grads, astat = z(params.numel()), z(tot.value)
         _lib.call('acmi_backward', ctypes.byref(nets[use_prep]), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
-                  ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), _lib.stream_handle())
+                  ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), ws.numel(), _lib.stream_handle())
         torch.cuda.synchronize()
         d1_loss = d[0].clone()
         ds = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
         bwd_s = _lib.Bwd(*[x.data_ptr() for x in ds], dhead.data_ptr(), ldh)
         gstat = z(tot.value)
         _lib.call('acmi_kfac_output_stats', ctypes.byref(nets[use_prep]), B, ctypes.byref(acts), ctypes.byref(bwd_s),
-                  7, 0, 3, _lib.ptr(gstat), _lib.ptr(ws), _lib.stream_handle())
+                  7, 0, 3, _lib.ptr(gstat), _lib.ptr(ws), ws.numel(), _lib.stream_handle())
         torch.cuda.synchronize()
         out[use_prep] = (d1_loss.cpu(), grads.cpu(), astat.cpu(), gstat.cpu(), ds[0].cpu())
     (d1a, ga, aa, sa, d1s), (d1b, gb, ab, sb, _) = out[False], out[True]
@@ -752,7 +830,7 @@ def test_conv1_afactor_and_weight_gradient_match_float64(lib, cuda, B):
     bwd = _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
     grads, astat = z(params.numel()), z(tot.value)
     _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs_d), 84 * 84 * 4, B, ctypes.byref(acts),
-              ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), _lib.stream_handle())
+              ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), ws.numel(), _lib.stream_handle())
     torch.cuda.synchronize()
     p = obs.double().unfold(1, 8, 4).unfold(2, 8, 4).permute(0, 1, 2, 4, 5, 3).reshape(-1, 256)
     d1 = d[0].cpu().double().reshape(-1, 32)

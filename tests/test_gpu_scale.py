@@ -87,7 +87,7 @@ def _backward_multichunk(lib, cuda):
     astat = z(tot.value)
     ws = z(lib.acmi_backward_ws_floats(B, A, C3))
     _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs_d), 84 * 84 * 4, B, ctypes.byref(acts),
-              ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), _lib.stream_handle())
+              ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(astat), _lib.ptr(ws), ws.numel(), _lib.stream_handle())
     # G statistics of a fixed output gradient through the same chain
     torch.cuda.synchronize()
     p64 = params.cpu().double().requires_grad_(True)
@@ -213,6 +213,48 @@ def test_two_stream_rollout_is_bit_identical(lib, cuda, monkeypatch):
         assert agent._bufs.halves == (split == '1')
         assert (agent._bufs.graph is not None) == (graph == '1')
         assert agent._bufs.fuse_steps == (fused == '1' and fsteps == '1')  # (x3 gemm mode: the default)
+        outs.append(got)
+    for other in outs[1:]:
+        for i, (a, b) in enumerate(zip(outs[0], other)):
+            if a.is_floating_point():  # episode rewards are NaN where no episode ended
+                assert torch.equal(torch.isnan(a), torch.isnan(b)), i
+                a, b = torch.nan_to_num(a, nan=0.0), torch.nan_to_num(b, nan=0.0)
+            assert torch.equal(a, b), i
+
+
+def test_split_rollout_step_bit_identical_across_terminals(lib, cuda, monkeypatch):
+    """32 envs (B <= 64: the split rollout step, each image's tower over 7
+    workgroups, the post-step env states parked in the forward workspace and
+    committed by the next step's fc4 launch): the fused steps, eagerly and
+    replayed from a captured hipGraph, give exactly the three-launch chain over
+    eight rollouts of 20 steps -- long enough that episodes end inside rollouts
+    and across rollout boundaries (auto-reset of a terminal env, episode totals
+    at terminals, the last unfused step's commit followed by the next rollout's
+    step 0).  Reference: agents.py:202-216, multi_env.py auto-reset."""
+    from actorcritic import session as sess
+    outs = []
+    for graph, fused, fsteps in (('0', '0', '0'), ('0', '1', '1'), ('1', '1', '1')):
+        monkeypatch.setenv('ACMI_ROLLOUT_SPLIT', '0')
+        monkeypatch.setenv('ACMI_ROLLOUT_GRAPH', graph)
+        monkeypatch.setenv('ACMI_ROLLOUT_FUSED', fused)
+        monkeypatch.setenv('ACMI_ROLLOUT_FUSE_STEPS', fsteps)
+        env, model, agent, obj, gs, opt, op = _bench_like(N=32, T=20, seed=77)
+        got, terms = [], []
+        with sess.Session() as s:
+            for _ in range(8):
+                obs, act, rew, term, nxt, info = agent.interact(s)
+                acts = agent._bufs.acts
+                got += [x.clone() for x in (obs, act, rew, term, nxt, info.episode_rewards, acts.a1, acts.a2,
+                                            acts.a3, acts.m1, acts.logits, acts.value)]
+                terms.append(term.clone())
+        torch.cuda.synchronize()
+        assert agent._bufs.fuse_steps == (fused == '1' and fsteps == '1')
+        assert (agent._bufs.graph is not None) == (graph == '1')
+        term_all = torch.stack(terms).cpu()  # [rollout, env, step]
+        assert term_all.any(), 'no episode ended: the terminal / auto-reset path went untested'
+        # some env ends an episode on a rollout's last step (its reset is committed
+        # by the unfused last step and read by the next rollout's step 0)
+        assert term_all[:-1, :, -1].any() or term_all[1:, :, 0].any()
         outs.append(got)
     for other in outs[1:]:
         for i, (a, b) in enumerate(zip(outs[0], other)):

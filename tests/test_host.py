@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol(lib):
     for name in declared:
         assert hasattr(lib, name), name
         assert name in _lib.EXPORTED, 'no ctypes signature for ' + name
-    assert lib.acmi_abi_version() == 3
+    assert lib.acmi_abi_version() == 4
 
 
 def test_ctypes_struct_mirrors_match_the_c_abi(lib):
