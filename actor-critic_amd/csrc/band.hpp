@@ -201,17 +201,6 @@ __global__ __launch_bounds__(256) void band_bounds_kernel(const float* w1, const
 // ---------------------------------------------------------------------------
 // the band kernel
 // ---------------------------------------------------------------------------
-#ifndef ACMI_BAND_DEPTH
-#define ACMI_BAND_DEPTH 2
-#endif
-constexpr int kBandDepth = ACMI_BAND_DEPTH;  // stages of loads in flight (register sets)
-#ifndef ACMI_BAND_PIPE  // 1: fragment reads one sub-tile ahead of the MFMAs (see the loop); 0: plain order
-#define ACMI_BAND_PIPE 1
-#endif
-#ifndef ACMI_BAND_PROBE  // timing probes (wrong results): 1 no split, 2 no column sums, 4 no loads,
-                         // 8 no LDS stores, 16 no MFMAs, 32 no LDS fragment reads
-#define ACMI_BAND_PROBE 0
-#endif
 constexpr int kBandRows = 16;                         // k-rows (images) per stage
 constexpr int kBandRowBytes = kBandSlabs * 64 * 2;    // 1024: one f16 row of the staged columns
 constexpr int kBandPart = kBandRows * kBandRowBytes;  // 16 KB
@@ -271,7 +260,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
       cld[u] = isx ? (uint32_t)p.kp : (uint32_t)p.ldy;
       cscale[u] = ((G.xmask >> (si & 7)) & 1) ? sx : sy;
     }
-    float4 ra[kBandDepth][4];
+    float4 ra[1][4];  // one register set of staged loads
     float csum[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
@@ -288,10 +277,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
         const bool rok = k0 + 2 * rp + r < kend;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          if constexpr (ACMI_BAND_PROBE & 4)
-            ra[set][2 * r + u] = make_float4((float)(k0 + r), (float)u, (float)lane, 1.f);
-          else
-            ra[set][2 * r + u] = stage_f4(cptr[u] + foff[u] + r * cld[u], rok && cok[u]);
+          ra[set][2 * r + u] = stage_f4(cptr[u] + foff[u] + r * cld[u], rok && cok[u]);
         }
       }
 #pragma unroll
@@ -306,28 +292,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
         const int q8 = 8 * (krow & 3);
         {
           const float4 v = ra[set][2 * r + u];
-          if constexpr (!(ACMI_BAND_PROBE & 2)) {
-            csum[4 * u] += v.x;
-            csum[4 * u + 1] += v.y;
-            csum[4 * u + 2] += v.z;
-            csum[4 * u + 3] += v.w;
-          }
+          csum[4 * u] += v.x;
+          csum[4 * u + 1] += v.y;
+          csum[4 * u + 2] += v.z;
+          csum[4 * u + 3] += v.w;
           uint2 h, l;
-          if constexpr (ACMI_BAND_PROBE & 1) {
-            h.x = __float_as_uint(v.x) ^ __float_as_uint(v.y);
-            h.y = __float_as_uint(v.z) ^ __float_as_uint(v.w);
-            l = h;
-          } else {
-            split2(v.x, v.y, cscale[u], h.x, l.x);
-            split2(v.z, v.w, cscale[u], h.y, l.y);
-          }
+          split2(v.x, v.y, cscale[u], h.x, l.x);
+          split2(v.z, v.w, cscale[u], h.y, l.y);
           const int off = 8 * ((64 * u + lane) ^ q8);  // 8-byte slot (4 columns) of column 4*(64u + lane)
-          if constexpr (ACMI_BAND_PROBE & 8) {
-            csum[4 * u] += __uint_as_float(h.x ^ l.y);
-          } else {
-            *reinterpret_cast<uint2*>(s + off) = h;
-            *reinterpret_cast<uint2*>(s + kBandPart + off) = l;
-          }
+          *reinterpret_cast<uint2*>(s + off) = h;
+          *reinterpret_cast<uint2*>(s + kBandPart + off) = l;
         }
       }
     };
@@ -368,7 +342,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
           for (int r = 0; r < 16; ++r) acc[t][a][b][r] = 0.f;
 
     using S0 = std::integral_constant<int, 0>;
-#if ACMI_BAND_PIPE
     // Software-pipelined fragment reads.  Each wave's sub-tiles of stage kt are
     // read from LDS one sub-tile AHEAD of their MFMAs, and the last sub-tile of a
     // stage is multiplied after the barrier, while the next stage's first
@@ -382,6 +355,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
     // sets: F[t] for tile t when a wave has two sub-tiles; by stage parity when
     // it has one.  Stages past the chunk end stage zeros (masked loads), so the
     // commit is unconditional and the trailing read is harmless.
+    // (Measured and removed: two 16-row stages per barrier over a ring of four
+    // LDS buffers -- half the barriers, bit-identical -- 0.66 vs 0.635 ms per
+    // conv2 launch; no stage prefetch depth or plain-order variant did better.)
     struct Frag {
       f16x8 a[2][2], b[2][2];  // [32-column block][part h, l]
     };
@@ -482,77 +458,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void b
     if (ntile == 0) prun(std::integral_constant<int, 0>{});
     else if (ntile == 1) prun(std::integral_constant<int, 1>{});
     else prun(std::integral_constant<int, 2>{});
-#else
-    if (nk > 0) {
-      fetch(kbeg, S0{});
-      fetch(kbeg + kBandRows, std::integral_constant<int, 1>{});
-      if constexpr (kBandDepth > 2) fetch(kbeg + 2 * kBandRows, std::integral_constant<int, 2 % kBandDepth>{});
-      commit(0, S0{});
-    }
-    __syncthreads();
-
-    auto tile = [&](const char* s, int t) {
-      f16x8 a[2][2], b[2][2];  // [32-column block][part h, l]
-#pragma unroll
-      for (int pt = 0; pt < 2; ++pt) {
-        const char* sp = s + pt * kBandPart;
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) {
-          if constexpr (ACMI_BAND_PROBE & 32) {
-            a[cb][pt] = b[cb][pt] = f16x8{(_Float16)(float)(aoff[t][cb] + pt), (_Float16)(float)cb, 0, 0, 0, 0, 0, 0};
-          } else {
-            a[cb][pt] = cat8h(ds_tr16(sp + aoff[t][cb]), ds_tr16(sp + aoff[t][cb] + 4 * kBandRowBytes));
-            b[cb][pt] = cat8h(ds_tr16(sp + boff[t][cb]), ds_tr16(sp + boff[t][cb] + 4 * kBandRowBytes));
-          }
-        }
-      }
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < 2; ++tn) {
-          f32x16 c = acc[t][tm][tn];
-          if constexpr (ACMI_BAND_PROBE & 16) {
-            c[0] += (float)a[tm][1][0] + (float)b[tn][0][1] + (float)a[tm][0][2] + (float)b[tn][1][3];
-          } else {
-            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][1], b[tn][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][0], b[tn][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[tm][0], b[tn][0], c, 0, 0, 0);
-          }
-          acc[t][tm][tn] = c;
-        }
-    };
-    // step kt: loads of kt + kBandDepth into the register set that held kt,
-    // tile 0 from stage kt, the commit of kt + 1 (its set) into the other LDS
-    // stage, tile 1, barrier.  I = kt mod the unroll (compile-time sets, stages).
-    constexpr int U = kBandDepth == 3 ? 6 : 2;
-    auto step = [&](int kt, auto I, auto NT) {
-      constexpr int nt = decltype(NT)::value;
-      constexpr int i = decltype(I)::value;
-      const int cur = i & 1;
-      const char* s = lds + cur * kBandBuf;
-      fetch(kbeg + (kt + kBandDepth) * kBandRows, std::integral_constant<int, i % kBandDepth>{});
-      if constexpr (nt >= 1) tile(s, 0);
-      if (kt + 1 < nk) commit(cur ^ 1, std::integral_constant<int, (i + 1) % kBandDepth>{});
-      if constexpr (nt >= 2) tile(s, 1);
-      __syncthreads();
-    };
-    auto run = [&](auto NT) {
-      for (int kt = 0; kt < nk; kt += U) {
-        step(kt, std::integral_constant<int, 0>{}, NT);
-        if (kt + 1 < nk) step(kt + 1, std::integral_constant<int, 1>{}, NT);
-        if constexpr (U > 2) {
-          if (kt + 2 < nk) step(kt + 2, std::integral_constant<int, 2>{}, NT);
-          if (kt + 3 < nk) step(kt + 3, std::integral_constant<int, 3>{}, NT);
-          if (kt + 4 < nk) step(kt + 4, std::integral_constant<int, 4>{}, NT);
-          if (kt + 5 < nk) step(kt + 5, std::integral_constant<int, 5>{}, NT);
-        }
-      }
-    };
-    if (ntile == 0) run(std::integral_constant<int, 0>{});
-    else if (ntile == 1) run(std::integral_constant<int, 1>{});
-    else run(std::integral_constant<int, 2>{});
-
-#endif
 
     // tiles, unscaled, into their compact slots of this chunk
     const int khalf = lane >> 5;

@@ -687,11 +687,6 @@ void tower_kernel(const uint8_t* obs, long long img_stride, const float* b1, con
                   const float* b3, float* a1g, float* a2g, float* a3g, long long st, const char* prep,
                   uint32_t* m1g, uint32_t* m2g, uint32_t* m3g) {
   __shared__ __attribute__((aligned(16))) char lds[kTowLds + kTowScr];
-#ifdef ACMI_TOWER_TWICE  // timing probe: the same image twice per block (instruction-fetch cost)
-  tower_body<C3, H16, false>(obs, img_stride, b1, b2, b3, a1g, a2g, a3g, st, prep, m1g, m2g, m3g, lds,
-                             blockIdx.x);
-  __syncthreads();
-#endif
   tower_body<C3, H16, false>(obs, img_stride, b1, b2, b3, a1g, a2g, a3g, st, prep, m1g, m2g, m3g, lds,
                              blockIdx.x);
 }

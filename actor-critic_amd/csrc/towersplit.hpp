@@ -147,9 +147,6 @@ __device__ __forceinline__ void tower_part_body(int j, const float* b1, const fl
     if (wave == 0) tile_out(4, [&](int r) { return acc[1][r] + scr[tow_row(r, lane) * 32 + col]; });
   }
   __syncthreads();
-#ifdef ACMI_SPLIT_STOP  // timing probe (wrong results): 1 stop after conv1, 2 after conv2
-  if constexpr (ACMI_SPLIT_STOP == 1) return;
-#endif
 
   // ---- conv2: a2 rows j .. j+2 (local pixel q2 = global - 9 j) -----------------
   {
@@ -208,9 +205,6 @@ __device__ __forceinline__ void tower_part_body(int j, const float* b1, const fl
     }
   }
   __syncthreads();
-#ifdef ACMI_SPLIT_STOP
-  if constexpr (ACMI_SPLIT_STOP == 2) return;
-#endif
 
   // ---- conv3: a3 row j (7 pixels) ------------------------------------------------
   {
