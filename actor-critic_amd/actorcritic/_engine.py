@@ -242,6 +242,21 @@ class NetEngine(object):
                   ctypes.byref(fwd.acts.struct), ctypes.byref(st.bwd), _lib.ptr(st.grads),
                   _lib.ptr(st.astat) if with_stats else None, _lib.ptr(st.bwd_ws), st.bwd_ws.numel(), self.stream())
 
+    def backward_stacked(self, fwd, st, sd, seed, counter):
+        """acmi_backward + the sampled-loss chain's input gradients into the side
+        buffers ``sd``, conv2's input gradient of both chains as one launch (on this
+        stream); output_stats_finish then forms the G factors."""
+        net = self.net()
+        _lib.call('acmi_backward_stacked', ctypes.byref(net), ctypes.c_void_p(fwd.obs.data_ptr()), OBS_BYTES, fwd.M,
+                  ctypes.byref(fwd.acts.struct), ctypes.byref(st.bwd), _lib.ptr(st.grads), _lib.ptr(st.astat),
+                  _lib.ptr(st.bwd_ws), st.bwd_ws.numel(), ctypes.byref(sd.bwd), seed, self.rank * fwd.M, counter,
+                  _lib.ptr(sd.ws), sd.ws.numel(), self.stream())
+
+    def output_stats_finish(self, fwd, st, sd):
+        net = self.net()
+        _lib.call('acmi_kfac_output_stats_finish', ctypes.byref(net), fwd.M, ctypes.byref(fwd.acts.struct),
+                  ctypes.byref(sd.bwd), _lib.ptr(st.gstat), _lib.ptr(sd.ws), sd.ws.numel(), self.stream())
+
     def output_stats(self, fwd, st, seed, counter, side=None):
         """side: run on UpdateState.side()'s stream and workspace (see there)."""
         net = self.net()
@@ -258,6 +273,9 @@ class NetEngine(object):
     # measured (ACKTR 512x20, one box): plain update 5.25 ms with the G chain started
     # next to the whole backward, 5.16 ms started after the backward's dX chain
     stats_after_dx = os.environ.get('ACMI_STATS_AFTER_DX', '1') != '0'
+    # on one stream (larger batches): the two chains' conv2 input gradients as one
+    # launch (acmi_backward_stacked; ACMI_STACKED_DX=0: the two calls)
+    stacked_dx = os.environ.get('ACMI_STACKED_DX', '1') != '0'
 
     def backward_and_stats(self, fwd, st, with_stats, seed, counter):
         """acmi_backward (+ A stats) and, with stats, acmi_kfac_output_stats (G stats);
@@ -265,6 +283,12 @@ class NetEngine(object):
         as it is enqueued and returns its handle (allreduce_end completes it).  With
         ``concurrent_stats`` the G chain runs on a side stream next to the backward."""
         conc = self.concurrent_stats if self.concurrent_stats is not None else fwd.M <= self.CONCURRENT_STATS_ROWS
+        if with_stats and not conc and self.stacked_dx:
+            sd = st.side(self)  # (its d1..d4 and workspace; the work stays on this stream)
+            self.backward_stacked(fwd, st, sd, seed, counter)
+            pending = self.allreduce_begin(st, True)
+            self.output_stats_finish(fwd, st, sd)
+            return pending
         if not (with_stats and conc):
             self.backward(fwd, st, with_stats)
             pending = self.allreduce_begin(st, with_stats)

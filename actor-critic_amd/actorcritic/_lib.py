@@ -100,7 +100,14 @@ _SIGS = {
                               ctypes.POINTER(Bwd), c_vp, c_vp, c_vp, c_i64, c_vp]),
     'acmi_kfac_output_stats': (c_int, [ctypes.POINTER(Net), c_int, ctypes.POINTER(Acts), ctypes.POINTER(Bwd),
                                        c_u32, c_u32, c_u32, c_vp, c_vp, c_i64, c_vp]),
+    'acmi_backward_stacked': (c_int, [ctypes.POINTER(Net), c_vp, c_i64, c_int, ctypes.POINTER(Acts),
+                                      ctypes.POINTER(Bwd), c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(Bwd), c_u32, c_u32,
+                                      c_u32, c_vp, c_i64, c_vp]),
+    'acmi_kfac_output_stats_finish': (c_int, [ctypes.POINTER(Net), c_int, ctypes.POINTER(Acts), ctypes.POINTER(Bwd),
+                                              c_vp, c_vp, c_i64, c_vp]),
     'acmi_debug_ws_flushes': (c_int, []),
+    'acmi_debug_convt2': (c_int, [ctypes.POINTER(Net), c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp]),
     'acmi_kfac_ema': (c_int, [c_vp, c_vp, c_vp, c_i64, c_float, c_float, c_float, c_vp]),
     'acmi_kfac_inverse_layout': (c_int, [c_int, c_int, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     'acmi_kfac_inverse_floats': (c_i64, [c_int, c_int]),

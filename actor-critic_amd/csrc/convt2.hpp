@@ -78,21 +78,42 @@ __device__ __forceinline__ void convt2_prep_body(const float* w2, char* out, int
   d[64] = l;
 }
 
-// MASK: a1 is the ReLU' bit words (acmi_acts_t m1) instead of the f32 activation
-template <bool GRAM, bool MASK = false>
+// MASK: a1 is the ReLU' bit words (acmi_acts_t m1) instead of the f32 activation.
+// MIX ("stacked"): the loss chain's and the sampled-loss chain's products as one
+// launch over both chains' tiles -- tiles [0, T) are the loss chain's (d2 scaled
+// by d2max, the STORE epilogue into d1), tiles [T, 2T) the sampled chain's (d2b
+// by d2bmax, the GRAM epilogue): one W2^T stream and one accumulator set per
+// wave, the epilogue chosen per tile; grid-stride over convt2_gram_blocks blocks.
+template <bool GRAM, bool MASK = false, bool MIX = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* __restrict__ a1,
                    float* __restrict__ d1, int B, float* __restrict__ gpart, const unsigned* d2max,
-                   unsigned* d1max) {
+                   unsigned* d1max, const float* __restrict__ d2b = nullptr, const unsigned* d2bmax = nullptr) {
   // 16 KB ring; the epilogue's transpose scratch (4 x 32 x 36 floats) reuses it
   __shared__ __attribute__((aligned(16))) char lds[std::max(2 * CT2::STEP_BYTES, 4 * 32 * 36 * 4)];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int J = B * CT2::L;
-  const int ntiles = (J + CT2::TILE - 1) / CT2::TILE;
+  const int ctiles = (J + CT2::TILE - 1) / CT2::TILE;  // tiles of one chain
+  // MIX: the sampled chain's tiles start at a multiple of the grid, so block b
+  // takes the same Gram tiles in the same order as the Gram launch (bit-identical
+  // partials); the slots [ctiles, gbase) are empty and skipped
+  const int G = gridDim.x;
+  const int gbase = MIX ? (ctiles + G - 1) / G * G : ctiles;
+  const int ntiles = MIX ? gbase + ctiles : ctiles;
+  auto valid_from = [&](int t) { return MIX && t >= ctiles && t < gbase ? t + G : t; };  // (gap < G)
   const int hl = lane >> 5;  // k half of the fragment; row offset 4 of the accumulator
   const float* zero = zero_run();
-  const float sd = f16x2_scale_of_bits(d2max);
-  const float inv = 1.f / (f16x2_scale_of_bits(reinterpret_cast<const unsigned*>(prep + CT2::FRAG_BYTES)) * sd);
+  const float sd_a = f16x2_scale_of_bits(d2max);
+  const float sw = f16x2_scale_of_bits(reinterpret_cast<const unsigned*>(prep + CT2::FRAG_BYTES));
+  const float inv_a = 1.f / (sw * sd_a);
+  float sd_b = sd_a, inv_b = inv_a;
+  if constexpr (MIX) {
+    sd_b = f16x2_scale_of_bits(d2bmax);
+    inv_b = 1.f / (sw * sd_b);
+  }
+  // a tile of the sampled chain (GRAM epilogue), its index within its chain
+  auto gram_tile = [&](int tile) { return MIX ? tile >= gbase : GRAM; };
+  auto local_tile = [&](int tile) { return MIX && tile >= gbase ? tile - gbase : tile; };
 
   float d1am = 0.f;  // !GRAM: max |d1| over the lane's stores, published once at the end
   f32x16 gacc;  // GRAM: this wave's D D^T over its tiles
@@ -107,14 +128,14 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
   };
   auto col_of = [&](int tile) {
     Col c;
-    const int j = tile * CT2::TILE + 32 * wave + (lane & 31);
+    const int j = local_tile(tile) * CT2::TILE + 32 * wave + (lane & 31);
     c.ok = j < J;
     const int jj = c.ok ? j : 0;
     c.n = jj / CT2::L;
     const int sp = jj - c.n * CT2::L;
     c.Y = sp / CT2::PW;
     c.X = sp - c.Y * CT2::PW;
-    c.dimg = d2 + (long long)c.n * (CT2::OH * CT2::OW * CT2::COUT);
+    c.dimg = (MIX && gram_tile(tile) ? d2b : d2) + (long long)c.n * (CT2::OH * CT2::OW * CT2::COUT);
     return c;
   };
   // lane's B fragment for k-step ks: dY pixel (Y - a, X - b), channels co..co+7.
@@ -145,16 +166,19 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
   // two B register sets, alternating by k-step parity (named, never indexed at
   // run time: a dynamically indexed register array lands in scratch)
   float4 bx0[2], bx1[2];
-  Col cur = col_of(blockIdx.x);
+  const int first = valid_from(blockIdx.x);
+  Col cur = col_of(min(first, ntiles - 1));
   afetch(0);
   bload(0, cur, bx0);
 
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int tile = first; tile < ntiles; tile = valid_from(tile + G)) {
     // step 0's operands were loaded before the loop or during the previous
     // tile's last k-step (its A is the same for every tile)
-    const Col nextc = col_of(min(tile + (int)gridDim.x, ntiles - 1));
+    const Col nextc = col_of(min(valid_from(tile + G), ntiles - 1));
     const bool jok = cur.ok;
     const int n = cur.n, Y = cur.Y, X = cur.X;
+    const bool gt = gram_tile(tile);
+    const float sd = MIX && gt ? sd_b : sd_a, inv = MIX && gt ? inv_b : inv_a;
     acommit(0);
     __syncthreads();
 
@@ -205,7 +229,7 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
 
     // epilogue: rows (phase p, ci) x this wave's 32 super-pixel columns
     float* scr = reinterpret_cast<float*>(lds) + wave * 32 * 36;  // [32][36] per wave
-    if constexpr (!GRAM) {
+    if (!gt) {
       // ReLU'-masked d1 through the LDS transpose (each store instruction writes 8
       // whole 128-byte pixel rows): after it, lane (ri = 4 (lane & 7), cj = lane >> 3)
       // holds channels ri .. ri+3 of super-pixel columns cj + 8 q (q < 4) of each
@@ -217,7 +241,7 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
       bool jok[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int j = tile * CT2::TILE + 32 * wave + cj + 8 * q;
+        const int j = local_tile(tile) * CT2::TILE + 32 * wave + cj + 8 * q;
         jok[q] = j < J;
         const int jj = jok[q] ? j : 0;
         const int nn = jj / CT2::L, sp = jj - nn * CT2::L;
@@ -313,8 +337,8 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
     __syncthreads();  // the ring / scratch is reused by the next tile
   }
 
-  if constexpr (!GRAM) amax_publish(d1max, d1am, lane);
-  if constexpr (GRAM) {
+  if constexpr (MIX || !GRAM) amax_publish(d1max, d1am, lane);
+  if constexpr (MIX || GRAM) {
     // the 4 waves' Grams summed in wave order through LDS, then part[block][33][32]
     float* red = reinterpret_cast<float*>(lds);  // [32][32]
     for (int w = 0; w < 4; ++w) {
@@ -332,6 +356,13 @@ void convt2_kernel(const char* prep, const float* __restrict__ d2, const float* 
   }
 }
 
+#ifndef ACMI_CT2_STORE_BLOCKS  // 0: one block per tile; else at most this many blocks (grid-stride)
+#define ACMI_CT2_STORE_BLOCKS 0
+#endif
+inline int convt2_store_blocks(int B) {
+  const int ntiles = (B * CT2::L + CT2::TILE - 1) / CT2::TILE;
+  return ACMI_CT2_STORE_BLOCKS > 0 ? std::max(1, std::min(ntiles, ACMI_CT2_STORE_BLOCKS)) : ntiles;
+}
 // blocks of the Gram variant (per-block partials, finalize_cov_kernel sums them)
 inline int convt2_gram_blocks(int B) {
   const int ntiles = (B * CT2::L + CT2::TILE - 1) / CT2::TILE;

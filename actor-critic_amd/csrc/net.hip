@@ -1407,18 +1407,17 @@ static hipEvent_t* dx_done_event() {
 // ---------------------------------------------------------------------------
 // backward (dX chain) shared by the loss backward and the sampled backward
 // ---------------------------------------------------------------------------
+// the chain up to d2: heads -> d4, fc4 -> d3, conv3 -> d2
 template <int C3>
-static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a,
-                    const acmi_bwd_t* bw, const float* dhead, int ldh,
-                    hipStream_t s, const char* prep = nullptr, float* gram_part = nullptr,
-                    bool* gram_done = nullptr, unsigned* dxs = nullptr) {
+static int dx_chain_pre(const Layout& L, const float* P, int B, const acmi_acts_t* a,
+                        const acmi_bwd_t* bw, const float* dhead, int ldh,
+                        hipStream_t s, const char* prep, unsigned* dxs) {
   // dxs: kBandScratch words of scratch (band.hpp layout): the dX epilogues publish
   // max |d3|, |d2| there, the f16x2 consumers (convt2, the band reductions) scale
   // by them
   ACMI_REQUIRE(dxs, ACMI_ERR_ARG, "dx_chain: no scratch");
   ACMI_REQUIRE(hipMemsetAsync(dxs, 0, kBandScratch * sizeof(unsigned), s) == hipSuccess, ACMI_ERR_HIP,
                "dx_chain: scratch reset failed");
-  if (gram_done) *gram_done = false;
   // heads -> d4 = (dhead W_h^T) * relu'(a4)
   if (L.A == 4 && ldh % 4 == 0 && (uintptr_t)(P + L.off[8]) % 16 == 0 && (uintptr_t)dhead % 16 == 0)
     hipLaunchKernelGGL(heads_dx4_kernel, dim3(cdiv((long long)B * 128, 256)), dim3(256), 0, s, dhead,
@@ -1472,6 +1471,17 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     if (a->m2) run(EpiConvT<9, 9, 1, 64, true>{bw->d2, reinterpret_cast<const float*>(a->m2), dxs + kBsMaxD2});
     else run(EpiConvT<9, 9, 1, 64>{bw->d2, a->a2, dxs + kBsMaxD2});
   }
+  ACMI_LAUNCH_CHECK("dx_chain");
+  return ACMI_OK;
+}
+
+// conv2's input gradient, from d2 (max |d2| in dxs): the loss chain stores the
+// masked d1 (gram_part null), the sampled chain reduces it to conv1's G-factor
+// Gram partials (*gram_done set when it did)
+template <int C3>
+static int dx_conv2(const Layout& L, const float* P, int B, const acmi_acts_t* a, const acmi_bwd_t* bw,
+                    hipStream_t s, const char* prep, float* gram_part, bool* gram_done, unsigned* dxs) {
+  if (gram_done) *gram_done = false;
   {  // conv2 -> d1 (stride 2: the four phases of a 2x2 super-pixel are the
      // 4 x 32 rows of one product over the 10x10 super-pixels)
     using Src = ConvTRows<20, 20, 4, 4, 2, 64>;
@@ -1491,7 +1501,7 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
           hipLaunchKernelGGL((convt2_kernel<GR, MK>), dim3(convt2_gram_blocks(B)), dim3(256), 0, s, p2, bw->d2,
                              act1, nullptr, B, gram_part, dxs + kBsMaxD2, nullptr);
         else
-          hipLaunchKernelGGL((convt2_kernel<GR, MK>), dim3(cdiv(B * CT2::L, CT2::TILE)), dim3(256), 0, s, p2,
+          hipLaunchKernelGGL((convt2_kernel<GR, MK>), dim3(convt2_store_blocks(B)), dim3(256), 0, s, p2,
                              bw->d2, act1, bw->d1, B, nullptr, dxs + kBsMaxD2, dxs + kBsMaxD1);
       };
       using T = std::true_type;
@@ -1513,15 +1523,27 @@ static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a
     }
     prof_end(ACMI_PROF_CONV2_DX, s);
   }
-  ACMI_LAUNCH_CHECK("dx_chain");
+  ACMI_LAUNCH_CHECK("dx_conv2");
   return ACMI_OK;
+}
+
+template <int C3>
+static int dx_chain(const Layout& L, const float* P, int B, const acmi_acts_t* a,
+                    const acmi_bwd_t* bw, const float* dhead, int ldh,
+                    hipStream_t s, const char* prep = nullptr, float* gram_part = nullptr,
+                    bool* gram_done = nullptr, unsigned* dxs = nullptr) {
+  const int rc = dx_chain_pre<C3>(L, P, B, a, bw, dhead, ldh, s, prep, dxs);
+  if (rc) return rc;
+  return dx_conv2<C3>(L, P, B, a, bw, s, prep, gram_part, gram_done, dxs);
 }
 
 template <int C3>
 static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
                          long long img_stride, int B, const acmi_acts_t* a,
                          const acmi_bwd_t* bw, float* grads, float* astat,
-                         float* ws, long long ws_cap, hipStream_t s, const char* prep) {
+                         float* ws, long long ws_cap, hipStream_t s, const char* prep,
+                         bool dx_done = false) {
+  // dx_done: the caller ran the dX chain into bw / the scratch (backward_stacked_impl)
   const bool st = astat != nullptr;
   // conv1's weight gradient is fused into the A-factor pass (bf16x3 mode; it needs
   // d1, so the pass follows the dX chain).  (Measured and removed: the A factor on a
@@ -1536,9 +1558,10 @@ static int backward_impl(const Layout& L, const float* P, const uint8_t* obs,
   float* part = ws + prefix;
   const long long avail = ws_cap - prefix;
   const bool band = band_on(st);
-  int rc = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s, prep, nullptr, nullptr, bscr);
-  if (rc) return rc;
-  {
+  int rc = ACMI_OK;
+  if (!dx_done) {
+    rc = dx_chain<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s, prep, nullptr, nullptr, bscr);
+    if (rc) return rc;
     hipEvent_t* ev = dx_done_event();
     ACMI_REQUIRE(ev && hipEventRecord(*ev, s) == hipSuccess, ACMI_ERR_HIP, "acmi_backward: dX event record failed");
   }
@@ -1675,7 +1698,9 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
                              const acmi_acts_t* a, const acmi_bwd_t* bw,
                              uint32_t seed, uint32_t row0, uint32_t ctr,
                              float* gstat, float* ws, long long ws_cap,
-                             hipStream_t s, const char* prep) {
+                             hipStream_t s, const char* prep, int stage = 0) {
+  // stage: 0 the whole chain; 2 only the G factors, from what backward_stacked_impl
+  // left in bw (d2..d4) and in this workspace (scratch maxima, conv1's Gram partials)
   const int ldg = (int)head_grad_ldg(L.A);
   // [the dX chain's scratch (operand-scale maxima) | ghead [B][ldg] | partials]
   unsigned* dxs = reinterpret_cast<unsigned*>(ws);
@@ -1683,12 +1708,17 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
   const long long prefix = stats_prefix_floats(B, L.A);
   float* part = ws + prefix;
   const long long cap = ws_cap - prefix;
-  hipLaunchKernelGGL(sampled_head_grad_kernel, dim3(cdiv(B, 128)), dim3(128), 0, s,
-                     a->logits, a->ld_logits, B, L.A, seed, row0, ctr, ghead, ldg);
   bool g1_done = false;
   const bool g1_fits = (long long)convt2_gram_blocks(B) * 33 * 32 <= cap;
-  int rc = dx_chain<C3>(L, P, B, a, bw, ghead, ldg, s, prep, g1_fits ? part : nullptr, &g1_done, dxs);
-  if (rc) return rc;
+  int rc = ACMI_OK;
+  if (stage == 0) {
+    hipLaunchKernelGGL(sampled_head_grad_kernel, dim3(cdiv(B, 128)), dim3(128), 0, s,
+                       a->logits, a->ld_logits, B, L.A, seed, row0, ctr, ghead, ldg);
+    rc = dx_chain<C3>(L, P, B, a, bw, ghead, ldg, s, prep, g1_fits ? part : nullptr, &g1_done, dxs);
+    if (rc) return rc;
+  } else {
+    g1_done = g1_fits && prep && g_gemm_mode == ACMI_GEMM_X3;  // (dx_conv2's Gram predicate)
+  }
   // the G factors' finalizes deferred into one launch: every Gram's partials in
   // their own range of the workspace (while they fit; else the set so far is
   // finalized and the ranges start over)
@@ -1732,6 +1762,56 @@ static int output_stats_impl(const Layout& L, const float* P, int B,
   flush();
   ACMI_LAUNCH_CHECK("G factor finalize");
   return ACMI_OK;
+}
+
+// acmi_backward + the input-gradient half of acmi_kfac_output_stats, with conv2's
+// input gradient of both chains as ONE launch (convt2_kernel MIX: one W2^T
+// stream, the loss chain's tiles storing d1, the sampled chain's reducing
+// conv1's G-factor Gram); the G factors follow in output_stats_impl stage 2.
+// Bit-identical to the two calls.
+template <int C3>
+static int backward_stacked_impl(const Layout& L, const float* P, const uint8_t* obs, long long img_stride, int B,
+                                 const acmi_acts_t* a, const acmi_bwd_t* bw, float* grads, float* astat, float* ws,
+                                 long long ws_cap, const acmi_bwd_t* bws, uint32_t seed, uint32_t row0, uint32_t ctr,
+                                 float* wss, long long wss_cap, hipStream_t s, const char* prep) {
+  unsigned* bscr = reinterpret_cast<unsigned*>(ws);
+  int rc = dx_chain_pre<C3>(L, P, B, a, bw, bw->dhead, bw->ldh, s, prep, bscr);
+  if (rc) return rc;
+  // the sampled chain's head gradients and its chain up to d2 (output_stats_impl's layout)
+  const int ldg = (int)head_grad_ldg(L.A);
+  unsigned* dxs = reinterpret_cast<unsigned*>(wss);
+  float* ghead = wss + kBandScratch;
+  float* part_s = wss + stats_prefix_floats(B, L.A);
+  const long long cap_s = wss_cap - stats_prefix_floats(B, L.A);
+  hipLaunchKernelGGL(sampled_head_grad_kernel, dim3(cdiv(B, 128)), dim3(128), 0, s, a->logits, a->ld_logits, B, L.A,
+                     seed, row0, ctr, ghead, ldg);
+  rc = dx_chain_pre<C3>(L, P, B, a, bws, ghead, ldg, s, prep, dxs);
+  if (rc) return rc;
+  const bool g1_fits = (long long)convt2_gram_blocks(B) * 33 * 32 <= cap_s;
+  if (prep && g_gemm_mode == ACMI_GEMM_X3 && g1_fits) {
+    const char* p2 = prep + TowerPrep<C3>::BYTES;
+    const float* act1 = a->m1 ? reinterpret_cast<const float*>(a->m1) : a->a1;
+    prof_begin(ACMI_PROF_CONV2_DX, s);
+    if (a->m1)
+      hipLaunchKernelGGL((convt2_kernel<true, true, true>), dim3(convt2_gram_blocks(B)), dim3(256), 0, s, p2, bw->d2,
+                         act1, bw->d1, B, part_s, bscr + kBsMaxD2, bscr + kBsMaxD1, bws->d2, dxs + kBsMaxD2);
+    else
+      hipLaunchKernelGGL((convt2_kernel<true, false, true>), dim3(convt2_gram_blocks(B)), dim3(256), 0, s, p2, bw->d2,
+                         act1, bw->d1, B, part_s, bscr + kBsMaxD2, bscr + kBsMaxD1, bws->d2, dxs + kBsMaxD2);
+    prof_end(ACMI_PROF_CONV2_DX, s);
+    ACMI_LAUNCH_CHECK("stacked conv2 dX");
+  } else {  // the two launches (no prepared weights / f32 mode / a workspace without room for the Gram)
+    rc = dx_conv2<C3>(L, P, B, a, bw, s, prep, nullptr, nullptr, bscr);
+    if (rc) return rc;
+    bool g1_done = false;
+    rc = dx_conv2<C3>(L, P, B, a, bws, s, prep, g1_fits ? part_s : nullptr, &g1_done, dxs);
+    if (rc) return rc;
+  }
+  {
+    hipEvent_t* ev = dx_done_event();
+    ACMI_REQUIRE(ev && hipEventRecord(*ev, s) == hipSuccess, ACMI_ERR_HIP, "acmi_backward: dX event record failed");
+  }
+  return backward_impl<C3>(L, P, obs, img_stride, B, a, bw, grads, astat, ws, ws_cap, s, prep, true);
 }
 
 }  // namespace acmi
@@ -2021,6 +2101,54 @@ int acmi_backward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride,
                            ws_floats, s, static_cast<const char*>(net->conv_prep));
 }
 
+int acmi_backward_stacked(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,
+                          const acmi_acts_t* acts, const acmi_bwd_t* bwd, float* grads, float* a_stats,
+                          float* ws, int64_t ws_floats, const acmi_bwd_t* bwd_s, uint32_t seed,
+                          uint32_t row_offset, uint32_t counter, float* ws_s, int64_t ws_s_floats,
+                          acmi_stream_t stream) {
+  Layout L;
+  ACMI_REQUIRE(net && acts && bwd && bwd_s && grads && a_stats && ws && ws_s && obs, ACMI_ERR_ARG,
+               "acmi_backward_stacked: null argument");
+  ACMI_REQUIRE(masks_ok(acts), ACMI_ERR_ARG, "acmi_backward_stacked: ReLU masks m1..m3 must be all set or all NULL");
+  ACMI_REQUIRE(make_layout(net->num_actions, net->conv3_filters, &L), ACMI_ERR_ARG, "acmi_backward_stacked: bad net");
+  ACMI_REQUIRE(B > 0 && img_stride >= 84 * 84 * 4 && img_stride % 4 == 0, ACMI_ERR_ARG,
+               "acmi_backward_stacked: bad B / img_stride");
+  ACMI_REQUIRE(bwd->ldh >= net->num_actions + 1 && bwd->ldh % 4 == 0, ACMI_ERR_ARG,
+               "acmi_backward_stacked: ldh must be >= A+1 and a multiple of 4 (zero padded)");
+  ACMI_REQUIRE(spans32(B, img_stride, 84 * 84 * 4) && spans32(B, 400 * 32, 400 * 32), ACMI_ERR_ARG,
+               "acmi_backward_stacked: batch spans >= 2^31 elements (B=%d)", B);
+  ACMI_REQUIRE(ws != ws_s && bwd->d1 != bwd_s->d1 && bwd->d2 != bwd_s->d2 && bwd->d3 != bwd_s->d3 &&
+                   bwd->d4 != bwd_s->d4,
+               ACMI_ERR_ARG, "acmi_backward_stacked: the two chains need their own workspaces and d1..d4");
+  const long long need = acmi_backward_ws_floats(B, net->num_actions, net->conv3_filters);
+  ACMI_REQUIRE(ws_floats >= need && ws_s_floats >= need, ACMI_ERR_WS,
+               "acmi_backward_stacked: workspaces of %lld / %lld floats < %lld", (long long)ws_floats,
+               (long long)ws_s_floats, need);
+  hipStream_t s = (hipStream_t)stream;
+  const char* prep = static_cast<const char*>(net->conv_prep);
+  if (L.C3 == 32)
+    return backward_stacked_impl<32>(L, net->params, obs, img_stride, B, acts, bwd, grads, a_stats, ws, ws_floats,
+                                     bwd_s, seed, row_offset, counter, ws_s, ws_s_floats, s, prep);
+  return backward_stacked_impl<64>(L, net->params, obs, img_stride, B, acts, bwd, grads, a_stats, ws, ws_floats,
+                                   bwd_s, seed, row_offset, counter, ws_s, ws_s_floats, s, prep);
+}
+
+int acmi_kfac_output_stats_finish(const acmi_net_t* net, int B, const acmi_acts_t* acts, const acmi_bwd_t* bwd_s,
+                                  float* g_stats, float* ws_s, int64_t ws_s_floats, acmi_stream_t stream) {
+  Layout L;
+  ACMI_REQUIRE(net && acts && bwd_s && g_stats && ws_s, ACMI_ERR_ARG, "acmi_kfac_output_stats_finish: null argument");
+  ACMI_REQUIRE(make_layout(net->num_actions, net->conv3_filters, &L), ACMI_ERR_ARG, "bad net");
+  ACMI_REQUIRE(B > 0 && spans32(B, 400 * 32, 400 * 32), ACMI_ERR_ARG, "bad B");
+  const long long need = acmi_backward_ws_floats(B, net->num_actions, net->conv3_filters);
+  ACMI_REQUIRE(ws_s_floats >= need, ACMI_ERR_WS, "acmi_kfac_output_stats_finish: workspace of %lld floats < %lld",
+               (long long)ws_s_floats, need);
+  hipStream_t s = (hipStream_t)stream;
+  const char* prep = static_cast<const char*>(net->conv_prep);
+  if (L.C3 == 32)
+    return output_stats_impl<32>(L, net->params, B, acts, bwd_s, 0, 0, 0, g_stats, ws_s, ws_s_floats, s, prep, 2);
+  return output_stats_impl<64>(L, net->params, B, acts, bwd_s, 0, 0, 0, g_stats, ws_s, ws_s_floats, s, prep, 2);
+}
+
 int acmi_stream_wait_backward_dx(acmi_stream_t stream) {
   hipEvent_t* ev = dx_done_event();
   ACMI_REQUIRE(ev && hipStreamWaitEvent((hipStream_t)stream, *ev, 0) == hipSuccess, ACMI_ERR_HIP,
@@ -2095,6 +2223,28 @@ int acmi_prof_collect(double* total_ms, int* count) {
 // upper triangle of P^T P and every (P, dY) sub-tile is produced by sym_plan's
 // groups, each column's sum by exactly one wave, for K = 64..max_k; and
 // plan_rounds' chunks cover the rows exactly.  0 = ok, else the failing K.
+int acmi_debug_convt2(const acmi_net_t* net, int mode, const float* d2a, const float* d2b, const uint32_t* m1,
+                      float* d1, int B, float* gram_part, const uint32_t* d2max_a, const uint32_t* d2max_b,
+                      uint32_t* d1max, acmi_stream_t stream) {
+  ACMI_REQUIRE(net && net->conv_prep && d2a && d2b && m1 && d1 && gram_part && d2max_a && d2max_b && d1max && B > 0,
+               ACMI_ERR_ARG, "acmi_debug_convt2: bad arguments");
+  const char* p2 = static_cast<const char*>(net->conv_prep) +
+                   (net->conv3_filters == 32 ? TowerPrep<32>::BYTES : TowerPrep<64>::BYTES);
+  hipStream_t s = (hipStream_t)stream;
+  const float* act1 = reinterpret_cast<const float*>(m1);
+  if (mode == 0) {
+    hipLaunchKernelGGL((convt2_kernel<false, true>), dim3(convt2_store_blocks(B)), dim3(256), 0, s, p2, d2a, act1, d1,
+                       B, nullptr, d2max_a, d1max, nullptr, nullptr);
+    hipLaunchKernelGGL((convt2_kernel<true, true>), dim3(convt2_gram_blocks(B)), dim3(256), 0, s, p2, d2b, act1,
+                       nullptr, B, gram_part, d2max_b, nullptr, nullptr, nullptr);
+  } else {
+    hipLaunchKernelGGL((convt2_kernel<true, true, true>), dim3(convt2_gram_blocks(B)), dim3(256), 0, s, p2, d2a,
+                       act1, d1, B, gram_part, d2max_a, d1max, d2b, d2max_b);
+  }
+  ACMI_LAUNCH_CHECK("acmi_debug_convt2");
+  return ACMI_OK;
+}
+
 int acmi_debug_ws_flushes(void) {
   const int n = g_ws_flushes;
   g_ws_flushes = 0;

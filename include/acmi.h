@@ -339,6 +339,28 @@ int acmi_kfac_output_stats(const acmi_net_t* net, int B,
                            uint32_t seed, uint32_t row_offset, uint32_t counter,
                            float* g_stats, float* ws, int64_t ws_floats,
                            acmi_stream_t stream);
+/* acmi_backward + the input-gradient half of acmi_kfac_output_stats in one
+ * call, with conv2's input gradient of BOTH chains as one launch (one W2^T
+ * stream over the loss chain's and the sampled chain's image rows, the
+ * epilogue chosen per tile: the masked d1 store, or conv1's G-factor Gram).
+ * bwd / ws: the loss chain's (as acmi_backward); bwd_s / ws_s: the sampled
+ * chain's own d1..d4 and workspace (ws_floats, ws_s_floats >=
+ * acmi_backward_ws_floats), on which acmi_kfac_output_stats_finish then forms
+ * the G factors.  The pair is bit-identical to acmi_backward followed by
+ * acmi_kfac_output_stats(bwd_s, ws_s) with the same seed / row_offset /
+ * counter, and records the same dX event.  Without net->conv_prep or in
+ * ACMI_GEMM_F32 mode the two conv2 launches run one after the other.
+ * Reference: the same graphs as acmi_backward / acmi_kfac_output_stats
+ * (objectives.py:78-79, policies.py:157-158). */
+int acmi_backward_stacked(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride,
+                          int B, const acmi_acts_t* acts, const acmi_bwd_t* bwd,
+                          float* grads, float* a_stats, float* ws, int64_t ws_floats,
+                          const acmi_bwd_t* bwd_s, uint32_t seed, uint32_t row_offset,
+                          uint32_t counter, float* ws_s, int64_t ws_s_floats,
+                          acmi_stream_t stream);
+int acmi_kfac_output_stats_finish(const acmi_net_t* net, int B, const acmi_acts_t* acts,
+                                  const acmi_bwd_t* bwd_s, float* g_stats, float* ws_s,
+                                  int64_t ws_s_floats, acmi_stream_t stream);
 /* Makes `stream` wait (stream-ordered, no host sync) for the point right after
  * the input-gradient chain of the most recent acmi_backward on this device, so
  * a sampled-loss chain (acmi_kfac_output_stats on its own buffers) enqueued on
@@ -564,6 +586,16 @@ int acmi_selftest_plans(int max_k);
  * split-K partials did not fit in the rest of the workspace (a legal size near
  * the minimum), since the previous call of this function (which resets it). */
 int acmi_debug_ws_flushes(void);
+/* Diagnostic (same-lease A/B of conv2's input gradient in the two K-FAC chains):
+ * mode 0 = the two launches of acmi_backward / acmi_kfac_output_stats (the
+ * loss chain's d2a -> masked d1 with max |d1| into d1max; the sampled chain's
+ * d2b -> conv1's G-factor Gram partials); mode 1 = the same products stacked in
+ * one launch (one W2^T stream, the epilogue chosen per tile).  d2max_*: the
+ * published max |d2| slots; m1: the ReLU' mask words; needs net->conv_prep. */
+int acmi_debug_convt2(const acmi_net_t* net, int mode, const float* d2a, const float* d2b,
+                      const uint32_t* m1, float* d1, int B, float* gram_part,
+                      const uint32_t* d2max_a, const uint32_t* d2max_b, uint32_t* d1max,
+                      acmi_stream_t stream);
 
 /* C[M][N] = A[M][K] @ B[K][N], row-major fp32, f32-input MFMA */
 int acmi_gemm_f32(const float* A, const float* B, float* C, int M, int N,

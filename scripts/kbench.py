@@ -63,6 +63,79 @@ def backward(M, with_stats=True, site=1, reps=10):
         M, with_stats, ms, site, tot.value / max(1, cnt.value), cnt.value))
 
 
+def stats_chain(M, reps=10):
+    """conv2 dX of the sampled-loss chain (site 5 inside acmi_kfac_output_stats: the
+    Gram epilogue), then of backward + output stats together (both epilogues)"""
+    from actorcritic._engine import NetEngine
+    eng = NetEngine(4, 32)
+    obs = torch.randint(0, 256, (M, 84, 84, 4), dtype=torch.uint8, device='cuda')
+    acts = eng.activations(M)
+    eng.forward(obs.data_ptr(), M, acts.struct)
+    st = eng.update_state(M)
+    st.dhead.normal_()
+    st.dhead[:, 5:] = 0
+
+    class F:
+        pass
+    f = F()
+    f.obs, f.M, f.acts = obs, M, acts
+    eng.backward(f, st, True)
+    for name, fn in (('stats', lambda: eng.output_stats(f, st, 7, 3)),
+                     ('backward+stats', lambda: (eng.backward(f, st, True), eng.output_stats(f, st, 7, 3)))):
+        _lib.call('acmi_prof_enable', 5, 64)
+        ms = timeit(fn, reps=reps, warm=2)
+        tot, cnt = ctypes.c_double(), ctypes.c_int()
+        _lib.call('acmi_prof_collect', ctypes.byref(tot), ctypes.byref(cnt))
+        _lib.call('acmi_prof_enable', 0, 0)
+        print('{} M={}: {:.3f} ms; conv2 dX kernel avg {:.3f} ms over {} (sum per call {:.3f})'.format(
+            name, M, ms, tot.value / max(1, cnt.value), cnt.value, tot.value / (reps + 2)))
+
+
+def c2mix(M, reps=20):
+    """conv2 dX of both K-FAC chains: the two launches of today (mode 0) against
+    the stacked launch (mode 1, acmi_debug_convt2), same lease, HIP events; and
+    the outputs (masked d1, max |d1|, Gram partials) compared bit for bit"""
+    from actorcritic._engine import NetEngine
+    K_AMAX = 64 * 64  # kAmaxWords
+    eng = NetEngine(4, 32)
+    obs = torch.randint(0, 256, (M, 84, 84, 4), dtype=torch.uint8, device='cuda')
+    acts = eng.activations(M)
+    eng.forward(obs.data_ptr(), M, acts.struct)
+    st = eng.update_state(M)
+    st.dhead.normal_()
+    st.dhead[:, 5:] = 0
+
+    class F:
+        pass
+    f = F()
+    f.obs, f.M, f.acts = obs, M, acts
+    sd = st.side(eng)
+    eng.backward(f, st, True)
+    eng.output_stats(f, st, 7, 3, side=sd)
+    torch.cuda.synchronize()
+    net = eng.net()
+    m1 = ctypes.c_void_p(acts.struct.m1)
+    d2max_a = st.bwd_ws[2 * K_AMAX:3 * K_AMAX]  # band scratch kBsMaxD2 (workspace prefix)
+    d2max_b = sd.ws[2 * K_AMAX:3 * K_AMAX]
+    nb = 768
+    outs = {}
+    for mode in (0, 1):
+        d1 = torch.zeros_like(st.d1)
+        gp = torch.zeros(nb * 33 * 32, device='cuda')
+        d1max = torch.zeros(K_AMAX, dtype=torch.int32, device='cuda')
+        run = lambda: _lib.call('acmi_debug_convt2', ctypes.byref(net), mode, _lib.ptr(st.d2), _lib.ptr(sd.d2), m1,
+                                _lib.ptr(d1), M, _lib.ptr(gp), _lib.ptr(d2max_a), _lib.ptr(d2max_b),
+                                _lib.ptr(d1max), _lib.stream_handle())
+        run()
+        torch.cuda.synchronize()
+        outs[mode] = (d1.clone(), gp.clone(), d1max.max().item())
+        ms = timeit(run, reps=reps, warm=3)
+        print('conv2 dX both chains, mode {} ({}): {:.1f} us'.format(mode, 'two launches' if mode == 0 else 'stacked',
+                                                                     1e3 * ms))
+    print('bit-identical: d1', torch.equal(outs[0][0], outs[1][0]), 'gram', torch.equal(outs[0][1], outs[1][1]),
+          'max|d1|', outs[0][2] == outs[1][2])
+
+
 def inverse(A=4, C3=32, reps=10):
     lib = _lib.load()
     din = (ctypes.c_int64 * 6)()
@@ -120,6 +193,10 @@ if __name__ == '__main__':
         inverse()
     elif what == 'gemm':
         gemm(int(sys.argv[2]) if len(sys.argv) > 2 else 4096)
+    elif what == 'c2mix':
+        c2mix(int(sys.argv[2]) if len(sys.argv) > 2 else 10240)
+    elif what == 'c2g':  # conv2 dX site of the sampled-loss chain (Gram epilogue) and of both chains
+        stats_chain(int(sys.argv[2]) if len(sys.argv) > 2 else 10240)
     elif what == 'c2':  # conv2 dX site (ACMI_PROF_CONV2_DX = 5)
         backward(int(sys.argv[2]) if len(sys.argv) > 2 else 10240, False, 5, reps=10)
     elif what == 'backward1x':  # the conv2 band launch alone (site 2), ten timed reps

@@ -210,6 +210,65 @@ def test_backward_workspace_contract(lib, cuda, C3, B):
         assert torch.equal(torch.nan_to_num(a), torch.nan_to_num(b))
 
 
+@pytest.mark.parametrize('B,use_prep,masks', [(700, True, True), (700, True, False), (24, True, True),
+                                               (24, False, True)], ids=['700-stacked', '700-stacked-nomask',
+                                                                        '24-stacked', '24-no-prep'])
+def test_backward_stacked_bit_identical_to_two_calls(lib, cuda, B, use_prep, masks):
+    """acmi_backward_stacked + acmi_kfac_output_stats_finish (conv2's input gradient
+    of the loss and the sampled-loss chain as ONE launch, convt2_kernel MIX) equal
+    acmi_backward + acmi_kfac_output_stats bit for bit: gradients, A and G
+    factors, the loss chain's d1..d4 and the sampled chain's d2..d4.  Without
+    prepared weights the stacked call runs the two conv2 launches itself.
+    Reference: objectives.py:78-79, policies.py:157-158 (the two graphs)."""
+    A, C3 = 4, 32
+    g = torch.Generator().manual_seed(41)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
+    params = rand_params(A, C3, cuda, seed=6)
+    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
+    net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr() if use_prep else None)
+    if use_prep:
+        _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), _lib.stream_handle())
+    ldh = 8
+    dhead = torch.zeros(B, ldh)
+    dhead[:, :A + 1] = torch.randn(B, A + 1, generator=g) / B
+    dhead = dhead.to(cuda)
+    so = (ctypes.c_int64 * 11)()
+    tot = ctypes.c_int64()
+    _lib.call('acmi_kfac_layout', A, C3, None, None, so, ctypes.byref(tot))
+    t, acts = alloc_acts(B, A, C3, cuda, masks=masks)
+    _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+              _lib.stream_handle())
+    need = int(lib.acmi_backward_ws_floats(B, A, C3))
+    z = lambda *sh: torch.zeros(*sh, dtype=torch.float32, device=cuda)
+
+    def dbufs():
+        d = [z(B, 20, 20, 32), z(B, 9, 9, 64), z(B, 7, 7, C3), z(B, 512)]
+        return d, _lib.Bwd(*[x.data_ptr() for x in d], dhead.data_ptr(), ldh)
+
+    out = {}
+    for stacked in (False, True):
+        d, bwd = dbufs()
+        ds, bwd_s = dbufs()
+        ws, ws_s = z(need), z(need)
+        grads, stats = z(params.numel()), z(tot.value)
+        if stacked:
+            _lib.call('acmi_backward_stacked', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
+                      ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(stats), _lib.ptr(ws), need, ctypes.byref(bwd_s), 7,
+                      0, 3, _lib.ptr(ws_s), need, _lib.stream_handle())
+            _lib.call('acmi_kfac_output_stats_finish', ctypes.byref(net), B, ctypes.byref(acts), ctypes.byref(bwd_s),
+                      _lib.ptr(stats), _lib.ptr(ws_s), need, _lib.stream_handle())
+        else:
+            _lib.call('acmi_backward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts),
+                      ctypes.byref(bwd), _lib.ptr(grads), _lib.ptr(stats), _lib.ptr(ws), need, _lib.stream_handle())
+            _lib.call('acmi_kfac_output_stats', ctypes.byref(net), B, ctypes.byref(acts), ctypes.byref(bwd_s), 7, 0,
+                      3, _lib.ptr(stats), _lib.ptr(ws_s), need, _lib.stream_handle())
+        torch.cuda.synchronize()
+        out[stacked] = [grads, stats] + d + ds[1:]
+    assert out[True][1].abs().sum() > 0
+    for i, (a, b) in enumerate(zip(out[False], out[True])):
+        assert torch.equal(a, b), i
+
+
 @pytest.mark.parametrize('C3', [32, 64])
 @pytest.mark.parametrize('fwd', ['f32', 'bf16'])
 def test_split_tower_bit_identical_to_one_block_tower(lib, cuda, C3, fwd):

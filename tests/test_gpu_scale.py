@@ -271,6 +271,12 @@ def test_concurrent_g_stats_bit_identical(lib, cuda, monkeypatch):
     from actorcritic._engine import NetEngine
     monkeypatch.setattr(NetEngine, 'concurrent_stats', False)
     serial = _run_two_updates()
+    # (one stream, the two chains' conv2 input gradients as one launch or two)
+    monkeypatch.setattr(NetEngine, 'stacked_dx', not NetEngine.stacked_dx)
+    other = _run_two_updates()
+    monkeypatch.setattr(NetEngine, 'stacked_dx', not NetEngine.stacked_dx)
+    for i, (a, b) in enumerate(zip(serial[:4], other[:4])):
+        assert torch.equal(a, b), ('stacked', i)
     monkeypatch.setattr(NetEngine, 'concurrent_stats', True)
     # side chain started with the backward, and at its dX event (acmi_stream_wait_backward_dx)
     for after_dx in (False, True):
