@@ -274,8 +274,12 @@ class NetEngine(object):
     # next to the whole backward, 5.16 ms started after the backward's dX chain
     stats_after_dx = os.environ.get('ACMI_STATS_AFTER_DX', '1') != '0'
     # on one stream (larger batches): the two chains' conv2 input gradients as one
-    # launch (acmi_backward_stacked; ACMI_STACKED_DX=0: the two calls)
-    stacked_dx = os.environ.get('ACMI_STACKED_DX', '1') != '0'
+    # launch (acmi_backward_stacked) with ACMI_STACKED_DX=1.  Off by default: the
+    # stacked launch is 11 % faster than the two launches back to back (kbench
+    # c2mix, 564 vs 632 us, bit-identical), but in the update it moves the sampled
+    # chain's dX ahead of the loss chain's reductions, which then re-read d1 / d2
+    # from further away: update 2.914-2.925 vs 2.885-2.897 ms (same lease, 512 x 20)
+    stacked_dx = os.environ.get('ACMI_STACKED_DX', '0') == '1'
 
     def backward_and_stats(self, fwd, st, with_stats, seed, counter):
         """acmi_backward (+ A stats) and, with stats, acmi_kfac_output_stats (G stats);
