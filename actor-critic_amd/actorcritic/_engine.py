@@ -265,11 +265,13 @@ class NetEngine(object):
                   ctypes.byref(bwd), seed, self.rank * fwd.M, counter, _lib.ptr(st.gstat), _lib.ptr(ws),
                   ws.numel(), self.stream())
 
-    # the G chain on a side stream: '1' always, '0' never, unset: at small batches
-    # (M <= CONCURRENT_STATS_ROWS), where each of its launches fills a fraction of
-    # the chip; at the bench shard one stream measured faster
+    # the G chain on a side stream: '1' always, '0' never, unset: at batches up to
+    # CONCURRENT_STATS_ROWS.  Round 6 at the bench shard (512 x 20, same lease):
+    # side stream 2.772-2.792 ms per update against 2.842-2.856 on one stream (the
+    # band reduction slows 0.57 -> 0.64 ms beside it, the rest more than pays);
+    # rounds 2-4 had measured one stream faster with the kernels of then
     concurrent_stats = {'1': True, '0': False}.get(os.environ.get('ACMI_CONCURRENT_STATS', ''))
-    CONCURRENT_STATS_ROWS = 2048
+    CONCURRENT_STATS_ROWS = 1 << 30
     # measured (ACKTR 512x20, one box): plain update 5.25 ms with the G chain started
     # next to the whole backward, 5.16 ms started after the backward's dX chain
     stats_after_dx = os.environ.get('ACMI_STATS_AFTER_DX', '1') != '0'
