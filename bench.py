@@ -153,8 +153,6 @@ def parse():
     p.add_argument('--no-configs2', action='store_true',
                    help='skip the nested BASELINE configs[2] line (ACKTR 32 envs x 20 steps) timed after the headline')
     p.add_argument('--configs2-steps', type=int, default=60)
-    p.add_argument('--no-solo', action='store_true',
-                   help='skip the roofline kernel\'s solo timing (3 iterations, one stream)')
     p.add_argument('--quiet', action='store_true')
     return p.parse_args()
 
@@ -341,19 +339,6 @@ def run(args):
     value, ms_per_step = r['value'], r['ms_per_step']
     tot_ms = ctypes.c_double(r['prof_ms'])
     cnt = ctypes.c_int(r['prof_n'])
-    # the roofline kernel alone on the GPU: a few iterations with the G-statistics
-    # chain on the compute stream (in the timed run it overlaps the band reductions
-    # on a side stream, which lengthens their launches while shortening the update)
-    solo = None
-    if args.algo == 'acktr' and not args.no_solo:
-        from actorcritic._engine import NetEngine
-        prev = NetEngine.concurrent_stats
-        NetEngine.concurrent_stats = False
-        try:
-            rs = _measure(args, N, T, A, args.algo, args.games, 3, 2, prof_site=_lib.PROF_CONV2_WGRAD)
-        finally:
-            NetEngine.concurrent_stats = prev
-        solo = rs['prof_ms'] / max(1, rs['prof_n']) if rs['prof_n'] else None
 
     # BASELINE configs[2] (the reference's own ACKTR config, a2c_acktr.py:306-310:
     # 32 envs x 20 steps, Breakout, f32) -- the config north_star's ">=10x the
@@ -416,11 +401,6 @@ def run(args):
                 'frac': (achieved / peak) if achieved else None, 'traffic': traffic,
                 'launches': cnt.value, 'avg_ms': kern_ms, 'flops_per_launch': kern_flops,
                 'executed_tflops': executed}
-    if solo:
-        # the same launch with the GPU to itself (see above): its rate and fraction
-        roofline['solo_avg_ms'] = solo
-        roofline['solo_achieved'] = kern_flops / (solo * 1e-3) / 1e12
-        roofline['solo_frac'] = roofline['solo_achieved'] / peak
     if band and achieved:
         roofline['sub_tiles'] = int(info[0])
         roofline['groups'] = int(info[1])
