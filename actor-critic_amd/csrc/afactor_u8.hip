@@ -240,7 +240,8 @@ __device__ __forceinline__ void af_transpose4(uint32_t w0, uint32_t w1, uint32_t
   out[3] = __builtin_amdgcn_perm(p23h, p01h, 0x07060302u);
 }
 
-// compile-time probes for timing (scripts/afprobe.sh); 0 in the product build
+// compile-time probes for timing (built as A/B variants by scripts/net_variant.sh-style
+// defines; the measurements are in DESIGN.md section 9); 0 in the product build
 #ifndef AF_PROBE
 #define AF_PROBE 0
 #endif
