@@ -175,7 +175,8 @@ class UpdateState(object):
 class NetEngine(object):
     """Parameters + kernels of one AtariModel on one device."""
 
-    def __init__(self, num_actions, conv3_filters, device=None, seed=0, params=None):
+    def __init__(self, num_actions, conv3_filters, device=None, seed=0, params=None, forward_mode=None,
+                 gemm_mode=None):
         _lib.require_gpu()
         self.lib = _lib.load()
         self.device = torch.device(device) if device is not None else torch.device('cuda',
@@ -190,6 +191,8 @@ class NetEngine(object):
         # the per-update exchange runs when there are ranks to exchange with -- or,
         # test-only (ACMI_FORCE_COLLECTIVE=1 with a process group of one rank), through
         # the same RCCL calls at world size 1, where the sum must leave every bit as is
+        # this net's arithmetic (acmi_net_t mode fields; None: the process default at each call)
+        self.forward_mode, self.gemm_mode = forward_mode, gemm_mode
         self.collective = self.world_size > 1 or (
             os.environ.get('ACMI_FORCE_COLLECTIVE') == '1' and parallel.is_initialized())
         if self.world_size > 1:  # identical initial parameters on every rank
@@ -413,7 +416,9 @@ class NetEngine(object):
         if self._prep is None:
             self._prep = torch.empty(int(self.lib.acmi_conv_prep_bytes(self.C3)), dtype=torch.uint8,
                                      device=self.device)
-        net = _lib.Net(self.A, self.C3, self.params.data_ptr(), self._prep.data_ptr())
+        net = _lib.Net(self.A, self.C3, self.params.data_ptr(), self._prep.data_ptr(),
+                       0 if self.gemm_mode is None else self.gemm_mode + 1,
+                       0 if self.forward_mode is None else self.forward_mode + 1, 0)
         if self._prep_version != (self.version, self.params.data_ptr()):
             _lib.call('acmi_conv_prepare', ctypes.byref(net), ctypes.c_void_p(self._prep.data_ptr()), self.stream())
             self._prep_version = (self.version, self.params.data_ptr())

@@ -26,7 +26,9 @@ class AcmiError(RuntimeError):
 
 
 class Net(ctypes.Structure):
-    _fields_ = [('num_actions', c_int), ('conv3_filters', c_int), ('params', c_vp), ('conv_prep', c_vp)]
+    # mode fields: the mode + 1, 0 = the process default (acmi.h acmi_net_t)
+    _fields_ = [('num_actions', c_int), ('conv3_filters', c_int), ('params', c_vp), ('conv_prep', c_vp),
+                ('gemm_mode', c_int), ('forward_mode', c_int), ('conv_stats_mode', c_int)]
 
 
 class Acts(ctypes.Structure):

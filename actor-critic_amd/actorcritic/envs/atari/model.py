@@ -121,11 +121,13 @@ class AtariModel(ActorCriticModel):
     """The A3C/ACKTR Atari model on MI355X.
 
     Args mirror the reference (envs/atari/model.py:45); ``device``, ``params`` (a flat
-    float32 vector in the acmi layout) and ``init_seed`` are extensions.
+    float32 vector in the acmi layout), ``init_seed`` and ``forward_mode`` (this
+    model's conv-tower precision, acmi ``FWD_F32`` / ``FWD_BF16``; None: the
+    process default) are extensions.
     """
 
     def __init__(self, observation_space, action_space, conv3_num_filters=64, random_seed=None, name=None,
-                 device=None, params=None, init_seed=0):
+                 device=None, params=None, init_seed=0, forward_mode=None):
         super().__init__(observation_space, action_space)
         assert spaces.is_discrete(action_space)
         assert spaces.is_box(observation_space)
@@ -136,7 +138,7 @@ class AtariModel(ActorCriticModel):
         self._name = name or 'AtariModel'
         self._random_seed = random_seed
         self._engine = NetEngine(self._num_actions, conv3_num_filters, device=device, seed=init_seed,
-                                 params=params)
+                                 params=params, forward_mode=forward_mode)
 
         self._forward = _TowerForward(self, self.observations_placeholder, bootstrap=False)
         self._bootstrap_forward = _TowerForward(self, self.bootstrap_observations_placeholder, bootstrap=True)

@@ -123,7 +123,8 @@ __device__ __forceinline__ float amax_read(const unsigned* p) {
 }
 
 // GEMM arithmetic mode (ACMI_GEMM_X3 / ACMI_GEMM_F32, acmi_set_gemm_mode; net.hip)
-extern int g_gemm_mode;
+// (the calling thread's mode for the current entry point: its net's or the process default)
+extern thread_local int g_gemm_mode;
 
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 

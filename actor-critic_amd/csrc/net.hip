@@ -27,6 +27,55 @@
 
 namespace acmi {
 
+// Arithmetic modes.  Process-wide defaults (acmi_set_*_mode; initial values from
+// the environment) and the modes in effect for the calling thread's current
+// entry point: a net's own (acmi_net_t gemm_mode / forward_mode /
+// conv_stats_mode, each mode + 1) or the defaults (ModeScope).
+//   gemm:  ACMI_GEMM_X3 = 16-bit split operands (f16x2 / bf16x3, f32-accurate),
+//          ACMI_GEMM_F32 = v_mfma_f32_32x32x2_f32; ACMI_GEMM ("f32" / "x3"), default x3
+//   conv stats: pixel-pair band reduction (band.hpp, x3 only) or patch rows; ACMI_BAND ("0": patches)
+//   forward: the conv tower's precision; ACMI_FORWARD ("bf16" / "f32")
+static int s_gemm_mode = [] {
+  const char* e = getenv("ACMI_GEMM");
+  return (e && e[0] == 'f') ? ACMI_GEMM_F32 : ACMI_GEMM_X3;
+}();
+static int s_conv_stats_mode = [] {
+  const char* e = getenv("ACMI_BAND");
+  return (e && e[0] == '0') ? ACMI_CONV_STATS_PATCHES : ACMI_CONV_STATS_BAND;
+}();
+static int s_forward_mode = [] {
+  const char* e = getenv("ACMI_FORWARD");
+  return (e && e[0] == 'b') ? ACMI_FWD_BF16 : ACMI_FWD_F32;
+}();
+thread_local int g_gemm_mode = s_gemm_mode;
+thread_local int g_conv_stats_mode = s_conv_stats_mode;
+thread_local int g_forward_mode = s_forward_mode;
+
+// a net's mode fields (0: the process default) are valid
+static bool net_modes_ok(const acmi_net_t* n) {
+  if (!n) return true;
+  const int g = n->gemm_mode ? n->gemm_mode - 1 : s_gemm_mode;
+  const int f = n->forward_mode ? n->forward_mode - 1 : s_forward_mode;
+  const int c = n->conv_stats_mode ? n->conv_stats_mode - 1 : s_conv_stats_mode;
+  return (g == ACMI_GEMM_F32 || g == ACMI_GEMM_X3) && (f == ACMI_FWD_F32 || f == ACMI_FWD_BF16) &&
+         (c == ACMI_CONV_STATS_PATCHES || c == ACMI_CONV_STATS_BAND) && (f == ACMI_FWD_F32 || g == ACMI_GEMM_X3);
+}
+// the modes of one entry point's call, restored when it returns (thread-local:
+// calls on different threads with different nets do not interfere)
+struct ModeScope {
+  int g, f, c;
+  explicit ModeScope(const acmi_net_t* n) : g(g_gemm_mode), f(g_forward_mode), c(g_conv_stats_mode) {
+    g_gemm_mode = n && n->gemm_mode ? n->gemm_mode - 1 : s_gemm_mode;
+    g_forward_mode = n && n->forward_mode ? n->forward_mode - 1 : s_forward_mode;
+    g_conv_stats_mode = n && n->conv_stats_mode ? n->conv_stats_mode - 1 : s_conv_stats_mode;
+  }
+  ~ModeScope() {
+    g_gemm_mode = g;
+    g_forward_mode = f;
+    g_conv_stats_mode = c;
+  }
+};
+
 static thread_local char g_err[512];
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -495,11 +544,6 @@ __global__ __launch_bounds__(256) void heads_kernel(const float* part, int nz, c
 // 26.5 / 82 us at 512 images against 26.5 / 30.  conv3's input gradient and
 // forward keep those kernels: 231 -> 186 us, 19.6 -> 18.7 us.)
 
-// forward precision (acmi_set_forward_mode): the tower's arithmetic
-int g_forward_mode = [] {
-  const char* e = getenv("ACMI_FORWARD");
-  return (e && e[0] == 'b') ? ACMI_FWD_BF16 : ACMI_FWD_F32;
-}();
 
 // split factor for fc4 at small batch (64 x 128 tiles over 512 columns; 4 / 6 /
 // 12 / 16 chunks measured no better than 8)
@@ -1134,22 +1178,6 @@ __global__ __launch_bounds__(256) void gram_small_kernel(const float* D, int ld,
 // MI355X has 256 CUs; blocks per CU follow from each config's LDS image
 constexpr int kCUs = 256;
 
-// Arithmetic of the slab-grouped wgrad + A-factor reductions (acmi_set_gemm_mode):
-// ACMI_GEMM_X3 = bf16x3 split operands on the bf16 matrix cores (symred3.hpp,
-// f32-accurate), ACMI_GEMM_F32 = v_mfma_f32_32x32x2_f32 (symred.hpp).  Initial
-// value from the environment variable ACMI_GEMM ("f32" or "x3"), default x3.
-int g_gemm_mode = [] {
-  const char* e = getenv("ACMI_GEMM");
-  return (e && e[0] == 'f') ? ACMI_GEMM_F32 : ACMI_GEMM_X3;
-}();
-
-// conv2 / conv3 weight gradient + A factor (acmi_set_conv_stats_mode): pixel-pair
-// band reduction (band.hpp, bf16x3 only) or the patch-row symmetric reduction.
-// Initial value from ACMI_BAND ("0": patch rows), default band.
-int g_conv_stats_mode = [] {
-  const char* e = getenv("ACMI_BAND");
-  return (e && e[0] == '0') ? ACMI_CONV_STATS_PATCHES : ACMI_CONV_STATS_BAND;
-}();
 static bool band_on(bool with_stats) {
   return with_stats && g_gemm_mode == ACMI_GEMM_X3 && g_conv_stats_mode == ACMI_CONV_STATS_BAND;
 }
@@ -1834,32 +1862,32 @@ int acmi_abi_struct_sizes(int64_t* sizes, int n) {
 int acmi_set_gemm_mode(int mode) {
   ACMI_REQUIRE(mode == ACMI_GEMM_F32 || mode == ACMI_GEMM_X3, ACMI_ERR_ARG,
                "acmi_set_gemm_mode: unknown mode %d", mode);
-  ACMI_REQUIRE(mode == ACMI_GEMM_X3 || g_forward_mode == ACMI_FWD_F32, ACMI_ERR_ARG,
+  ACMI_REQUIRE(mode == ACMI_GEMM_X3 || s_forward_mode == ACMI_FWD_F32, ACMI_ERR_ARG,
                "acmi_set_gemm_mode: f32 gemm mode has no bf16 forward (acmi_set_forward_mode(ACMI_FWD_F32) first)");
-  g_gemm_mode = mode;
+  s_gemm_mode = g_gemm_mode = mode;
   return ACMI_OK;
 }
-int acmi_get_gemm_mode(void) { return g_gemm_mode; }
+int acmi_get_gemm_mode(void) { return s_gemm_mode; }
 
 int acmi_set_forward_mode(int mode) {
   ACMI_REQUIRE(mode == ACMI_FWD_F32 || mode == ACMI_FWD_BF16, ACMI_ERR_ARG, "acmi_set_forward_mode: bad mode %d",
                mode);
   // the bf16 arithmetic exists only in the fused tower (tower.hpp): refuse a mode
   // the forward could not honour instead of silently computing in f32
-  ACMI_REQUIRE(mode == ACMI_FWD_F32 || g_gemm_mode == ACMI_GEMM_X3, ACMI_ERR_ARG,
+  ACMI_REQUIRE(mode == ACMI_FWD_F32 || s_gemm_mode == ACMI_GEMM_X3, ACMI_ERR_ARG,
                "acmi_set_forward_mode: bf16 forward needs the fused tower (x3 gemm mode)");
-  g_forward_mode = mode;
+  s_forward_mode = g_forward_mode = mode;
   return ACMI_OK;
 }
-int acmi_get_forward_mode(void) { return g_forward_mode; }
+int acmi_get_forward_mode(void) { return s_forward_mode; }
 
 int acmi_set_conv_stats_mode(int mode) {
   ACMI_REQUIRE(mode == ACMI_CONV_STATS_PATCHES || mode == ACMI_CONV_STATS_BAND, ACMI_ERR_ARG,
                "acmi_set_conv_stats_mode: unknown mode %d", mode);
-  g_conv_stats_mode = mode;
+  s_conv_stats_mode = g_conv_stats_mode = mode;
   return ACMI_OK;
 }
-int acmi_get_conv_stats_mode(void) { return g_conv_stats_mode; }
+int acmi_get_conv_stats_mode(void) { return s_conv_stats_mode; }
 
 
 int acmi_band_info(int layer, int C3, int64_t rows, int64_t* info) {
@@ -2002,6 +2030,8 @@ __global__ __launch_bounds__(256) void conv_prep_split_kernel(PrepArgs a) {
 }
 
 int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
+  ACMI_REQUIRE(net_modes_ok(net), ACMI_ERR_ARG, "acmi_conv_prepare: bad acmi_net_t mode fields");
+  const ModeScope mode_scope(net);
   Layout L;
   ACMI_REQUIRE(net && net->params && prep && make_layout(net->num_actions, net->conv3_filters, &L),
                ACMI_ERR_ARG, "acmi_conv_prepare: bad arguments");
@@ -2035,6 +2065,8 @@ int acmi_conv_prepare(const acmi_net_t* net, void* prep, acmi_stream_t stream) {
 
 int acmi_forward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,
                  const acmi_acts_t* acts, int want_value, acmi_stream_t stream) {
+  ACMI_REQUIRE(net_modes_ok(net), ACMI_ERR_ARG, "acmi_forward: bad acmi_net_t mode fields");
+  const ModeScope mode_scope(net);
   return forward_dispatch(net, obs, img_stride, B, acts, want_value, 1, stream);
 }
 
@@ -2043,12 +2075,16 @@ int acmi_forward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, 
 int acmi_forward_strided(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,
                          const acmi_acts_t* acts, int want_value, int64_t act_img_stride,
                          acmi_stream_t stream) {
+  ACMI_REQUIRE(net_modes_ok(net), ACMI_ERR_ARG, "acmi_forward_strided: bad acmi_net_t mode fields");
+  const ModeScope mode_scope(net);
   return forward_dispatch(net, obs, img_stride, B, acts, want_value, act_img_stride, stream);
 }
 
 int acmi_rollout_step(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,
                       const acmi_acts_t* acts, int64_t act_img_stride, const acmi_rollout_io_t* io,
                       acmi_stream_t stream) {
+  ACMI_REQUIRE(net_modes_ok(net), ACMI_ERR_ARG, "acmi_rollout_step: bad acmi_net_t mode fields");
+  const ModeScope mode_scope(net);
   ACMI_REQUIRE(io && io->actions && io->bad_rows && io->obs_out && io->rewards && io->terminals &&
                    io->episode_rewards && io->ld >= 1 && io->out_stride % 16 == 0 &&
                    img_stride % 16 == 0 && io->row_offset >= 0 && net &&
@@ -2078,6 +2114,8 @@ int64_t acmi_backward_ws_floats(int B, int A, int C3) {
 int acmi_backward(const acmi_net_t* net, const uint8_t* obs, int64_t img_stride, int B,
                   const acmi_acts_t* acts, const acmi_bwd_t* bwd, float* grads,
                   float* a_stats, float* ws, int64_t ws_floats, acmi_stream_t stream) {
+  ACMI_REQUIRE(net_modes_ok(net), ACMI_ERR_ARG, "acmi_backward: bad acmi_net_t mode fields");
+  const ModeScope mode_scope(net);
   Layout L;
   ACMI_REQUIRE(net && acts && bwd && grads && ws && obs, ACMI_ERR_ARG,
                "acmi_backward: null argument");
@@ -2106,6 +2144,8 @@ int acmi_backward_stacked(const acmi_net_t* net, const uint8_t* obs, int64_t img
                           float* ws, int64_t ws_floats, const acmi_bwd_t* bwd_s, uint32_t seed,
                           uint32_t row_offset, uint32_t counter, float* ws_s, int64_t ws_s_floats,
                           acmi_stream_t stream) {
+  ACMI_REQUIRE(net_modes_ok(net), ACMI_ERR_ARG, "acmi_backward_stacked: bad acmi_net_t mode fields");
+  const ModeScope mode_scope(net);
   Layout L;
   ACMI_REQUIRE(net && acts && bwd && bwd_s && grads && a_stats && ws && ws_s && obs, ACMI_ERR_ARG,
                "acmi_backward_stacked: null argument");
@@ -2135,6 +2175,8 @@ int acmi_backward_stacked(const acmi_net_t* net, const uint8_t* obs, int64_t img
 
 int acmi_kfac_output_stats_finish(const acmi_net_t* net, int B, const acmi_acts_t* acts, const acmi_bwd_t* bwd_s,
                                   float* g_stats, float* ws_s, int64_t ws_s_floats, acmi_stream_t stream) {
+  ACMI_REQUIRE(net_modes_ok(net), ACMI_ERR_ARG, "acmi_kfac_output_stats_finish: bad acmi_net_t mode fields");
+  const ModeScope mode_scope(net);
   Layout L;
   ACMI_REQUIRE(net && acts && bwd_s && g_stats && ws_s, ACMI_ERR_ARG, "acmi_kfac_output_stats_finish: null argument");
   ACMI_REQUIRE(make_layout(net->num_actions, net->conv3_filters, &L), ACMI_ERR_ARG, "bad net");
@@ -2160,6 +2202,8 @@ int acmi_kfac_output_stats(const acmi_net_t* net, int B, const acmi_acts_t* acts
                            const acmi_bwd_t* bwd, uint32_t seed, uint32_t row_offset,
                            uint32_t counter, float* g_stats, float* ws, int64_t ws_floats,
                            acmi_stream_t stream) {
+  ACMI_REQUIRE(net_modes_ok(net), ACMI_ERR_ARG, "acmi_kfac_output_stats: bad acmi_net_t mode fields");
+  const ModeScope mode_scope(net);
   Layout L;
   ACMI_REQUIRE(net && acts && bwd && g_stats && ws, ACMI_ERR_ARG,
                "acmi_kfac_output_stats: null argument");
@@ -2226,6 +2270,8 @@ int acmi_prof_collect(double* total_ms, int* count) {
 int acmi_debug_convt2(const acmi_net_t* net, int mode, const float* d2a, const float* d2b, const uint32_t* m1,
                       float* d1, int B, float* gram_part, const uint32_t* d2max_a, const uint32_t* d2max_b,
                       uint32_t* d1max, acmi_stream_t stream) {
+  ACMI_REQUIRE(net_modes_ok(net), ACMI_ERR_ARG, "acmi_debug_convt2: bad acmi_net_t mode fields");
+  const ModeScope mode_scope(net);
   ACMI_REQUIRE(net && net->conv_prep && d2a && d2b && m1 && d1 && gram_part && d2max_a && d2max_b && d1max && B > 0,
                ACMI_ERR_ARG, "acmi_debug_convt2: bad arguments");
   const char* p2 = static_cast<const char*>(net->conv_prep) +

@@ -208,7 +208,7 @@ def main():
     run(args)
 
 
-def _measure(args, N, T, A, algo, games, steps, warmup, prof_site=None):
+def _measure(args, N, T, A, algo, games, steps, warmup, prof_site=None, forward_mode=None):
     """Build the reference training graph for one workload and time `steps`
     iterations after `warmup` (barrier + synchronize on both sides; wall time is
     the max over ranks).  prof_site: the libacmi HIP-event profiling site of the
@@ -231,7 +231,9 @@ def _measure(args, N, T, A, algo, games, steps, warmup, prof_site=None):
     sess.reset_default_graph()
     env = MultiEnv(SyntheticAtariEnvs(N, num_actions=A, seed=1234, env_offset=rank * N, device=dev,
                                       games=games))
-    model = AtariModel(env.observation_space, env.action_space, C3, random_seed=7, device=dev)
+    # (forward_mode: this model's conv-tower precision, the acmi_net_t mode field)
+    model = AtariModel(env.observation_space, env.action_space, C3, random_seed=7, device=dev,
+                       forward_mode=forward_mode)
     agent = MultiEnvAgent(env, model, T)
     objective = A2CObjective(model, discount_factor=0.99, entropy_regularization_strength=0.01)
     gs = sess.get_or_create_global_step()
@@ -324,9 +326,10 @@ def run(args):
     from actorcritic import _lib, parallel
 
     world, rank = parallel.init_from_env()
-    if args.forward is not None:
-        _lib.call('acmi_set_forward_mode', _lib.FWD_BF16 if args.forward == 'bf16' else _lib.FWD_F32)
-    args.forward = 'bf16' if _lib.load().acmi_get_forward_mode() == _lib.FWD_BF16 else 'f32'
+    # the headline model's forward precision: --forward, else the process default
+    # (ACMI_FORWARD); carried by its net, not set process-wide
+    fwd = {'bf16': _lib.FWD_BF16, 'f32': _lib.FWD_F32}.get(args.forward, _lib.load().acmi_get_forward_mode())
+    args.forward = 'bf16' if fwd == _lib.FWD_BF16 else 'f32'
     if world != args.gpus:
         raise SystemExit('bench: --gpus {} but the process group has {} ranks (WORLD_SIZE={})'.format(
             args.gpus, world, os.environ.get('WORLD_SIZE')))
@@ -335,7 +338,8 @@ def run(args):
     T = args.nsteps or (20 if acktr else 5)
     C3 = 32 if acktr else 64
     A = args.num_actions
-    r = _measure(args, N, T, A, args.algo, args.games, args.steps, args.warmup, prof_site=_lib.PROF_CONV2_WGRAD)
+    r = _measure(args, N, T, A, args.algo, args.games, args.steps, args.warmup, prof_site=_lib.PROF_CONV2_WGRAD,
+                 forward_mode=fwd)
     value, ms_per_step = r['value'], r['ms_per_step']
     tot_ms = ctypes.c_double(r['prof_ms'])
     cnt = ctypes.c_int(r['prof_n'])
@@ -347,10 +351,8 @@ def run(args):
     c2 = None
     if (world == 1 and not args.no_configs2
             and not (acktr and N == 32 and T == 20 and A == 4 and args.forward == 'f32' and not args.games)):
-        fwd_mode = _lib.load().acmi_get_forward_mode()
-        _lib.call('acmi_set_forward_mode', _lib.FWD_F32)
-        c2r = _measure(args, 32, 20, 4, 'acktr', None, args.configs2_steps, max(5, args.warmup))
-        _lib.call('acmi_set_forward_mode', fwd_mode)
+        c2r = _measure(args, 32, 20, 4, 'acktr', None, args.configs2_steps, max(5, args.warmup),
+                       forward_mode=_lib.FWD_F32)
         c2 = {'workload': workload_name('acktr', 32, 20, 4, 'f32', 1), 'envs': 32, 'num_steps': 20,
               'num_actions': 4, 'forward': 'f32', 'steps': args.configs2_steps, 'warmup': max(5, args.warmup),
               'value': c2r['value'], 'unit': 'env-steps/s', 'ms_per_step': c2r['ms_per_step'],

@@ -23,7 +23,8 @@ extern "C" {
 #endif
 
 #define ACMI_ABI_VERSION 4  /* 3: acmi_env_state_t.game, acmi_rollout_io_t step fusion fields;
-                               4: ws_floats on acmi_backward / acmi_kfac_output_stats */
+                               4: ws_floats on acmi_backward / acmi_kfac_output_stats, per-net
+                                  mode fields in acmi_net_t */
 
 enum {
   ACMI_OK = 0,
@@ -50,6 +51,8 @@ int acmi_abi_struct_sizes(int64_t* sizes, int n);
  *                 and fc4 reductions; bf16x3 (6 MFMAs) for the small rest
  *   ACMI_GEMM_F32 v_mfma_f32_32x32x2_f32
  * Initial mode from the environment variable ACMI_GEMM ("x3" / "f32").
+ * The acmi_set_*_mode functions set the PROCESS DEFAULT, which nets with a
+ * zero mode field use; a net's own field overrides it (acmi_net_t).
  * Not stream-ordered: set it between launches. */
 #define ACMI_GEMM_F32 0
 #define ACMI_GEMM_X3 1
@@ -125,6 +128,14 @@ typedef struct acmi_net {
   const void* conv_prep; /* nullable: device, acmi_conv_prep_bytes(C3) bytes,
                             filled by acmi_conv_prepare from THESE params (the
                             caller re-prepares after every parameter change) */
+  /* This net's arithmetic, each the mode + 1 (ACMI_GEMM_*, ACMI_FWD_*,
+   * ACMI_CONV_STATS_*); 0 = the process default (acmi_set_*_mode).  Every
+   * entry point taking a net runs in its net's modes (held per calling thread
+   * for the call), so two nets in one process, or two threads, never see each
+   * other's settings; an invalid combination fails with ACMI_ERR_ARG. */
+  int gemm_mode;
+  int forward_mode;
+  int conv_stats_mode;
 } acmi_net_t;
 
 /* The forward's fused conv tower (x3 gemm mode), fc4 at rollout batches

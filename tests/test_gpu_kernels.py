@@ -269,6 +269,46 @@ def test_backward_stacked_bit_identical_to_two_calls(lib, cuda, B, use_prep, mas
         assert torch.equal(a, b), i
 
 
+def test_per_net_modes_override_the_process_default(lib, cuda):
+    """acmi_net_t's mode fields (mode + 1; 0 = the process default): a net carrying
+    ACMI_FWD_BF16 computes under an f32 process default exactly what the bf16
+    process default computes, and the reverse; an invalid combination (bf16
+    forward in f32 gemm mode) is refused.  (The modes are held per calling thread
+    for the call, so nets in one process do not see each other's settings.)"""
+    A, C3, B = 4, 32, 40
+    g = torch.Generator().manual_seed(9)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
+    params = rand_params(A, C3, cuda, seed=12)
+    prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
+
+    def fwd(process_mode, net_field):
+        prev = lib.acmi_get_forward_mode()
+        _lib.call('acmi_set_forward_mode', process_mode)
+        try:
+            net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr(), 0, net_field, 0)
+            _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), _lib.stream_handle())
+            t, acts = alloc_acts(B, A, C3, cuda, masks=True)
+            _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+                      _lib.stream_handle())
+            torch.cuda.synchronize()
+            return [t[k].clone() for k in ('a1', 'a2', 'a3', 'logits', 'm1')]
+        finally:
+            _lib.call('acmi_set_forward_mode', prev)
+
+    f32_default = fwd(_lib.FWD_F32, 0)
+    bf16_default = fwd(_lib.FWD_BF16, 0)
+    assert not torch.equal(f32_default[0], bf16_default[0])
+    for a, b in zip(fwd(_lib.FWD_F32, _lib.FWD_BF16 + 1), bf16_default):
+        assert torch.equal(a, b)
+    for a, b in zip(fwd(_lib.FWD_BF16, _lib.FWD_F32 + 1), f32_default):
+        assert torch.equal(a, b)
+    bad = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr(), _lib.GEMM_F32 + 1, _lib.FWD_BF16 + 1, 0)
+    t, acts = alloc_acts(B, A, C3, cuda)
+    assert lib.acmi_forward(ctypes.byref(bad), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1,
+                            _lib.stream_handle()) == -1
+    assert b'mode' in lib.acmi_last_error()
+
+
 @pytest.mark.parametrize('C3', [32, 64])
 @pytest.mark.parametrize('fwd', ['f32', 'bf16'])
 def test_split_tower_bit_identical_to_one_block_tower(lib, cuda, C3, fwd):
