@@ -70,12 +70,13 @@ U8F16X2_F32EQ_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 2  # u8 pixels exact: two f1
 FP64_MFMA_PEAK_TFLOPS = 78.6  # v_mfma_f64_16x16x4f64, dense
 
 
-def iteration_ceiling(N, T, A, C3, acktr, band_tiles=None):
+def iteration_ceiling(N, T, A, C3, acktr, band_tiles=None, forward='f32'):
     """The build's algorithmic work per training iteration (DESIGN.md section 3,
     per-kernel accounting), each kernel's work priced at the ceiling of the
     arithmetic it runs: the time the iteration would take if every kernel ran at
     its roofline.  band_tiles: (conv2, conv3) needed 64x64 sub-tiles of the band
-    reductions (acmi_band_info).  Returns {component: (work, unit, ceiling, ms)}."""
+    reductions (acmi_band_info); forward 'bf16': the conv tower on one 16-bit MFMA per
+    product.  Returns {component: (work, unit, ceiling, ms)}."""
     M = N * T
     K3 = 49 * C3
     imgs = M + N  # the rollout's towers (T steps) and the bootstrap forward
@@ -87,8 +88,10 @@ def iteration_ceiling(N, T, A, C3, acktr, band_tiles=None):
         c[name] = (work, unit, ceil, work / ceil)
 
     # rollout: conv tower (conv1 u8 x f16x2 on two MFMAs; conv2 / conv3 f16x2), fc4 + heads
-    add('tower conv1', 2 * 400 * 256 * 32 * imgs / 1e9, U8F16X2_F32EQ_PEAK_TFLOPS)
-    add('tower conv2 + conv3', (2 * 81 * 512 * 64 + 2 * 49 * 576 * C3) * imgs / 1e9, f2)
+    tw1, tw23 = ((BF16_MFMA_PEAK_TFLOPS, BF16_MFMA_PEAK_TFLOPS) if forward == 'bf16'
+                 else (U8F16X2_F32EQ_PEAK_TFLOPS, f2))
+    add('tower conv1', 2 * 400 * 256 * 32 * imgs / 1e9, tw1)
+    add('tower conv2 + conv3', (2 * 81 * 512 * 64 + 2 * 49 * 576 * C3) * imgs / 1e9, tw23)
     add('rollout fc4 + heads', (2 * K3 * 512 + 2 * 512 * (A + 1)) * imgs / 1e9, f2)
     # env stepping: the 4-frame stack read and written per env-step (HBM)
     add('stepper', 2 * 84 * 84 * 4 * M / 1e9, HBM_PEAK_GBS / 1e3, 'GB')
@@ -419,7 +422,7 @@ def run(args):
             _lib.call('acmi_band_info', 1, C3, M, i2)
             _lib.call('acmi_band_info', 2, C3, M, i3)
             bt = (int(i2[0]), int(i3[0]))
-        ceil = iteration_ceiling(N, T, A, C3, acktr, bt)
+        ceil = iteration_ceiling(N, T, A, C3, acktr, bt, args.forward)
         ceil_ms = sum(v[3] for v in ceil.values())
         roofline['iteration_frac'] = ceil_ms / ms_per_step
         roofline['iteration_ceiling_ms'] = ceil_ms
