@@ -74,6 +74,33 @@ def test_bad_arguments_report_errors(lib):
     assert b'bad' in lib.acmi_last_error()
 
 
+def test_workspace_and_mode_checks_fail_before_any_launch(lib):
+    """The ABI-4 argument checks run on the host before anything is enqueued (here
+    without a GPU: fake device addresses are never touched): a workspace one float
+    below acmi_backward_ws_floats is ACMI_ERR_WS for both update entry points, and
+    an invalid per-net mode combination (bf16 forward in f32 gemm mode) is
+    ACMI_ERR_ARG.  Reference: SURVEY 8(b), model.py:180-186 (errors raised early)."""
+    from actorcritic import _lib
+    A, C3, B = 4, 32, 24
+    fake = lambda k: ctypes.c_void_p(0x100000 * k)
+    net = _lib.Net(A, C3, fake(1).value, fake(2).value)
+    acts = _lib.Acts(*[fake(3 + i).value for i in range(6)], A)
+    bwd = _lib.Bwd(*[fake(10 + i).value for i in range(5)], 8)
+    need = lib.acmi_backward_ws_floats(B, A, C3)
+    assert need > 0
+    rc = lib.acmi_backward(ctypes.byref(net), fake(20), 84 * 84 * 4, B, ctypes.byref(acts), ctypes.byref(bwd),
+                           fake(21), fake(22), fake(23), need - 1, None)
+    assert rc == -3 and b'workspace' in lib.acmi_last_error()
+    rc = lib.acmi_kfac_output_stats(ctypes.byref(net), B, ctypes.byref(acts), ctypes.byref(bwd), 7, 0, 3,
+                                    fake(22), fake(23), need - 1, None)
+    assert rc == -3 and b'workspace' in lib.acmi_last_error()
+    bad = _lib.Net(A, C3, fake(1).value, fake(2).value, _lib.GEMM_F32 + 1, _lib.FWD_BF16 + 1, 0)
+    rc = lib.acmi_backward(ctypes.byref(bad), fake(20), 84 * 84 * 4, B, ctypes.byref(acts), ctypes.byref(bwd),
+                           fake(21), fake(22), fake(23), need, None)
+    assert rc == -1 and b'mode' in lib.acmi_last_error()
+    assert lib.acmi_get_gemm_mode() == _lib.GEMM_X3  # the failed call changed no default
+
+
 def test_schedule_matches_reference_semantics():
     from actorcritic.kfac_utils import schedule
     gs = 0
