@@ -306,6 +306,7 @@ class NetEngine(object):
             return pending
         main = torch.cuda.current_stream(self.device)
         sd = st.side(self)
+        self.net()  # (any pending prepare on main, ahead of the fork)
         sd.stream.wait_stream(main)
         if self.stats_after_dx:
             # the sampled-loss chain starts where the loss backward's input-gradient
@@ -410,16 +411,20 @@ class NetEngine(object):
         return sum(ms) / len(ms), self._comm[-1][2], len(ms)
 
     # -- plumbing ------------------------------------------------------------
-    def net(self):
+    def net(self, force_prepare=False):
         """The C-ABI net: parameters + the conv tower's pre-split weights, re-prepared
-        (acmi_conv_prepare, stream-ordered) at the first use after a parameter update."""
+        (acmi_conv_prepare, stream-ordered, on the CURRENT stream) at the first use after
+        a parameter update, or always with ``force_prepare`` (a hipGraph capture: every
+        replay re-prepares from the parameters as they are then).  A caller that forks
+        work onto a second stream calls this on the parent stream BEFORE the fork, so the
+        prepare is ordered ahead of both chains."""
         if self._prep is None:
             self._prep = torch.empty(int(self.lib.acmi_conv_prep_bytes(self.C3)), dtype=torch.uint8,
                                      device=self.device)
         net = _lib.Net(self.A, self.C3, self.params.data_ptr(), self._prep.data_ptr(),
                        0 if self.gemm_mode is None else self.gemm_mode + 1,
                        0 if self.forward_mode is None else self.forward_mode + 1, 0)
-        if self._prep_version != (self.version, self.params.data_ptr()):
+        if force_prepare or self._prep_version != (self.version, self.params.data_ptr()):
             _lib.call('acmi_conv_prepare', ctypes.byref(net), ctypes.c_void_p(self._prep.data_ptr()), self.stream())
             self._prep_version = (self.version, self.params.data_ptr())
         return net

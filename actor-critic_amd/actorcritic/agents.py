@@ -9,14 +9,16 @@ observation buffer — no host copies, no Python lists.  Anything else takes the
 reference's list-based loop.
 
 Two opt-in variants, bit-identical to the one-chain rollout (test_two_stream_rollout_
-is_bit_identical): ACMI_ROLLOUT_SPLIT=1 runs the two env halves as two chains on two
-HIP streams (the sampler keys its RNG by the global row, acmi_sample_actions_at, the
-stepper by the global env id); ACMI_ROLLOUT_GRAPH=1 captures the rollout once as a
-hipGraph and replays it (the RNG counter read from device memory,
-acmi_sample_actions_dev).  Neither is faster on one MI355X at 512 envs (2.21-2.25 ms
-per 20-step rollout in all four combinations): the per-step kernels are GPU-bound,
-half-batch kernels cost 70-80 % of full-batch ones, and the host keeps up.  They are
-kept for hosts where launch overhead is not hidden.
+is_bit_identical, and across updates test_rollout_variants_give_identical_updates):
+ACMI_ROLLOUT_SPLIT=1 runs the two env halves as two chains on two HIP streams (the
+sampler keys its RNG by the global row, acmi_sample_actions_at, the stepper by the global
+env id); ACMI_ROLLOUT_GRAPH=1 captures the rollout once as a hipGraph and replays it (the
+RNG counter read from device memory, acmi_sample_actions_dev).  Neither is faster on one
+MI355X (same lease, two rounds each: 512 x 20 2.68 vs 2.69-2.70 M env-steps/s split on /
+off; 1024 x 20 bf16 2.72-2.75 M both): the per-step kernels are GPU-bound and the host
+keeps up.  They are kept for hosts where launch overhead is not hidden.  (An earlier
++6 % for the split came from a race, since fixed: half 1 read the conv tower's prepared
+weights while half 0's step 0 was re-making them after an update.)
 """
 
 import ctypes
@@ -146,6 +148,11 @@ class MultiEnvAgent(Agent):
         main = torch.cuda.current_stream(eng.device)
         if not rb.fused:  # (the fused step 0 reads next_obs in place and files it into obs[:, 0])
             rb.obs[:, 0].copy_(rb.next_obs)
+        # the tower's prepared weights are re-made on the first use after an update:
+        # here, on this stream ahead of the fork (half 1 on rb.side would otherwise
+        # read them before half 0's step 0 re-made them); always when capturing a
+        # graph, so that every replay re-prepares from the updated parameters
+        eng.net(force_prepare=dev_ctr)
         if rb.halves:
             rb.side.wait_stream(main)
         N2 = N // 2 if rb.halves else N

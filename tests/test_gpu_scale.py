@@ -148,12 +148,11 @@ def _bench_like(N=512, T=20, seed=1234):
     return env, model, agent, obj, gs, opt, op
 
 
-def _run_two_updates():
+def _run_two_updates(iters=2):
     from actorcritic import session as sess
     env, model, agent, obj, gs, opt, op = _bench_like()
-    feeds = []
     with sess.Session() as s:
-        for _ in range(2):
+        for _ in range(iters):
             obs, act, rew, term, nxt, _ = agent.interact(s)
             s.run(op, feed_dict={model.observations_placeholder: obs, model.bootstrap_observations_placeholder: nxt,
                                  model.actions_placeholder: act, model.rewards_placeholder: rew,
@@ -161,6 +160,23 @@ def _run_two_updates():
     torch.cuda.synchronize()
     return (model.params.clone(), opt.state['factors'].clone(), opt.state['inv'].clone(),
             opt.state['velocity'].clone(), model.engine.layout)
+
+
+def test_rollout_variants_give_identical_updates(lib, cuda, monkeypatch):
+    """Three rollout + ACKTR update iterations at 512 envs x 20 steps give bit-identical
+    parameters, factors, inverses and velocities whichever rollout runs: one chain,
+    the two env halves on two streams, and either replayed from a
+    captured hipGraph.  The rollouts after an update read the conv tower's weights
+    re-prepared from the updated parameters: prepared on the parent stream before the
+    halves fork, and inside the captured graph so that every replay re-prepares."""
+    outs = []
+    for split, graph in (('0', '0'), ('1', '0'), ('1', '1'), ('0', '1')):
+        monkeypatch.setenv('ACMI_ROLLOUT_SPLIT', split)
+        monkeypatch.setenv('ACMI_ROLLOUT_GRAPH', graph)
+        outs.append(_run_two_updates(iters=3)[:4])
+    for k, other in enumerate(outs[1:], 1):
+        for i, (a, b) in enumerate(zip(outs[0], other)):
+            assert torch.equal(a, b), (k, i)
 
 
 def test_full_size_updates_are_bit_identical_and_factors_well_formed(lib, cuda):
