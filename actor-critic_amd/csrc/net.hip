@@ -1477,8 +1477,10 @@ static int dx_chain_pre(const Layout& L, const float* P, int B, const acmi_acts_
         launch_mm<64, 128, 32, 1, 2, false, false, 16>(opA, opB, epi, B, K3, 512, 1, 0, s);
     };
     // ReLU'(a3) from the mask bits when the forward wrote them
+    prof_begin(ACMI_PROF_FC4_DX, s);
     if (a->m3) run(EpiReluGrad<true>{bw->d3, reinterpret_cast<const float*>(a->m3), K3, dxs + kBsMaxD3});
     else run(EpiReluGrad<false>{bw->d3, a->a3, K3, dxs + kBsMaxD3});
+    prof_end(ACMI_PROF_FC4_DX, s);
   }
   // conv input gradients as transposed products: rows = (phase, channel) of
   // the weights, columns = (super-)pixels gathering dY (EpiConvT, float4 rows)
@@ -1496,8 +1498,10 @@ static int dx_chain_pre(const Layout& L, const float* P, int B, const acmi_acts_
       else
         launch_mm<64, 128, 16, 1, 2, false, false, 16>(opA, opB, epi, W::N, B * Src::L, Src::COLS, 1, 0, s);
     };
+    prof_begin(ACMI_PROF_CONV3_DX, s);
     if (a->m2) run(EpiConvT<9, 9, 1, 64, true>{bw->d2, reinterpret_cast<const float*>(a->m2), dxs + kBsMaxD2});
     else run(EpiConvT<9, 9, 1, 64>{bw->d2, a->a2, dxs + kBsMaxD2});
+    prof_end(ACMI_PROF_CONV3_DX, s);
   }
   ACMI_LAUNCH_CHECK("dx_chain");
   return ACMI_OK;

@@ -621,6 +621,8 @@ int acmi_gemm_f32(const float* A, const float* B, float* C, int M, int N,
 #define ACMI_PROF_CONV1_FWD 3
 #define ACMI_PROF_CONV1_AFACTOR 4 /* exact-integer i8-MFMA conv1 A factor */
 #define ACMI_PROF_CONV2_DX 5      /* conv2 input gradient (all stride phases) */
+#define ACMI_PROF_FC4_DX 6        /* fc4 input gradient d4 W4^T (+ ReLU') */
+#define ACMI_PROF_CONV3_DX 7      /* conv3 input gradient */
 int acmi_prof_enable(int site, int capacity);
 int acmi_prof_collect(double* total_ms, int* count);
 

@@ -197,6 +197,10 @@ if __name__ == '__main__':
         c2mix(int(sys.argv[2]) if len(sys.argv) > 2 else 10240)
     elif what == 'c2g':  # conv2 dX site of the sampled-loss chain (Gram epilogue) and of both chains
         stats_chain(int(sys.argv[2]) if len(sys.argv) > 2 else 10240)
+    elif what == 'fc4dx':  # fc4 dX site (ACMI_PROF_FC4_DX = 6), then conv3 dX (7)
+        M = int(sys.argv[2]) if len(sys.argv) > 2 else 10240
+        backward(M, False, 6, reps=10)
+        backward(M, False, 7, reps=10)
     elif what == 'c2':  # conv2 dX site (ACMI_PROF_CONV2_DX = 5)
         backward(int(sys.argv[2]) if len(sys.argv) > 2 else 10240, False, 5, reps=10)
     elif what == 'backward1x':  # the conv2 band launch alone (site 2), ten timed reps
