@@ -43,7 +43,7 @@ X3_F32EQ_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
 # f16x2 split operands (f16x2.hpp): three f16 MFMAs (f16 dense peak = bf16's)
 F16X2_F32EQ_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
 HBM_PEAK_GBS = 8000.0
-PMC_PACKAGE = 'r05_final'  # profiles/<this>/: the current measurement package
+PMC_PACKAGE = 'r06_final'  # profiles/<this>/: the current measurement package
 
 
 def measured_traffic(kernel, workload):
