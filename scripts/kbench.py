@@ -201,6 +201,8 @@ if __name__ == '__main__':
         M = int(sys.argv[2]) if len(sys.argv) > 2 else 10240
         backward(M, False, 6, reps=10)
         backward(M, False, 7, reps=10)
+    elif what == 'af':  # conv1 A factor + weight gradient site (ACMI_PROF_CONV1_AFACTOR = 4)
+        backward(int(sys.argv[2]) if len(sys.argv) > 2 else 10240, True, 4, reps=10)
     elif what == 'c2':  # conv2 dX site (ACMI_PROF_CONV2_DX = 5)
         backward(int(sys.argv[2]) if len(sys.argv) > 2 else 10240, False, 5, reps=10)
     elif what == 'backward1x':  # the conv2 band launch alone (site 2), ten timed reps
