@@ -309,6 +309,60 @@ def test_per_net_modes_override_the_process_default(lib, cuda):
     assert b'mode' in lib.acmi_last_error()
 
 
+def test_per_net_modes_hold_across_concurrent_threads(lib, cuda):
+    """Two host threads call acmi_conv_prepare + acmi_forward at the same time, 25 times
+    each, on their own HIP streams, one net carrying the bf16 forward and one the f32
+    forward (process default f32): every output equals the single-threaded run of the
+    same net bit for bit -- the per-call modes are held per thread (net.hip ModeScope),
+    so concurrent calls with different nets do not see each other's settings (ctypes
+    releases the GIL around each foreign call, so the calls overlap in the library)."""
+    import threading
+    A, C3, B = 4, 32, 40
+    g = torch.Generator().manual_seed(21)
+    obs = torch.randint(0, 256, (B, 84, 84, 4), generator=g, dtype=torch.uint8).to(cuda)
+    params = rand_params(A, C3, cuda, seed=22)
+    torch.cuda.synchronize()  # the threads' streams do not wait on the default stream
+    modes = (_lib.FWD_BF16 + 1, _lib.FWD_F32 + 1)
+
+    def run(mode, stream, reps, out, errors, start=None):
+        try:
+            with torch.cuda.stream(stream):
+                prep = torch.empty(int(lib.acmi_conv_prep_bytes(C3)), dtype=torch.uint8, device=cuda)
+                net = _lib.Net(A, C3, params.data_ptr(), prep.data_ptr(), 0, mode, 0)
+                t, acts = alloc_acts(B, A, C3, cuda, masks=True)
+            h = ctypes.c_void_p(stream.cuda_stream)
+            if start is not None:
+                start.wait()
+            for _ in range(reps):
+                _lib.call('acmi_conv_prepare', ctypes.byref(net), _lib.ptr(prep), h)
+                _lib.call('acmi_forward', ctypes.byref(net), _lib.ptr(obs), 84 * 84 * 4, B, ctypes.byref(acts), 1, h)
+            stream.synchronize()
+            out.append([t[k].clone() for k in ('a1', 'a2', 'a3', 'logits', 'value', 'm1')])
+        except Exception as e:  # surfaced by the main thread
+            errors.append(e)
+
+    refs = []
+    for mode in modes:
+        out, errors = [], []
+        run(mode, torch.cuda.Stream(), 1, out, errors)
+        assert not errors, errors
+        refs.append(out[0])
+    assert not torch.equal(refs[0][0], refs[1][0])  # the two modes really differ
+    outs, errors = [[], []], []
+    start = threading.Barrier(2)
+    threads = [threading.Thread(target=run, args=(m, torch.cuda.Stream(), 25, outs[i], errors, start))
+               for i, m in enumerate(modes)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not errors, errors
+    for i in range(2):
+        assert len(outs[i]) == 1
+        for a, b in zip(outs[i][0], refs[i]):
+            assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize('C3', [32, 64])
 @pytest.mark.parametrize('fwd', ['f32', 'bf16'])
 def test_split_tower_bit_identical_to_one_block_tower(lib, cuda, C3, fwd):
