@@ -240,11 +240,6 @@ __device__ __forceinline__ void af_transpose4(uint32_t w0, uint32_t w1, uint32_t
   out[3] = __builtin_amdgcn_perm(p23h, p01h, 0x07060302u);
 }
 
-// compile-time probes for timing (built as A/B variants by scripts/net_variant.sh-style
-// defines; the measurements are in DESIGN.md section 9); 0 in the product build
-#ifndef AF_PROBE
-#define AF_PROBE 0
-#endif
 
 struct AfRegs {  // one stage's gather: 4 rows x 8 patch bytes, one float4 of d1
   uint2 a[4];
@@ -293,13 +288,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   int fk = r_begin + drow;                                    // d1 row
   const uint32_t dcb = (uint32_t)dcol * 4u;
   auto fetch = [&](AfRegs& R) {
-    if constexpr (AF_PROBE == 8) {  // no loads: synthetic bytes
-      R.a[0] = make_uint2(fr, fp); R.a[1] = make_uint2(fp, fr); R.a[2] = make_uint2(fk, fr); R.a[3] = make_uint2(fr, fk);
-      R.f = 0x80808080u;
-      R.d = make_float4((float)fk, 0.f, 1.f, 2.f);
-      fr += AF_BK; fk += AF_BK; fp += 3;
-      return;
-    }
     const bool ok = fr < r_end;
     const uint32_t oh = (fp * 3277u) >> 16;  // fp / 20 (fp < 400)
     // ((4 oh) * 84 + 4 ow) * 4 with ow = fp - 20 oh
@@ -318,13 +306,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     fimg = wrap ? fimg + istride : fimg;
   };
   double dsum[4] = {0.0, 0.0, 0.0, 0.0};  // bias gradient: ~8000 rows per thread column
-  uint32_t sink = 0;
   auto commit = [&](const AfRegs& R, int buf) {
-    if constexpr (AF_PROBE == 3 || AF_PROBE == 4) {
-      sink ^= R.a[0].x ^ R.a[1].x ^ R.a[2].x ^ R.a[3].x ^ R.a[0].y ^ R.a[1].y ^ R.a[2].y ^ R.a[3].y ^
-              __float_as_uint(R.d.x) ^ __float_as_uint(R.d.w);
-      return;
-    }
     const uint32_t F = R.f;
     uint32_t cols[8];
     af_transpose4(R.a[0].x ^ F, R.a[1].x ^ F, R.a[2].x ^ F, R.a[3].x ^ F, cols);
@@ -372,9 +354,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     int csum[2] = {0, 0};  // weight-gradient role: its two patch columns' sums of x
 
     auto compute = [&](int cur) {
-      if constexpr (AF_PROBE == 1 || AF_PROBE == 4 || AF_PROBE == 7 || (AF_PROBE == 5 && ROLE == 2) ||
-                    (AF_PROBE == 6 && ROLE < 2))
-        return;
       const uint8_t* S = lds[cur] + (lane & 31) * AF_LINE + 16 * half;
       if constexpr (ROLE == 0) {
 #pragma unroll
@@ -475,7 +454,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
       compute(cur);
       __builtin_amdgcn_sched_barrier(0);
       commit(Rc, cur ^ 1);
-      if constexpr (AF_PROBE != 7) __syncthreads();
+      __syncthreads();
     };
     // (the odd last stage after the loop: a conditional second stage inside it
     // would leave the first set's loads pending at the back edge, and the wait
@@ -528,7 +507,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     run(std::integral_constant<int, 1>{});
   else
     run(std::integral_constant<int, 2>{});
-  if (AF_PROBE != 0 && sink == 0x9e3779b9u && rows < 0) colsum[0] = (int)sink;
 
   // bias gradient (row 256): the 64 row-threads of each channel group through LDS
   double* cs = reinterpret_cast<double*>(&lds[0][0]);  // free after the last stage's barrier

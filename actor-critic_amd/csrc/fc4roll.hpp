@@ -85,25 +85,16 @@ void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w
 
   float4 av[NSLOT][2];
   uint4 bv[NSLOT][CT][2];
-#ifndef ACMI_FC4_PROBE  // timing probes (wrong results): 1 no a3 loads, 2 no W4 loads, 4 no MFMAs
-#define ACMI_FC4_PROBE 0
-#endif
   auto load = [&](int i, int slot) {
     const float4* a = reinterpret_cast<const float4*>(ap + 16 * i);
-    if constexpr (ACMI_FC4_PROBE & 1) {
-      av[slot][0] = make_float4(i, 1.f, 2.f, 3.f);
-      av[slot][1] = make_float4(i, 2.f, 1.f, 3.f);
-    } else {
-      av[slot][0] = a[0];
-      av[slot][1] = a[1];
-    }
+    av[slot][0] = a[0];
+    av[slot][1] = a[1];
     const uint4* b = bp + (long long)i * 16 * 128;
 #pragma unroll
     for (int t = 0; t < CT; ++t)
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt) {
-        if constexpr (ACMI_FC4_PROBE & 2) bv[slot][t][pt] = make_uint4(i, t, pt, lane);
-        else bv[slot][t][pt] = b[t * 128 + 64 * pt];
+        bv[slot][t][pt] = b[t * 128 + 64 * pt];
       }
   };
   f32x16 acc[CT];
@@ -127,8 +118,7 @@ void fc4_roll_kernel(const float* a3, long long lda, int B, int K, const char* w
 #pragma unroll
         for (int t = 0; t < CT; ++t) {
           const f16x8 b[2] = {as_f16x8(bv[sl][t][0]), as_f16x8(bv[sl][t][1])};
-          if constexpr (ACMI_FC4_PROBE & 4) acc[t][0] += (float)a[0][0] * (float)b[1][1] + (float)a[1][2];
-          else acc[t] = mfma_x2(a, b, acc[t]);
+          acc[t] = mfma_x2(a, b, acc[t]);
         }
       }
     }

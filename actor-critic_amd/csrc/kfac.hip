@@ -309,9 +309,6 @@ __device__ __forceinline__ void gj_mfma32(f64x4 (&acc)[NB], FA a, FB b) {
       acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a(u, ar, 4 * s + ak), b(u, 4 * s + ak, ar), acc[u], 0, 0, 0);
 }
 
-#ifndef ACMI_GJ_PROBE  // timing probes (wrong results): 1 no tile updates, 2 no next-pivot blocks,
-#define ACMI_GJ_PROBE 0  // 4 no pivot inverse (sweeps), 8 next-pivot blocks stop after their loads
-#endif
 // block (m, 0): Pinv_{k+1} from M_k and Pinv_k
 __device__ void gj_next_pivot(const MatSet& s, double* ws, int step, int mi, double* lds) {
   const int np = s.np[mi];
@@ -339,10 +336,6 @@ __device__ void gj_next_pivot(const MatSet& s, double* ws, int step, int mi, dou
     oldv[u] = M[(long long)(nb + br + gj_lrow(u)) * np + nb + bc + gj_lcol()];
   }
   __syncthreads();
-  if constexpr (ACMI_GJ_PROBE & 8) {
-    if (Pv[0][0] == 12345.0) PIn[0] = Mr[1][1] + Cn[2][2] + oldv[0];
-    return;
-  }
   {  // the tile blocks' Rrow' = Pinv_k M_k[kb.., nb..]
     f64x4 acc[1];
     gj_mfma32(acc, [&](int, int i, int k) { return Pv[br + i][k]; }, [&](int, int k, int j) { return Mr[k][bc + j]; });
@@ -357,7 +350,7 @@ __device__ void gj_next_pivot(const MatSet& s, double* ws, int step, int mi, dou
     for (int r = 0; r < 4; ++r) P[br + gj_lrow(r)][bc + gj_lcol()] = oldv[r] - acc[0][r];
   }
   __syncthreads();
-  if constexpr (!(ACMI_GJ_PROBE & 4)) pivot_inverse(P, Q);
+  pivot_inverse(P, Q);
 #pragma unroll
   for (int u = 0; u < 4; ++u) PIn[(r0 + 8 * u) * GJB + c] = P[r0 + 8 * u][c];
 }
@@ -367,10 +360,9 @@ __device__ void gj_next_pivot(const MatSet& s, double* ws, int step, int mi, dou
 __global__ __launch_bounds__(256) void gj_step_kernel(MatSet s, double* ws, int step) {
   __shared__ double lds[kGjLds];
   if ((int)blockIdx.x < s.count) {
-    if constexpr (!(ACMI_GJ_PROBE & 2)) gj_next_pivot(s, ws, step, blockIdx.x, lds);
+    gj_next_pivot(s, ws, step, blockIdx.x, lds);
     return;
   }
-  if constexpr (ACMI_GJ_PROBE & 1) return;
   const int b = blockIdx.x - s.count;
   int mi = 0;
   while (mi + 1 < s.count && b >= s.tile0[mi + 1]) ++mi;
@@ -441,10 +433,6 @@ __global__ __launch_bounds__(256) void gj_step_kernel(MatSet s, double* ws, int 
     Rs[q][c] = rv[u];
   }
   __syncthreads();
-  if constexpr (ACMI_GJ_PROBE & 16) {  // tiles stop after their staging
-    if (Pv[1][1] == 12345.0) Mo[0] = Cs[2][2] + Rs[3][3] + old[0][0];
-    return;
-  }
   {  // Rrow' = Pinv_k M_k[kb.., j] in place of the pivot rows: wave w, columns 16 w ..
     f64x4 acc[2];  // row blocks 0, 16
     gj_mfma32(acc, [&](int u, int i, int k) { return Pv[16 * u + i][k]; },
@@ -467,10 +455,6 @@ __global__ __launch_bounds__(256) void gj_step_kernel(MatSet s, double* ws, int 
       for (int r = 0; r < 4; ++r) Rs[16 * u + gj_lrow(r)][cj] = v[u][r];
   }
   __syncthreads();
-  if constexpr (ACMI_GJ_PROBE & 32) {  // tiles stop after Rrow'
-    if (Pv[1][1] == 12345.0) Mo[0] = Cs[2][2] + Rs[3][3] + old[0][0];
-    return;
-  }
   f64x4 acc[4];  // Ccol Rrow' over the wave's quadrant
   gj_mfma32(acc, [&](int u, int i, int k) { return Cs[qr + 16 * (u >> 1) + i][k]; },
             [&](int u, int k, int j) { return Rs[k][qc + 16 * (u & 1) + j]; });

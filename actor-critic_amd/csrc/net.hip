@@ -446,16 +446,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void r
   const int n = blockIdx.x / kSplitParts, j = blockIdx.x - n * kSplitParts;
   float* sx = reinterpret_cast<float*>(lds + kSpImg);  // the tail's scratch in the a1 image
   int* s_action = reinterpret_cast<int*>(sx + 512 + kMaxHeads);
-#ifndef ACMI_SPLIT_PROBE  // timing probes (wrong results): 1 no tower part, 2 no tail
-#define ACMI_SPLIT_PROBE 0
-#endif
-  if constexpr (!(ACMI_SPLIT_PROBE & 2))
-    rollout_tail_body<NZ, true>(part, nz, b4, a4, a4_stride, B, wpi, bpi, wv, bv, A, logits, l_stride, value,
-                                v_stride, ta, sx, sx + 512, *s_action, reinterpret_cast<uint4*>(lds), n, j, pend);
+  rollout_tail_body<NZ, true>(part, nz, b4, a4, a4_stride, B, wpi, bpi, wv, bv, A, logits, l_stride, value,
+                              v_stride, ta, sx, sx + 512, *s_action, reinterpret_cast<uint4*>(lds), n, j, pend);
   __syncthreads();  // the image rows in LDS; the tail's scratch free again
-  if constexpr (!(ACMI_SPLIT_PROBE & 1))
-    tower_part_body<C3, H16>(j, nt.b1, nt.b2, nt.b3, nt.a1, nt.a2, nt.a3, nt.st, nt.prep, nt.m1, nt.m2, nt.m3, lds,
-                             n);
+  tower_part_body<C3, H16>(j, nt.b1, nt.b2, nt.b3, nt.a1, nt.a2, nt.a3, nt.st, nt.prep, nt.m1, nt.m2, nt.m3, lds, n);
 }
 // the split tower alone (small batches without a fused tail: step 0, the bootstrap
 // forward): part j loads the input rows 8j .. 8j+35 of image n

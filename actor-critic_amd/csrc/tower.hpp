@@ -356,10 +356,6 @@ struct TowB {
 };
 
 
-#ifndef ACMI_TOW_PROBE  // timing probes (wrong results): 1 stop after conv1, 2 after conv2, 4 no global
-#define ACMI_TOW_PROBE 0  // stores, 8 stop after the image load, 16 no conv1 epilogue, 32 no conv1 MFMAs,
-#endif                    // 64 conv1 without the weight loads' dependency
-
 // The tower of image `img` by one 256-thread block over the caller's LDS
 // (kTowLds + kTowScr bytes).  IMG_IN_LDS: the u8 image is already in the
 // image region (written there by the fused rollout tail's env step, which
@@ -414,19 +410,11 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
 #pragma unroll
     for (int i = 0; i < kTowDepth; ++i) bw.fetch(i, 0, lane, i);
     __syncthreads();
-    if constexpr (ACMI_TOW_PROBE & 8) {
-      if (tid == 0 && (unsigned char)imgL[7] == 255 && imgL[5000] == 3) a1g[img] = 1.f;
-      return;
-    }
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       if (s + kTowDepth < 16) bw.fetch(s + kTowDepth, 0, lane, (s + kTowDepth) % kTowSlots);
       f16x8 b[2];
       bw.get(s % kTowSlots, b);
-      if constexpr (ACMI_TOW_PROBE & 64) {  // probe: constant weights (no B dependency)
-        b[0] = f16x8{1, 1, 1, 1, 1, 1, 1, 1};
-        b[1] = b[0];
-      }
       const int koff = (s >> 1) * 336 + 16 * (s & 1);  // kernel row kh = s/2, kw half
       if (s == 8) {  // every pixel sums its K halves (k-steps 0-7) + (8-15): the split tower's partition
 #pragma unroll
@@ -440,10 +428,6 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       for (int u = 0; u < 4; ++u) {
         if (u == 3 && (w < 2 || (s >> 3) != w - 2)) continue;
         const f16x8 a = u8x8_to_f16(*reinterpret_cast<const uint2*>(imgL + abase[u] + koff));
-        if constexpr (ACMI_TOW_PROBE & 32) {  // probe: no MFMAs (the operands kept live)
-          acc[u][s & 15] += (float)a[s & 7] + (float)b[0][s & 7];
-          continue;
-        }
         if constexpr (!H16) acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[1], acc[u], 0, 0, 0);
         acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[0], acc[u], 0, 0, 0);
       }
@@ -459,13 +443,9 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     // row R of row tile T (pixel 32 T + tow_row(R, lane))
     auto emit1 = [&](auto RC, int T, float v) -> unsigned long long {
       constexpr int R = decltype(RC)::value;
-      if constexpr (ACMI_TOW_PROBE & 16) {  // probe: no conv1 epilogue (one store keeps acc live)
-        if (v == 12345.f) g.store(T, v);
-        return 0;
-      }
       v = fmaxf(__builtin_fmaf(v, inv1, bias), 0.f);
       tow1_put<R>(a1L, T, ad, v, sa1);
-      if constexpr (!(ACMI_TOW_PROBE & 4)) g.store_imm<tow1_roff<R>()>(T * 4096 + ad.go, v);
+      g.store_imm<tow1_roff<R>()>(T * 4096 + ad.go, v);
       return __ballot(v > 0.f);
     };
     // the tile's ReLU' words gathered by v_writelane (lane j: the tile's row j) and
@@ -477,7 +457,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
         constexpr int r = decltype(R)::value;
         mw = tow_mword<r>(mw, emit1(R, tile_of(u), h0[u][r] + acc[u][r]));
       });
-      if (!(ACMI_TOW_PROBE & 4) && mg && lane < 32) mg[32 * tile_of(u) + lane] = mw;
+      if (mg && lane < 32) mg[32 * tile_of(u) + lane] = mw;
     }
     float* scr12 = reinterpret_cast<float*>(lds + kTowLds);  // [16 rows][32]
     if (w == 3) {
@@ -493,14 +473,10 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
         const int m = tow_row(r, lane);
         mw = tow_mword<r>(mw, emit1(R, 12, acc[3][r] + scr12[m * 32 + col]));
       });
-      if (!(ACMI_TOW_PROBE & 4) && mg && lane < 16) mg[384 + lane] = mw;
+      if (mg && lane < 16) mg[384 + lane] = mw;
     }
   }
   __syncthreads();
-  if constexpr (ACMI_TOW_PROBE & 1) {
-    if (tid == 0 && a1L[5] == 3 && a1L[333] == 4) a1g[img] = 1.f;
-    return;
-  }
 
   // ---- conv2: a1 -> a2 [9][9][64] ------------------------------------------------
   {
@@ -569,7 +545,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
       v = fmaxf(__builtin_fmaf(v, inv2, bias), 0.f);
       if (act) {
         tow2_put<R>(imgL, T, ad, v, sa2);
-        if constexpr (!(ACMI_TOW_PROBE & 4)) g.store_imm<tow2_roff<R>()>(T * 8192 + ad.go, v);
+        g.store_imm<tow2_roff<R>()>(T * 8192 + ad.go, v);
       }
       return __ballot(act && v > 0.f);
     };
@@ -579,7 +555,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
         constexpr int r = decltype(R)::value;
         mw = tow_mword<r>(mw, emit(R, rtf, hF[r] + accF[r], true));
       });
-      if (!(ACMI_TOW_PROBE & 4) && mg && lane < 32) mg[2 * (32 * rtf + lane) + ct] = mw;
+      if (mg && lane < 32) mg[2 * (32 * rtf + lane) + ct] = mw;
     }
     if (wave < 2) {  // rows 64..80: r < 8 on every lane, r = 8 (row 80) on the lower half
       uint32_t mw = 0;
@@ -589,14 +565,10 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
         const bool act = m < 17;
         mw = tow_mword<r>(mw, emit(R, 2, act ? accH[r] + scr[(ct * 17 + m) * 32 + col] : 0.f, act));
       });
-      if (!(ACMI_TOW_PROBE & 4) && mg && lane < 17) mg[2 * (64 + lane) + ct] = mw;
+      if (mg && lane < 17) mg[2 * (64 + lane) + ct] = mw;
     }
   }
   __syncthreads();
-  if constexpr (ACMI_TOW_PROBE & 2) {
-    if (tid == 0 && imgL[5] == 3 && imgL[333] == 4) a1g[img] = 1.f;
-    return;
-  }
 
   // ---- conv3: a2 -> a3 [7][7][C3] -------------------------------------------------
   {
@@ -644,7 +616,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
     // (act: the lane's row exists; the ballot runs on every lane)
     auto emit3 = [&](int p, float v, bool act) -> unsigned long long {
       v = fmaxf(__builtin_fmaf(v, inv3, bias), 0.f);
-      if (!(ACMI_TOW_PROBE & 4) && act) g[p * C3 + c] = v;
+      if (act) g[p * C3 + c] = v;
       return __ballot(act && v > 0.f);
     };
     // rows 32 rt + tow_row(r, lane) < 49: row tile 0 all 16 r; row tile 1 r < 8 on
@@ -665,7 +637,7 @@ __device__ __forceinline__ void tower_body(const uint8_t* obs, long long img_str
           mw = tow_mword<r>(mw, emit3(p, act ? get(r) : 0.f, act));
         });
       }
-      if (!(ACMI_TOW_PROBE & 4) && mg && lane < (rt ? 17 : 32)) mg[(32 * rt + lane) * (C3 / 32) + ct] = mw;
+      if (mg && lane < (rt ? 17 : 32)) mg[(32 * rt + lane) * (C3 / 32) + ct] = mw;
     };
     if constexpr (C3 == 32) {  // the second K half (waves 2, 3) through LDS to the first
       float* scr = reinterpret_cast<float*>(a1L);  // [rt][32 rows][32]
