@@ -6,6 +6,7 @@ critical path is read here.  The rollout's per-step kernels are folded into one
 line per kernel name.
 
   python scripts/iter_timeline.py <kernel_trace.csv> [iteration index] > timeline.md
+  python scripts/iter_timeline.py <kernel_trace.csv> band   (the band launches by shape)
 """
 import collections
 import csv
@@ -38,5 +39,23 @@ def main(path, it=4):
     print('\niteration span: %.1f us' % end)
 
 
+def band_by_grid(path, warm=2):
+    """The band reductions by launch shape (conv2 and conv3 share `band_kernel`, the stats
+    summary averages them together): mean duration over all launches and after the
+    first `warm` (the bench's warm-up iterations)."""
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r['Start_Timestamp']))
+    d = collections.OrderedDict()
+    for r in rows:
+        if 'band_kernel' in r['Kernel_Name']:
+            d.setdefault(r['Grid_Size_X'], []).append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
+    print('| band launch (grid threads) | launches | mean us | mean us after %d |' % warm)
+    print('|---|---|---|---|')
+    for g, v in d.items():
+        print('| %s | %d | %.1f | %.1f |' % (g, len(v), sum(v) / len(v), sum(v[warm:]) / max(1, len(v[warm:]))))
+
+
 if __name__ == '__main__':
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 4)
+    if len(sys.argv) > 2 and sys.argv[2] == 'band':
+        band_by_grid(sys.argv[1])
+    else:
+        main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 4)
